@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident srtp_protect() throughput on MI355X.
+
+Workload (BASELINE.json configs[1], the headline): AES-128-ICM + HMAC-SHA1-80
+protect, one stream (SSRC 0xcafebabe), 2^20 packets x 1400-byte payload
+(1412-byte RTP packets -> 1422-byte SRTP packets) resident in HBM.  One step
+= srtp_protect_device() over the whole batch: header parse, the in-order
+index / replay / key-limit pre-pass, and the HIP crypto kernels, in place.
+Before each step the 16-bit sequence numbers are advanced on the device (a
+new batch of packets, as a sender would produce; replay protection would
+otherwise reject a repeated index).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config icm128|gcm256|g711]
+
+Multi-GPU: one process per GPU (torch.distributed.run), each rank protects
+its own 2^20-packet batch of its own stream (weak scaling; no data-path
+collective: every rank derives identical session keys from the policy, so
+there is nothing to broadcast).  value = all ranks' packets / max rank time.
+
+Extra fields: roofline (dominant kernel, HIP-event timed on the stream the
+kernels ran on), cpu_baseline (the reference, cisco/libsrtp built from its
+own sources, srtp_protect() per packet on host threads, rank 0 only).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (cipher policy dict, payload bytes, packets per GPU, tag bytes)
+    "icm128": (dict(cipher_type=1, cipher_key_len=30, auth_type=3,
+                    auth_key_len=20, auth_tag_len=10, sec_serv=3), 1400,
+               1 << 20, 10),
+    "gcm256": (dict(cipher_type=7, cipher_key_len=44, auth_type=0,
+                    auth_key_len=0, auth_tag_len=16, sec_serv=3), 1400,
+               1 << 20, 16),
+    "g711": (dict(cipher_type=1, cipher_key_len=30, auth_type=3,
+                  auth_key_len=20, auth_tag_len=10, sec_serv=3), 160,
+             1 << 23, 10),
+}
+WORKLOAD = {
+    "icm128": "AES-128-ICM + HMAC-SHA1-80 protect, 1M packets x 1400B, 1 stream",
+    "gcm256": "AES-256-GCM-16 protect, 1M packets x 1400B per GPU, 1 stream",
+    "g711": "AES-128-ICM + HMAC-SHA1-80 protect, 8M packets x 160B, 1 stream",
+}
+# master key: test/srtp_driver.c test_key (46 bytes) -- any key works
+TEST_KEY = ("e1f97a0d3e018be0d64fa32c06de41390ec675ad498afeebb6960b3aabe6"
+            "c173c317f2dabe357793b6960b3aabe6")
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="icm128", choices=sorted(CONFIGS))
+    ap.add_argument("--packets", type=int, default=0,
+                    help="override packets per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target wall time of the CPU-baseline sample")
+    ap.add_argument("--pmc-traffic", default="",
+                    help="rocprofv3 --pmc counter_collection.csv to report "
+                         "roofline.traffic from (FETCH_SIZE/WRITE_SIZE)")
+    return ap.parse_args()
+
+
+def pmc_traffic(path, kernel_substr):
+    """HBM bytes per launch of the dominant kernel from a rocprofv3 --pmc
+    CSV holding FETCH_SIZE and WRITE_SIZE (KB).  gfx950 correction
+    (MI355X_MICROARCH.md HBM section): FETCH_SIZE reports half of a wide
+    streaming read -> doubled; WRITE_SIZE exact for 16-B stores."""
+    import csv
+    if not path or not os.path.exists(path):
+        return None
+    fetch, write, nf, nw = 0.0, 0.0, 0, 0
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr not in row.get("Kernel_Name", ""):
+                continue
+            name = row.get("Counter_Name", "")
+            val = float(row.get("Counter_Value", 0) or 0)
+            if name == "FETCH_SIZE":
+                fetch += val
+                nf += 1
+            elif name == "WRITE_SIZE":
+                write += val
+                nw += 1
+    if not nf or not nw:
+        return None
+    return (2.0 * fetch / nf + write / nw) * 1024.0
+
+
+def cpu_baseline(cfg, payload, seconds):
+    """The reference on the host: srtp_protect() per packet, one srtp_t per
+    thread (oracle/bench_ref.c over oracle/_ref/libsrtp_ref_*.so)."""
+    gcm = cfg == "gcm256"
+    lib = os.path.join(ROOT, "oracle", "_ref",
+                       "bench_ref_ossl.so" if gcm else "bench_ref_int.so")
+    if not os.path.exists(lib):
+        return None
+    L = C.CDLL(lib)
+    L.ref_bench.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int,
+                            C.POINTER(C.c_double)]
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    secs = C.c_double()
+    # calibrate on one thread, then size the sample to ~`seconds`
+    n = L.ref_bench(1, 2000, payload, int(gcm), C.byref(secs))
+    per_thread_rate = n / max(secs.value, 1e-6)
+    per_thread = int(per_thread_rate * seconds)
+    done = L.ref_bench(threads, per_thread, payload, int(gcm), C.byref(secs))
+    kind = "reference"
+    backend = "OpenSSL 3 backend (AES-GCM)" if gcm else "internal crypto kernel"
+    return {"value": done / secs.value, "unit": "pkt/s", "cores": threads,
+            "kind": kind,
+            "sample": "%d x srtp_protect() of %d-byte payloads, %d threads x "
+                      "1 srtp_t, cisco/libsrtp 3.0.0 %s built from source"
+                      % (done, payload, threads, backend),
+            "payload_GBps": done * payload / secs.value / 1e9}
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(0)
+    import libsrtp_amd as L
+
+    pol, payload, npk, tag = CONFIGS[a.config]
+    n = a.packets or npk
+    ssrc = 0xcafebabe ^ rank
+    policy = dict(pol, ssrc_type=1, ssrc=ssrc, window_size=128,
+                  allow_repeat_tx=0, keys=[TEST_KEY])
+    sess = L.Session([policy])
+
+    # packet arena in HBM: slot = roundup16(rtp_len + tag)
+    rtp_len = 12 + payload
+    slot = (rtp_len + tag + 15) & ~15
+    dev = torch.device("cuda", torch.cuda.current_device())
+    g = torch.Generator(device=dev).manual_seed(0x5352545030303031 & 0x7fffffff)
+    arena = torch.randint(0, 256, (n, slot), dtype=torch.uint8, device=dev,
+                          generator=g)
+    arena[:, 0] = 0x80
+    arena[:, 1] = 96
+    arena[:, 4:8] = 0
+    arena[:, 8:12] = torch.tensor(list(ssrc.to_bytes(4, "big")),
+                                  dtype=torch.uint8, device=dev)
+    flat = arena.view(-1)
+    off = torch.arange(n, dtype=torch.int64, device=dev) * slot
+    in_len = torch.full((n,), rtp_len, dtype=torch.int32, device=dev)
+    out_len = torch.empty(n, dtype=torch.int32, device=dev)
+    status = torch.empty(n, dtype=torch.int32, device=dev)
+    idx = torch.arange(n, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    sess.set_timing(True)
+
+    seq_base = [0x1234]
+
+    def step():
+        seq = (idx + seq_base[0]) & 0xffff
+        arena[:, 2] = (seq >> 8).to(torch.uint8)
+        arena[:, 3] = (seq & 0xff).to(torch.uint8)
+        out_len.fill_(slot)
+        seq_base[0] += n
+        st = sess.protect_device(flat, off, in_len, flat, off, out_len,
+                                 status, stream=stream)
+        if st != 0:
+            raise RuntimeError("srtp_protect_device: %s" % st)
+        return sess.last_kernel_ms()
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    bad = int((status != 0).sum())
+    if bad:
+        raise RuntimeError("%d packets failed in warmup" % bad)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = []
+    for _ in range(a.steps):
+        kms.append(step())
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t[0])
+    assert int((status != 0).sum()) == 0
+
+    total_pk = n * a.steps * world
+    value = total_pk / dt
+    kernel_ms = sum(kms) / len(kms)
+    algo_bytes = n * (rtp_len + rtp_len + tag)   # read rtp + write srtp
+    achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
+    kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
+    traffic = pmc_traffic(a.pmc_traffic, kname)
+    if rank != 0:
+        return
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(a.config, payload, a.cpu_seconds)
+    out = {
+        "metric": "SRTP packets/sec + payload GB/s, device-resident, "
+                  "1M×1400B batch",
+        "value": value,
+        "unit": "pkt/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (random payloads, seq advanced per step)",
+        "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": n,
+                   "payload_bytes": payload, "rtp_bytes": rtp_len,
+                   "srtp_bytes": rtp_len + tag, "parallelism": "dp%d" % world},
+        "payload_GBps": value * payload / 1e9,
+        "roofline": {"bound": "hbm", "achieved": achieved,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": traffic,
+                     "kernel": kname, "kernel_ms": kernel_ms,
+                     "algorithmic_bytes_per_launch": algo_bytes},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

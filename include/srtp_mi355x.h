@@ -1,0 +1,353 @@
+/*
+ * srtp_mi355x.h -- C ABI of libsrtp_mi355x, an MI355X (gfx950) SRTP engine.
+ *
+ * Drop-in surface: every declaration in the first half keeps the name,
+ * signature, struct layout and enum values of cisco/libsrtp 3.0.0's public
+ * header (include/srtp.h; symbol list srtp.def:1-69), so C code written
+ * against libsrtp compiles and links against this library unchanged.  Each
+ * group cites the reference declaration it replaces.
+ *
+ * The second half adds the batch extension that the throughput path uses:
+ * many packets per call, either from host buffers or already resident in
+ * device memory (HBM).  Per-packet semantics -- status codes, replay and
+ * index handling, key-usage limits, events, output layout -- are exactly
+ * those of calling srtp_protect()/srtp_unprotect() once per packet in array
+ * order.
+ *
+ * All packet cryptography (AES-ICM, HMAC-SHA1, AES-GCM) runs in HIP kernels
+ * on the GPU; there is no CPU crypto fallback.  Calls fail with
+ * srtp_err_status_init_fail when no GPU is present.
+ */
+#ifndef SRTP_MI355X_H
+#define SRTP_MI355X_H
+
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants: include/srtp.h:62-116 ----------------------------------- */
+#define SRTP_MASTER_KEY_LEN 30
+#define SRTP_MAX_KEY_LEN 64
+#define SRTP_MAX_TAG_LEN 16
+#define SRTP_MAX_MKI_LEN 128
+#define SRTP_MAX_TRAILER_LEN (SRTP_MAX_TAG_LEN + SRTP_MAX_MKI_LEN)
+#define SRTP_SRCTP_INDEX_LEN 4
+#define SRTP_MAX_SRTCP_TRAILER_LEN \
+    (SRTP_SRCTP_INDEX_LEN + SRTP_MAX_TAG_LEN + SRTP_MAX_MKI_LEN)
+#define SRTP_MAX_NUM_MASTER_KEYS 16
+#define SRTP_SALT_LEN 14
+#define SRTP_AEAD_SALT_LEN 12
+#define SRTP_AES_128_KEY_LEN 16
+#define SRTP_AES_192_KEY_LEN 24
+#define SRTP_AES_256_KEY_LEN 32
+#define SRTP_AES_ICM_128_KEY_LEN_WSALT (SRTP_SALT_LEN + SRTP_AES_128_KEY_LEN)
+#define SRTP_AES_ICM_192_KEY_LEN_WSALT (SRTP_SALT_LEN + SRTP_AES_192_KEY_LEN)
+#define SRTP_AES_ICM_256_KEY_LEN_WSALT (SRTP_SALT_LEN + SRTP_AES_256_KEY_LEN)
+#define SRTP_AES_GCM_128_KEY_LEN_WSALT (SRTP_AEAD_SALT_LEN + SRTP_AES_128_KEY_LEN)
+#define SRTP_AES_GCM_192_KEY_LEN_WSALT (SRTP_AEAD_SALT_LEN + SRTP_AES_192_KEY_LEN)
+#define SRTP_AES_GCM_256_KEY_LEN_WSALT (SRTP_AEAD_SALT_LEN + SRTP_AES_256_KEY_LEN)
+
+/* cipher / auth type ids: crypto/include/crypto_types.h:55-114 */
+#define SRTP_NULL_CIPHER 0
+#define SRTP_AES_ICM_128 1
+#define SRTP_AES_ICM_192 4
+#define SRTP_AES_ICM_256 5
+#define SRTP_AES_GCM_128 6
+#define SRTP_AES_GCM_256 7
+#define SRTP_NULL_AUTH 0
+#define SRTP_HMAC_SHA1 3
+
+typedef uint32_t srtp_cipher_type_id_t;
+typedef uint32_t srtp_auth_type_id_t;
+
+/* ---- error codes: include/srtp.h:183-220 (values are ABI) --------------- */
+typedef enum {
+    srtp_err_status_ok = 0,
+    srtp_err_status_fail = 1,
+    srtp_err_status_bad_param = 2,
+    srtp_err_status_alloc_fail = 3,
+    srtp_err_status_dealloc_fail = 4,
+    srtp_err_status_init_fail = 5,
+    srtp_err_status_terminus = 6,
+    srtp_err_status_auth_fail = 7,
+    srtp_err_status_cipher_fail = 8,
+    srtp_err_status_replay_fail = 9,
+    srtp_err_status_replay_old = 10,
+    srtp_err_status_algo_fail = 11,
+    srtp_err_status_no_such_op = 12,
+    srtp_err_status_no_ctx = 13,
+    srtp_err_status_cant_check = 14,
+    srtp_err_status_key_expired = 15,
+    srtp_err_status_socket_err = 16,
+    srtp_err_status_signal_err = 17,
+    srtp_err_status_nonce_bad = 18,
+    srtp_err_status_read_fail = 19,
+    srtp_err_status_write_fail = 20,
+    srtp_err_status_parse_err = 21,
+    srtp_err_status_encode_err = 22,
+    srtp_err_status_semaphore_err = 23,
+    srtp_err_status_pfkey_err = 24,
+    srtp_err_status_bad_mki = 25,
+    srtp_err_status_pkt_idx_old = 26,
+    srtp_err_status_pkt_idx_adv = 27,
+    srtp_err_status_buffer_small = 28,
+    srtp_err_status_cryptex_err = 29
+} srtp_err_status_t;
+
+/* ---- policy types: include/srtp.h:222-358 ------------------------------- */
+typedef struct srtp_ctx_t_ srtp_ctx_t;
+typedef srtp_ctx_t *srtp_t;
+
+typedef enum {
+    sec_serv_none = 0,
+    sec_serv_conf = 1,
+    sec_serv_auth = 2,
+    sec_serv_conf_and_auth = 3
+} srtp_sec_serv_t;
+
+typedef struct srtp_crypto_policy_t {
+    srtp_cipher_type_id_t cipher_type;
+    size_t cipher_key_len;
+    srtp_auth_type_id_t auth_type;
+    size_t auth_key_len;
+    size_t auth_tag_len;
+    srtp_sec_serv_t sec_serv;
+} srtp_crypto_policy_t;
+
+typedef enum {
+    ssrc_undefined = 0,
+    ssrc_specific = 1,
+    ssrc_any_inbound = 2,
+    ssrc_any_outbound = 3
+} srtp_ssrc_type_t;
+
+typedef struct {
+    srtp_ssrc_type_t type;
+    uint32_t value;
+} srtp_ssrc_t;
+
+typedef struct srtp_master_key_t {
+    uint8_t *key;
+    uint8_t *mki_id;
+} srtp_master_key_t;
+
+typedef struct srtp_policy_t {
+    srtp_ssrc_t ssrc;
+    srtp_crypto_policy_t rtp;
+    srtp_crypto_policy_t rtcp;
+    uint8_t *key;
+    srtp_master_key_t **keys;
+    size_t num_master_keys;
+    bool use_mki;
+    size_t mki_size;
+    size_t window_size;
+    bool allow_repeat_tx;
+    uint8_t *enc_xtn_hdr;
+    size_t enc_xtn_hdr_count;
+    bool use_cryptex;
+    struct srtp_policy_t *next;
+} srtp_policy_t;
+
+/* SRTP profiles, include/srtp.h:1010-1040 */
+typedef enum {
+    srtp_profile_reserved = 0,
+    srtp_profile_aes128_cm_sha1_80 = 1,
+    srtp_profile_aes128_cm_sha1_32 = 2,
+    srtp_profile_null_sha1_80 = 5,
+    srtp_profile_null_sha1_32 = 6,
+    srtp_profile_aead_aes_128_gcm = 7,
+    srtp_profile_aead_aes_256_gcm = 8
+} srtp_profile_t;
+
+/* events, include/srtp.h:1290-1352 */
+typedef enum {
+    event_ssrc_collision,
+    event_key_soft_limit,
+    event_key_hard_limit,
+    event_packet_index_limit
+} srtp_event_t;
+
+typedef struct srtp_stream_ctx_t_ srtp_stream_ctx_t;
+typedef srtp_stream_ctx_t *srtp_stream_t;
+
+typedef struct srtp_event_data_t {
+    srtp_t session;
+    uint32_t ssrc;
+    srtp_event_t event;
+} srtp_event_data_t;
+
+typedef void(srtp_event_handler_func_t)(srtp_event_data_t *data);
+
+typedef enum {
+    srtp_log_level_error,
+    srtp_log_level_warning,
+    srtp_log_level_info,
+    srtp_log_level_debug
+} srtp_log_level_t;
+
+typedef void(srtp_log_handler_func_t)(srtp_log_level_t level,
+                                      const char *msg,
+                                      void *data);
+
+/* ---- lifecycle: include/srtp.h:380-387, 512-604, 1001 ------------------- */
+srtp_err_status_t srtp_init(void);
+srtp_err_status_t srtp_shutdown(void);
+srtp_err_status_t srtp_create(srtp_t *session, const srtp_policy_t *policy);
+srtp_err_status_t srtp_stream_add(srtp_t session, const srtp_policy_t *policy);
+srtp_err_status_t srtp_stream_remove(srtp_t session, uint32_t ssrc);
+srtp_err_status_t srtp_update(srtp_t session, const srtp_policy_t *policy);
+srtp_err_status_t srtp_stream_update(srtp_t session,
+                                     const srtp_policy_t *policy);
+srtp_err_status_t srtp_dealloc(srtp_t s);
+srtp_stream_ctx_t *srtp_get_stream(srtp_t srtp, uint32_t ssrc);
+
+/* ---- per-packet hot path: include/srtp.h:433-438, 485-489 --------------- */
+srtp_err_status_t srtp_protect(srtp_t ctx,
+                               const uint8_t *rtp,
+                               size_t rtp_len,
+                               uint8_t *srtp,
+                               size_t *srtp_len,
+                               size_t mki_index);
+srtp_err_status_t srtp_unprotect(srtp_t ctx,
+                                 const uint8_t *srtp,
+                                 size_t srtp_len,
+                                 uint8_t *rtp,
+                                 size_t *rtp_len);
+
+/* ---- crypto policy setters: include/srtp.h:625-984 ---------------------- */
+void srtp_crypto_policy_set_rtp_default(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_rtcp_default(srtp_crypto_policy_t *p);
+/* include/srtp.h:661-662: an alias of the RTP default */
+#define srtp_crypto_policy_set_aes_cm_128_hmac_sha1_80(p) \
+    srtp_crypto_policy_set_rtp_default(p)
+void srtp_crypto_policy_set_aes_cm_128_hmac_sha1_32(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_128_null_auth(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_null_cipher_hmac_sha1_80(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_null_cipher_hmac_null(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_256_hmac_sha1_80(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_256_hmac_sha1_32(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_256_null_auth(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_192_hmac_sha1_80(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_192_hmac_sha1_32(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_cm_192_null_auth(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_gcm_128_16_auth(srtp_crypto_policy_t *p);
+void srtp_crypto_policy_set_aes_gcm_256_16_auth(srtp_crypto_policy_t *p);
+
+/* ---- profiles / keys: include/srtp.h:1042-1100 -------------------------- */
+srtp_err_status_t srtp_crypto_policy_set_from_profile_for_rtp(
+    srtp_crypto_policy_t *policy, srtp_profile_t profile);
+srtp_err_status_t srtp_crypto_policy_set_from_profile_for_rtcp(
+    srtp_crypto_policy_t *policy, srtp_profile_t profile);
+size_t srtp_profile_get_master_key_length(srtp_profile_t profile);
+size_t srtp_profile_get_master_salt_length(srtp_profile_t profile);
+void srtp_append_salt_to_key(uint8_t *key,
+                             size_t bytes_in_key,
+                             uint8_t *salt,
+                             size_t bytes_in_salt);
+
+/* ---- RTCP: include/srtp.h:1162-1216 (not on the GPU path yet: returns
+ *      srtp_err_status_no_such_op; see DESIGN.md "Out of scope") ----------- */
+srtp_err_status_t srtp_protect_rtcp(srtp_t ctx,
+                                    const uint8_t *rtcp,
+                                    size_t rtcp_len,
+                                    uint8_t *srtcp,
+                                    size_t *srtcp_len,
+                                    size_t mki_index);
+srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx,
+                                      const uint8_t *srtcp,
+                                      size_t srtcp_len,
+                                      uint8_t *rtcp,
+                                      size_t *rtcp_len);
+
+/* ---- misc: include/srtp.h:1240-1480 ------------------------------------- */
+void srtp_set_user_data(srtp_t ctx, void *data);
+void *srtp_get_user_data(srtp_t ctx);
+srtp_err_status_t srtp_install_event_handler(srtp_event_handler_func_t func);
+const char *srtp_get_version_string(void);
+unsigned int srtp_get_version(void);
+srtp_err_status_t srtp_set_debug_module(const char *mod_name, bool v);
+srtp_err_status_t srtp_list_debug_modules(void);
+srtp_err_status_t srtp_install_log_handler(srtp_log_handler_func_t func,
+                                           void *data);
+srtp_err_status_t srtp_get_protect_trailer_length(srtp_t session,
+                                                  size_t mki_index,
+                                                  size_t *length);
+srtp_err_status_t srtp_get_protect_rtcp_trailer_length(srtp_t session,
+                                                       size_t mki_index,
+                                                       size_t *length);
+srtp_err_status_t srtp_stream_set_roc(srtp_t session,
+                                      uint32_t ssrc,
+                                      uint32_t roc);
+srtp_err_status_t srtp_stream_get_roc(srtp_t session,
+                                      uint32_t ssrc,
+                                      uint32_t *roc);
+
+/* ======================================================================
+ * Batch extension (new).  Semantics == a loop of single-packet calls.
+ * ====================================================================== */
+
+/*
+ * Host buffers.  Packet i is rtp[i] (rtp_len[i] bytes); its result goes to
+ * srtp[i] whose capacity is srtp_len[i] on input and whose length is stored
+ * there on success.  srtp[i] may equal rtp[i] (in place).  mki_index may be
+ * NULL (all zero).  status[i] receives the per-packet result; the return
+ * value is srtp_err_status_ok unless the batch itself could not run.
+ */
+srtp_err_status_t srtp_protect_batch(srtp_t ctx,
+                                     size_t n,
+                                     const uint8_t *const *rtp,
+                                     const size_t *rtp_len,
+                                     uint8_t *const *srtp,
+                                     size_t *srtp_len,
+                                     const size_t *mki_index,
+                                     srtp_err_status_t *status);
+srtp_err_status_t srtp_unprotect_batch(srtp_t ctx,
+                                       size_t n,
+                                       const uint8_t *const *srtp,
+                                       const size_t *srtp_len,
+                                       uint8_t *const *rtp,
+                                       size_t *rtp_len,
+                                       srtp_err_status_t *status);
+
+/*
+ * Device-resident batch: every pointer below except mki_index is a device
+ * (HBM) pointer.  Packet i occupies in[in_off[i] .. +in_len[i]); in_off[i]
+ * must be 16-byte aligned and the arena readable up to
+ * in_off[i] + roundup16(in_len[i]).  Output goes to out + out_off[i] (may be
+ * the same bytes as the input: in place) with capacity out_len[i]; on
+ * success out_len[i] is overwritten with the output length.  status[i] is an
+ * int32 srtp_err_status_t.  `stream` is a hipStream_t (NULL: the session's
+ * own stream); the call returns after the batch has completed.
+ */
+typedef struct srtp_device_batch_t {
+    size_t n;
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint32_t *out_len;
+    int32_t *status;
+    const uint8_t *mki_index; /* HOST array, protect only; may be NULL */
+    void *stream;
+} srtp_device_batch_t;
+
+srtp_err_status_t srtp_protect_device(srtp_t ctx, const srtp_device_batch_t *b);
+srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
+                                        const srtp_device_batch_t *b);
+
+/* Instrumentation for bench.py: device time (ms) of the crypto kernels of
+ * the last batch, measured with HIP events on the stream they ran on. */
+void srtp_mi355x_set_timing(srtp_t ctx, int on);
+double srtp_mi355x_last_kernel_ms(srtp_t ctx);
+/* 1 when a HIP device is usable from this process */
+int srtp_mi355x_gpu_available(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SRTP_MI355X_H */

@@ -1,0 +1,133 @@
+/*
+ * srtp_dev.h -- layouts shared by the host protocol engine (C) and the HIP
+ * kernels, plus the thin extern "C" FFI the C host calls.
+ *
+ * Data layout in HBM (see DESIGN.md "Data layout"):
+ *   key table   : srtp_dev_key_t[nkeys]  one 512-byte slot per session key
+ *                 (round keys, salt, HMAC midstates, MKI, GHASH table index)
+ *   ghash table : 4 KiB per GCM key: M[b] = b(x)*H for every byte b
+ *   packet arena: caller bytes; packet i at in_off[i] (16-byte aligned,
+ *                 readable up to in_off + roundup16(len))
+ *   meta        : srtp_dev_meta_t[n] written by the pre-pass
+ */
+#ifndef SRTP_DEV_H
+#define SRTP_DEV_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cipher families as the kernels see them */
+enum {
+    SRTP_DEV_NULL = 0,
+    SRTP_DEV_ICM = 1,
+    SRTP_DEV_GCM = 2
+};
+
+typedef struct srtp_dev_key {
+    uint32_t rk[60];    /* AES round keys, little-endian words of the bytes */
+    uint32_t salt[4];   /* ICM: 14-byte salt || 00 00; GCM: 12-byte salt   */
+    uint32_t ipad[5];   /* SHA-1 state after (K ^ ipad)                      */
+    uint32_t opad[5];   /* SHA-1 state after (K ^ opad)                      */
+    uint32_t rounds;    /* 10 / 12 / 14, 0 for the null cipher              */
+    uint32_t family;    /* SRTP_DEV_*                                        */
+    uint32_t auth;      /* 1 = HMAC-SHA1 computed, 0 = none                  */
+    uint32_t tag_len;   /* bytes of tag on the wire                          */
+    uint32_t mki_size;  /* bytes of MKI on the wire (0 if not used)          */
+    uint32_t conf;      /* 1 = payload encrypted (sec_serv_conf)             */
+    uint32_t ghash_slot;/* index into the GHASH table arena (GCM only)       */
+    uint32_t pad0;
+    uint32_t h[4];      /* GCM hash subkey E_K(0^128), big-endian words      */
+    uint8_t mki[128];
+    uint32_t pad1[10];
+} srtp_dev_key_t;
+
+/* per-packet work descriptor written by the pre-pass */
+typedef struct srtp_dev_meta {
+    uint32_t key;   /* key slot                                              */
+    uint32_t roc;   /* rollover counter of the estimated index               */
+    uint32_t info;  /* [15:0] enc_start, [23:16] status (0 = run crypto),
+                       [31:24] kernel variant (SRTP_VARIANT)                 */
+    uint32_t len;   /* bytes authenticated / encrypted region end            */
+} srtp_dev_meta_t;
+
+#define SRTP_META_ENC_START(i) ((i) & 0xffffu)
+#define SRTP_META_STATUS(i) (((i) >> 16) & 0xffu)
+#define SRTP_META_VARIANT(i) (((i) >> 24) & 0xffu)
+/* kernel variant id: family*8 + rounds_code*2 + auth, rounds_code 0 null,
+ * 1 AES-128, 2 AES-192, 3 AES-256 */
+#define SRTP_VARIANT(fam, rc, au) ((uint32_t)((fam) * 8 + (rc) * 2 + (au)))
+
+/* compact header summary produced by the device parse kernel */
+typedef struct srtp_dev_hdr {
+    uint32_t ssrc;      /* big-endian numeric value                          */
+    uint32_t seq_len;   /* [15:0] seq, [31:16] reserved                      */
+    uint32_t enc_start; /* header length incl. extension, or error code<<24 */
+    uint32_t len;       /* packet length                                     */
+} srtp_dev_hdr_t;
+
+/* ---- thin FFI implemented in HIP (srtp_gpu.hip) ----------------------- */
+
+typedef struct srtp_gpu srtp_gpu_t;
+
+int srtp_gpu_open(srtp_gpu_t **g);
+void srtp_gpu_close(srtp_gpu_t *g);
+int srtp_gpu_available(void);
+const char *srtp_gpu_last_error(void);
+
+/* key table (device copy of srtp_dev_key_t, grown on demand) */
+int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
+                     const uint32_t *ghash_tab /* 1024 words or NULL */);
+
+/* One pass over a batch in device memory.  Packets whose meta status is
+ * non-zero are skipped.  For unprotect, auth_ok[i] receives 1 when the tag
+ * verified.  op: 0 protect, 1 unprotect.  Asynchronous on the g's stream
+ * unless `stream` is non-NULL (a hipStream_t). */
+typedef struct srtp_gpu_batch {
+    size_t n;
+    const uint8_t *in;      /* device arena */
+    const uint64_t *in_off; /* device */
+    uint8_t *out;           /* device arena (may equal in) */
+    const uint64_t *out_off;/* device */
+    const srtp_dev_meta_t *meta; /* device */
+    uint8_t *auth_ok;       /* device, unprotect only */
+    uint32_t uniform_key;   /* slot when every packet uses one key, else ~0 */
+    uint32_t mask;          /* bitmask of kernel variants present (hint)   */
+    void *stream;           /* hipStream_t or NULL for the context stream */
+} srtp_gpu_batch_t;
+
+int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b);
+
+/* re-apply the keystream of the given (speculative) meta to the packets at
+ * arena+off: undoes an in-place speculative decryption before a re-run */
+int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
+                  const uint64_t *off, const srtp_dev_meta_t *meta,
+                  void *stream);
+
+/* device header parse for the device-resident API */
+int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
+                   const uint64_t *in_off, const uint32_t *in_len,
+                   srtp_dev_hdr_t *hdr_out, void *stream);
+
+/* memory helpers */
+void *srtp_gpu_malloc(size_t bytes);
+void srtp_gpu_free(void *p);
+void *srtp_gpu_host_alloc(size_t bytes); /* pinned */
+void srtp_gpu_host_free(void *p);
+int srtp_gpu_h2d(srtp_gpu_t *g, void *dst, const void *src, size_t n,
+                 void *stream);
+int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
+                 void *stream);
+int srtp_gpu_sync(srtp_gpu_t *g, void *stream);
+
+/* timing of the last srtp_gpu_run kernels (ms, from HIP events) */
+double srtp_gpu_last_kernel_ms(srtp_gpu_t *g);
+void srtp_gpu_set_timing(srtp_gpu_t *g, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

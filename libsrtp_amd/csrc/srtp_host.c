@@ -1,0 +1,2265 @@
+/*
+ * srtp_host.c -- the host half of libsrtp_mi355x: the libsrtp C API
+ * (include/srtp_mi355x.h) on top of the HIP kernels (srtp_kernels.hip).
+ *
+ * What lives here is the part of srtp/srtp.c that is inherently sequential
+ * per stream and cheap: session/stream management and key derivation
+ * (srtp.c:594-1716, 3250-3648), the SSRC -> stream map (replaces the linear
+ * list of srtp.c:5169-5335 with an O(1) open-addressing map; first inserted
+ * wins, like srtp_stream_list_get), packet-index estimation and the replay
+ * window (crypto/replay/rdbx.c), key-usage limits (crypto/kernel/key.c) and
+ * events.  For a batch it runs a PRE-PASS in packet order that fixes every
+ * packet's index/ROC, key slot and early error exactly as srtp_protect /
+ * srtp_unprotect would, then hands the whole batch to the GPU, which does
+ * all AES / HMAC / GHASH work.
+ *
+ * Unprotect is speculative: the pre-pass assumes earlier packets of the
+ * batch authenticate; a POST-PASS replays the reference's per-packet logic
+ * in order with the real authentication results (srtp.c:2994-3167), and
+ * re-runs ("redo") any packet whose index estimate changed because an
+ * earlier packet failed.  Outputs and statuses are therefore identical to
+ * calling the reference once per packet.
+ */
+#include "srtp_mi355x.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "host_crypto.h"
+#include "srtp_dev.h"
+
+int srtp_mi355x_debug_index(size_t window, int allow_repeat_tx,
+                            uint32_t pending_roc, size_t n,
+                            const uint16_t *seq, int32_t *status,
+                            uint64_t *est_out);
+
+#define SEQ_MEDIAN 32768
+#define SEQ_MAX 65536
+#define SOFT_LIMIT 0x10000
+
+enum { DIR_UNKNOWN = 0, DIR_SENDER = 1, DIR_RECEIVER = 2 };
+
+/* ------------------------------------------------------------------------
+ * logging / events (srtp.c:1723-1773, 5085-5135)
+ * ---------------------------------------------------------------------- */
+static srtp_log_handler_func_t *g_log_handler;
+static void *g_log_data;
+
+static void log_msg(srtp_log_level_t lvl, const char *msg)
+{
+    if (g_log_handler)
+        g_log_handler(lvl, msg, g_log_data);
+    else
+        fprintf(stderr, "%s", msg);
+}
+
+static void default_event_reporter(srtp_event_data_t *d)
+{
+    static const char *what[] = { "SSRC collision",
+                                  "key usage soft limit reached",
+                                  "key usage hard limit reached",
+                                  "packet index limit reached" };
+    char buf[128];
+    snprintf(buf, sizeof buf, "srtp: in stream 0x%x: %s\n",
+             (unsigned)d->ssrc,
+             (unsigned)d->event < 4 ? what[d->event] : "unknown event");
+    log_msg(srtp_log_level_warning, buf);
+}
+
+static srtp_event_handler_func_t *g_event_handler = default_event_reporter;
+
+/* ------------------------------------------------------------------------
+ * session keys: one per master key of a stream, shared by template clones
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    uint32_t slot;          /* device key slot                               */
+    uint32_t cipher_type;   /* SRTP_* cipher id                              */
+    uint32_t family;        /* SRTP_DEV_*                                    */
+    uint32_t rounds;
+    uint32_t variant;       /* kernel variant id (srtp_dev.h)                */
+    size_t tag_len;
+    uint8_t mki[SRTP_MAX_MKI_LEN];
+    uint64_t num_left;      /* key.c: srtp_key_limit_ctx_t                   */
+    int limit_state;        /* 0 normal, 1 past soft limit, 2 expired        */
+} hkey_t;
+
+typedef struct {
+    int refs;
+    size_t n;
+    hkey_t k[SRTP_MAX_NUM_MASTER_KEYS];
+} keyset_t;
+
+/* replay database (crypto/replay/rdbx.c) */
+typedef struct {
+    uint64_t index;
+    size_t bits;      /* window length rounded up to 32 (datatypes.c:264) */
+    uint32_t *w;
+    uint32_t pending_roc;
+} rdbx_t;
+
+struct srtp_stream_ctx_t_ {
+    uint32_t ssrc;    /* host-order numeric value */
+    int direction;
+    int rtp_services;
+    int rtcp_services;
+    bool allow_repeat_tx;
+    bool use_mki;
+    size_t mki_size;
+    keyset_t *keys;
+    rdbx_t rdbx;
+    size_t window_size; /* as requested */
+    /* per-batch speculative shadow (unprotect pre-pass) */
+    uint64_t spec_epoch;
+    rdbx_t spec;
+};
+
+typedef struct {
+    uint32_t *keys; /* ssrc */
+    srtp_stream_ctx_t **vals;
+    size_t cap;     /* power of two */
+    size_t used;
+} ssrc_map_t;
+
+typedef struct {
+    /* host-buffer batch staging (pinned) and its device mirror */
+    uint8_t *h_arena, *d_arena;
+    size_t arena_cap;
+    uint64_t *h_off, *d_off;
+    srtp_dev_meta_t *h_meta, *d_meta;
+    uint8_t *h_auth, *d_auth;
+    srtp_dev_hdr_t *h_hdr, *d_hdr;
+    size_t n_cap;
+} stage_t;
+
+struct srtp_ctx_t_ {
+    srtp_stream_ctx_t *templ;
+    srtp_stream_ctx_t **list; /* insertion order, like the reference list */
+    size_t n, cap;
+    ssrc_map_t map;
+    void *user_data;
+    srtp_gpu_t *gpu;
+    uint32_t next_slot;
+    uint32_t *free_slots;
+    size_t n_free, free_cap;
+    uint32_t variant_mask;
+    stage_t st;
+    uint64_t epoch;
+    int timing;
+    double last_ms;
+};
+
+/* ------------------------------------------------------------------------
+ * SSRC map
+ * ---------------------------------------------------------------------- */
+static size_t map_hash(uint32_t k, size_t cap)
+{
+    uint32_t h = k * 0x9e3779b1u;
+    h ^= h >> 15;
+    return h & (cap - 1);
+}
+
+static int map_rebuild(srtp_t ctx, size_t cap)
+{
+    ssrc_map_t m;
+    m.cap = cap;
+    m.used = 0;
+    m.keys = (uint32_t *)calloc(cap, sizeof(uint32_t));
+    m.vals = (srtp_stream_ctx_t **)calloc(cap, sizeof(void *));
+    if (!m.keys || !m.vals) {
+        free(m.keys);
+        free(m.vals);
+        return -1;
+    }
+    for (size_t i = 0; i < ctx->n; i++) {
+        srtp_stream_ctx_t *s = ctx->list[i];
+        size_t h = map_hash(s->ssrc, cap);
+        int dup = 0;
+        while (m.vals[h]) {
+            if (m.keys[h] == s->ssrc) {
+                dup = 1; /* first inserted wins (srtp.c:5292-5305) */
+                break;
+            }
+            h = (h + 1) & (cap - 1);
+        }
+        if (!dup) {
+            m.keys[h] = s->ssrc;
+            m.vals[h] = s;
+            m.used++;
+        }
+    }
+    free(ctx->map.keys);
+    free(ctx->map.vals);
+    ctx->map = m;
+    return 0;
+}
+
+static srtp_stream_ctx_t *map_get(const srtp_t ctx, uint32_t ssrc)
+{
+    if (!ctx->map.cap)
+        return NULL;
+    size_t h = map_hash(ssrc, ctx->map.cap);
+    while (ctx->map.vals[h]) {
+        if (ctx->map.keys[h] == ssrc)
+            return ctx->map.vals[h];
+        h = (h + 1) & (ctx->map.cap - 1);
+    }
+    return NULL;
+}
+
+static int list_insert(srtp_t ctx, srtp_stream_ctx_t *s)
+{
+    if (ctx->n == ctx->cap) {
+        size_t nc = ctx->cap ? 2 * ctx->cap : 4;
+        void *p = realloc(ctx->list, nc * sizeof(void *));
+        if (!p)
+            return -1;
+        ctx->list = (srtp_stream_ctx_t **)p;
+        ctx->cap = nc;
+    }
+    ctx->list[ctx->n++] = s;
+    if (2 * (ctx->map.used + 1) > ctx->map.cap)
+        return map_rebuild(ctx, ctx->map.cap ? 2 * ctx->map.cap : 64);
+    /* plain insert unless an older stream already owns the SSRC */
+    size_t h = map_hash(s->ssrc, ctx->map.cap);
+    while (ctx->map.vals[h]) {
+        if (ctx->map.keys[h] == s->ssrc)
+            return 0;
+        h = (h + 1) & (ctx->map.cap - 1);
+    }
+    ctx->map.keys[h] = s->ssrc;
+    ctx->map.vals[h] = s;
+    ctx->map.used++;
+    return 0;
+}
+
+static void list_remove(srtp_t ctx, srtp_stream_ctx_t *s)
+{
+    for (size_t i = 0; i < ctx->n; i++)
+        if (ctx->list[i] == s) {
+            memmove(&ctx->list[i], &ctx->list[i + 1],
+                    (ctx->n - i - 1) * sizeof(void *));
+            ctx->n--;
+            break;
+        }
+    map_rebuild(ctx, ctx->map.cap ? ctx->map.cap : 64);
+}
+
+/* ------------------------------------------------------------------------
+ * rdbx: crypto/replay/rdbx.c, bitvector of crypto/math/datatypes.c
+ * ---------------------------------------------------------------------- */
+static int rdbx_init(rdbx_t *r, size_t ws)
+{
+    r->bits = (ws + 31) & ~(size_t)31;
+    r->w = (uint32_t *)calloc(r->bits / 32 + 1, sizeof(uint32_t));
+    r->index = 0;
+    r->pending_roc = 0;
+    return r->w ? 0 : -1;
+}
+
+static void rdbx_copy(rdbx_t *dst, const rdbx_t *src)
+{
+    if (dst->bits != src->bits) {
+        free(dst->w);
+        dst->w = (uint32_t *)calloc(src->bits / 32 + 1, sizeof(uint32_t));
+        dst->bits = src->bits;
+    }
+    memcpy(dst->w, src->w, src->bits / 8);
+    dst->index = src->index;
+    dst->pending_roc = src->pending_roc;
+}
+
+static void win_zero(rdbx_t *r) { memset(r->w, 0, r->bits / 8); }
+
+static void win_shift(rdbx_t *r, size_t shift)
+{
+    size_t words = r->bits >> 5;
+    if (shift >= r->bits) {
+        win_zero(r);
+        return;
+    }
+    size_t base = shift >> 5, bi = shift & 31;
+    if (bi == 0) {
+        memmove(r->w, r->w + base, (words - base) * 4);
+    } else {
+        for (size_t i = 0; i + base + 1 < words; i++)
+            r->w[i] = (r->w[i + base] >> bi) | (r->w[i + base + 1] << (32 - bi));
+        r->w[words - base - 1] = r->w[words - 1] >> bi;
+    }
+    memset(r->w + (words - base), 0, base * 4);
+}
+
+static int64_t index_guess(uint64_t local, uint64_t *guess, uint16_t s)
+{
+    /* rdbx.c:112-145 */
+    uint32_t local_roc = (uint32_t)(local >> 16);
+    uint16_t local_seq = (uint16_t)local;
+    uint32_t roc;
+    int64_t diff;
+    if (local_seq < SEQ_MEDIAN) {
+        if ((int)s - (int)local_seq > SEQ_MEDIAN) {
+            roc = local_roc - 1;
+            diff = (int64_t)s - local_seq - SEQ_MAX;
+        } else {
+            roc = local_roc;
+            diff = (int64_t)s - local_seq;
+        }
+    } else {
+        if ((int)local_seq - SEQ_MEDIAN > (int)s) {
+            roc = local_roc + 1;
+            diff = (int64_t)s - local_seq + SEQ_MAX;
+        } else {
+            roc = local_roc;
+            diff = (int64_t)s - local_seq;
+        }
+    }
+    *guess = ((uint64_t)roc << 16) | s;
+    return diff;
+}
+
+static srtp_err_status_t estimate(const rdbx_t *r, uint16_t seq, uint64_t *est,
+                                  int64_t *delta)
+{
+    /* srtp_get_est_pkt_index + srtp_estimate_index, srtp.c:2038-2081;
+     * srtp_rdbx_estimate_index, rdbx.c:280-299 */
+    if (r->pending_roc) {
+        *est = ((uint64_t)r->pending_roc << 16) | seq;
+        *delta = (int64_t)(*est - r->index);
+        if (*est > r->index) {
+            if (*est - r->index > SEQ_MEDIAN) {
+                *delta = 0;
+                return srtp_err_status_pkt_idx_adv;
+            }
+        } else if (*est < r->index) {
+            if (r->index - *est > SEQ_MEDIAN) {
+                *delta = 0;
+                return srtp_err_status_pkt_idx_old;
+            }
+        }
+        return srtp_err_status_ok;
+    }
+    if (r->index > SEQ_MEDIAN) {
+        *delta = index_guess(r->index, est, seq);
+    } else {
+        *est = seq;
+        *delta = (int64_t)seq - (int64_t)r->index;
+    }
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t rdbx_check(const rdbx_t *r, int64_t delta)
+{
+    /* rdbx.c:227-243 */
+    if (delta > 0)
+        return srtp_err_status_ok;
+    if ((int64_t)(r->bits - 1) + delta < 0)
+        return srtp_err_status_replay_old;
+    size_t bit = (size_t)((int64_t)(r->bits - 1) + delta);
+    if ((r->w[bit >> 5] >> (bit & 31)) & 1)
+        return srtp_err_status_replay_fail;
+    return srtp_err_status_ok;
+}
+
+static void rdbx_add(rdbx_t *r, int64_t delta)
+{
+    /* rdbx.c:253-270 */
+    size_t bit;
+    if (delta > 0) {
+        r->index += (uint16_t)delta;
+        win_shift(r, (size_t)delta);
+        bit = r->bits - 1;
+    } else {
+        bit = (size_t)((int64_t)(r->bits - 1) + delta);
+    }
+    r->w[bit >> 5] |= 1u << (bit & 31);
+}
+
+static void rdbx_set_roc_seq(rdbx_t *r, uint32_t roc, uint16_t seq)
+{
+    /* rdbx.c:323-338 */
+    if (roc < (r->index >> 16))
+        return;
+    r->index = ((uint64_t)roc << 16) | seq;
+    win_zero(r);
+}
+
+/* the index/replay step shared by protect and unprotect-commit */
+static void rdbx_accept(rdbx_t *r, uint64_t est, int64_t delta, int adv)
+{
+    if (adv) {
+        rdbx_set_roc_seq(r, (uint32_t)(est >> 16), (uint16_t)est);
+        r->pending_roc = 0;
+        rdbx_add(r, 0);
+    } else {
+        rdbx_add(r, delta);
+    }
+}
+
+/* key.c:74-90 -> 0 normal, 1 soft, 2 hard */
+static int key_limit_update(hkey_t *k)
+{
+    k->num_left--;
+    if (k->num_left >= SOFT_LIMIT)
+        return 0;
+    if (k->limit_state == 0)
+        k->limit_state = 1;
+    if (k->num_left < 1) {
+        k->limit_state = 2;
+        return 2;
+    }
+    return 1;
+}
+
+static void fire(srtp_t ctx, const srtp_stream_ctx_t *s, srtp_event_t ev)
+{
+    if (g_event_handler) {
+        srtp_event_data_t d;
+        d.session = ctx;
+        d.ssrc = s->ssrc;
+        d.event = ev;
+        g_event_handler(&d);
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * KDF and key setup (srtp.c:1070-1142, 1233-1607)
+ * ---------------------------------------------------------------------- */
+static size_t full_key_length(uint32_t id)
+{
+    switch (id) {
+    case SRTP_AES_ICM_128: return SRTP_AES_ICM_128_KEY_LEN_WSALT;
+    case SRTP_AES_ICM_192: return SRTP_AES_ICM_192_KEY_LEN_WSALT;
+    case SRTP_AES_ICM_256: return SRTP_AES_ICM_256_KEY_LEN_WSALT;
+    case SRTP_AES_GCM_128: return SRTP_AES_GCM_128_KEY_LEN_WSALT;
+    case SRTP_AES_GCM_256: return SRTP_AES_GCM_256_KEY_LEN_WSALT;
+    default: return 0;
+    }
+}
+
+static size_t base_key_length(uint32_t id, size_t key_len)
+{
+    switch (id) {
+    case SRTP_NULL_CIPHER: return 0;
+    case SRTP_AES_ICM_128:
+    case SRTP_AES_ICM_192:
+    case SRTP_AES_ICM_256: return key_len - SRTP_SALT_LEN;
+    case SRTP_AES_GCM_128:
+    case SRTP_AES_GCM_256: return key_len - SRTP_AEAD_SALT_LEN;
+    default: return key_len;
+    }
+}
+
+static int cipher_supported(const srtp_crypto_policy_t *c)
+{
+    switch (c->cipher_type) {
+    case SRTP_NULL_CIPHER:
+        return 1;
+    case SRTP_AES_ICM_128:
+    case SRTP_AES_ICM_192:
+    case SRTP_AES_ICM_256:
+        /* aes_icm(_ossl).c: key_len 30 / 38 / 46 only */
+        return c->cipher_key_len == full_key_length(c->cipher_type);
+    case SRTP_AES_GCM_128:
+    case SRTP_AES_GCM_256:
+        /* aes_gcm_ossl.c:97-99: tag 8 or 16 */
+        return c->cipher_key_len == full_key_length(c->cipher_type) &&
+               (c->auth_tag_len == 8 || c->auth_tag_len == 16);
+    default:
+        return 0;
+    }
+}
+
+static int auth_supported(const srtp_crypto_policy_t *c)
+{
+    if (c->auth_type == SRTP_HMAC_SHA1)
+        return c->auth_key_len <= 20 && c->auth_tag_len <= 20; /* hmac.c:76 */
+    if (c->auth_type == SRTP_NULL_AUTH) {
+        /* a null auth with a non-zero tag turns into libsrtp's legacy
+         * keystream-prefix mode (srtp.c:2729-2741); not supported here */
+        bool aead = c->cipher_type == SRTP_AES_GCM_128 ||
+                    c->cipher_type == SRTP_AES_GCM_256;
+        return aead || c->auth_tag_len == 0 || !(c->sec_serv & sec_serv_auth);
+    }
+    return 0;
+}
+
+static void kdf_gen(const hc_aes_t *kdf, const uint8_t salt14[14],
+                    uint8_t label, uint8_t *out, size_t len)
+{
+    uint8_t nonce[16] = { 0 };
+    nonce[7] = label; /* srtp.c:1112-1113 */
+    hc_icm_keystream(kdf, salt14, nonce, out, len);
+}
+
+static uint32_t alloc_slot(srtp_t ctx)
+{
+    if (ctx->n_free)
+        return ctx->free_slots[--ctx->n_free];
+    return ctx->next_slot++;
+}
+
+static void release_slot(srtp_t ctx, uint32_t slot)
+{
+    if (ctx->n_free == ctx->free_cap) {
+        size_t nc = ctx->free_cap ? 2 * ctx->free_cap : 16;
+        uint32_t *p = (uint32_t *)realloc(ctx->free_slots, nc * 4);
+        if (!p)
+            return;
+        ctx->free_slots = p;
+        ctx->free_cap = nc;
+    }
+    ctx->free_slots[ctx->n_free++] = slot;
+}
+
+static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
+                                  const srtp_policy_t *p, const uint8_t *master,
+                                  const uint8_t *mki_id, size_t mki_size)
+{
+    const srtp_crypto_policy_t *rtp = &p->rtp, *rtcp = &p->rtcp;
+    size_t input_keylen = full_key_length(rtp->cipher_type), t;
+    if (rtp->auth_type == SRTP_HMAC_SHA1 && 30 > input_keylen)
+        input_keylen = 30;
+    t = full_key_length(rtcp->cipher_type);
+    if (t > input_keylen)
+        input_keylen = t;
+    if (rtcp->auth_type == SRTP_HMAC_SHA1 && 30 > input_keylen)
+        input_keylen = 30;
+    size_t rtp_keylen = rtp->cipher_key_len, rtcp_keylen = rtcp->cipher_key_len;
+    size_t base = base_key_length(rtp->cipher_type, rtp_keylen);
+    size_t salt_len = rtp_keylen - base;
+    if (rtp_keylen < input_keylen && rtcp_keylen < input_keylen)
+        return srtp_err_status_bad_param; /* srtp.c:1293-1295 */
+    size_t kdf_keylen = 30;
+    if (rtp_keylen > kdf_keylen)
+        kdf_keylen = rtp_keylen;
+    if (rtcp_keylen > kdf_keylen)
+        kdf_keylen = rtcp_keylen;
+    if (input_keylen > kdf_keylen)
+        kdf_keylen = input_keylen;
+    if (kdf_keylen == SRTP_AES_GCM_128_KEY_LEN_WSALT ||
+        kdf_keylen == SRTP_AES_GCM_256_KEY_LEN_WSALT)
+        kdf_keylen += 2; /* srtp.c:1309-1312 */
+    if (kdf_keylen != 30 && kdf_keylen != 38 && kdf_keylen != 46)
+        return srtp_err_status_init_fail;
+
+    uint8_t tmp[256];
+    memset(tmp, 0, sizeof tmp);
+    memcpy(tmp, master, input_keylen);
+    hc_aes_t kdf;
+    hc_aes_init(&kdf, tmp, kdf_keylen - SRTP_SALT_LEN);
+    uint8_t kdf_salt[14];
+    memcpy(kdf_salt, tmp + kdf_keylen - SRTP_SALT_LEN, 14);
+
+    uint8_t ek[32], salt[64], ak[20];
+    memset(salt, 0, sizeof salt);
+    kdf_gen(&kdf, kdf_salt, 0x00, ek, base);
+    if (salt_len > 0)
+        kdf_gen(&kdf, kdf_salt, 0x02, salt, salt_len);
+    size_t auth_key_len = rtp->auth_type == SRTP_HMAC_SHA1 ? rtp->auth_key_len : 0;
+    kdf_gen(&kdf, kdf_salt, 0x01, ak, auth_key_len);
+
+    srtp_dev_key_t dk;
+    memset(&dk, 0, sizeof dk);
+    hk->cipher_type = rtp->cipher_type;
+    hk->tag_len = rtp->auth_tag_len;
+    hk->num_left = 0xffffffffffffULL; /* srtp.c:1251 */
+    hk->limit_state = 0;
+    memset(hk->mki, 0, sizeof hk->mki);
+    if (mki_size)
+        memcpy(hk->mki, mki_id, mki_size);
+    memcpy(dk.mki, hk->mki, sizeof dk.mki);
+    dk.mki_size = (uint32_t)mki_size;
+    dk.tag_len = (uint32_t)hk->tag_len;
+    dk.conf = (rtp->sec_serv & sec_serv_conf) ? 1 : 0;
+
+    int rc_code = 0;
+    uint32_t *gtab = NULL;
+    uint32_t gbuf[1024];
+    if (rtp->cipher_type == SRTP_NULL_CIPHER) {
+        hk->family = SRTP_DEV_NULL;
+        hk->rounds = 0;
+        dk.conf = 0;
+    } else {
+        hc_aes_t ca;
+        hc_aes_init(&ca, ek, base);
+        memcpy(dk.rk, ca.rk, sizeof dk.rk);
+        hk->rounds = (uint32_t)ca.rounds;
+        rc_code = (ca.rounds - 8) / 2;
+        if (rtp->cipher_type == SRTP_AES_GCM_128 ||
+            rtp->cipher_type == SRTP_AES_GCM_256) {
+            hk->family = SRTP_DEV_GCM;
+            uint8_t z[16] = { 0 }, h[16];
+            hc_aes_block(&ca, z, h);
+            for (int i = 0; i < 4; i++)
+                dk.h[i] = (uint32_t)h[4 * i] << 24 | (uint32_t)h[4 * i + 1] << 16 |
+                          (uint32_t)h[4 * i + 2] << 8 | h[4 * i + 3];
+            hc_ghash_table(h, gbuf);
+            gtab = gbuf;
+            dk.conf = 1; /* AEAD always encrypts (srtp.c:2088-2098) */
+        } else {
+            hk->family = SRTP_DEV_ICM;
+        }
+    }
+    dk.rounds = hk->rounds;
+    dk.family = hk->family;
+    /* salt as little-endian words; bytes past the salt are zero */
+    uint8_t sb[16];
+    memset(sb, 0, sizeof sb);
+    if (hk->family == SRTP_DEV_ICM)
+        memcpy(sb, salt, 14);
+    else if (hk->family == SRTP_DEV_GCM)
+        memcpy(sb, salt, 12);
+    for (int i = 0; i < 4; i++)
+        dk.salt[i] = (uint32_t)sb[4 * i] | (uint32_t)sb[4 * i + 1] << 8 |
+                     (uint32_t)sb[4 * i + 2] << 16 | (uint32_t)sb[4 * i + 3] << 24;
+    int auth_on = rtp->auth_type == SRTP_HMAC_SHA1 &&
+                  (rtp->sec_serv & sec_serv_auth) && hk->family != SRTP_DEV_GCM;
+    dk.auth = (uint32_t)auth_on;
+    if (rtp->auth_type == SRTP_HMAC_SHA1) {
+        uint8_t pad[64];
+        for (int i = 0; i < 64; i++)
+            pad[i] = (uint8_t)((i < (int)auth_key_len ? ak[i] : 0) ^ 0x36);
+        hc_sha1_midstate(pad, dk.ipad);
+        for (int i = 0; i < 64; i++)
+            pad[i] = (uint8_t)((i < (int)auth_key_len ? ak[i] : 0) ^ 0x5c);
+        hc_sha1_midstate(pad, dk.opad);
+    }
+    hk->variant = hk->family == SRTP_DEV_GCM
+                      ? SRTP_VARIANT(SRTP_DEV_GCM, rc_code, 0)
+                      : SRTP_VARIANT(hk->family, hk->family ? rc_code : 0,
+                                     auth_on);
+    hk->slot = alloc_slot(ctx);
+    dk.ghash_slot = hk->slot;
+    memset(tmp, 0, sizeof tmp);
+    memset(ek, 0, sizeof ek);
+    memset(ak, 0, sizeof ak);
+    if (srtp_gpu_set_key(ctx->gpu, hk->slot, &dk, gtab))
+        return srtp_err_status_init_fail;
+    ctx->variant_mask |= 1u << hk->variant;
+    return srtp_err_status_ok;
+}
+
+static void keyset_release(srtp_t ctx, keyset_t *ks)
+{
+    if (!ks || --ks->refs > 0)
+        return;
+    for (size_t i = 0; i < ks->n; i++)
+        release_slot(ctx, ks->k[i].slot);
+    memset(ks, 0, sizeof *ks);
+    free(ks);
+}
+
+static void stream_free(srtp_t ctx, srtp_stream_ctx_t *s)
+{
+    if (!s)
+        return;
+    keyset_release(ctx, s->keys);
+    free(s->rdbx.w);
+    free(s->spec.w);
+    free(s);
+}
+
+/* srtp_valid_policy, srtp.c:554-592 + what this build supports */
+static srtp_err_status_t valid_policy(const srtp_policy_t *p)
+{
+    if (!p)
+        return srtp_err_status_bad_param;
+    if (p->key == NULL) {
+        if (p->num_master_keys <= 0 ||
+            p->num_master_keys > SRTP_MAX_NUM_MASTER_KEYS)
+            return srtp_err_status_bad_param;
+        if (p->use_mki) {
+            if (p->mki_size == 0 || p->mki_size > SRTP_MAX_MKI_LEN)
+                return srtp_err_status_bad_param;
+        } else if (p->mki_size != 0) {
+            return srtp_err_status_bad_param;
+        }
+        for (size_t i = 0; i < p->num_master_keys; i++) {
+            if (p->keys[i]->key == NULL)
+                return srtp_err_status_bad_param;
+            if (p->use_mki && p->keys[i]->mki_id == NULL)
+                return srtp_err_status_bad_param;
+        }
+    } else if (p->use_mki || p->mki_size != 0) {
+        return srtp_err_status_bad_param;
+    }
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t stream_new(srtp_t ctx, const srtp_policy_t *p,
+                                    srtp_stream_ctx_t **out)
+{
+    srtp_err_status_t st = valid_policy(p);
+    if (st)
+        return st;
+    if (!cipher_supported(&p->rtp) || !auth_supported(&p->rtp))
+        return srtp_err_status_bad_param;
+    /* RFC 6904 header-extension encryption and RFC 9335 cryptex are not on
+     * the GPU path yet (DESIGN.md "Out of scope") */
+    if ((p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0) || p->use_cryptex)
+        return srtp_err_status_bad_param;
+    if (p->window_size != 0 &&
+        (p->window_size < 64 || p->window_size >= 0x8000))
+        return srtp_err_status_bad_param; /* srtp.c:1670-1672 */
+    srtp_stream_ctx_t *s = (srtp_stream_ctx_t *)calloc(1, sizeof *s);
+    if (!s)
+        return srtp_err_status_alloc_fail;
+    s->window_size = p->window_size ? p->window_size : 128;
+    if (rdbx_init(&s->rdbx, s->window_size)) {
+        free(s);
+        return srtp_err_status_alloc_fail;
+    }
+    s->ssrc = p->ssrc.value;
+    s->rtp_services = p->rtp.sec_serv;
+    s->rtcp_services = p->rtcp.sec_serv;
+    s->direction = DIR_UNKNOWN;
+    s->allow_repeat_tx = p->allow_repeat_tx;
+    keyset_t *ks = (keyset_t *)calloc(1, sizeof *ks);
+    if (!ks) {
+        stream_free(ctx, s);
+        return srtp_err_status_alloc_fail;
+    }
+    ks->refs = 1;
+    s->keys = ks;
+    if (p->key) {
+        s->use_mki = false;
+        s->mki_size = 0;
+        ks->n = 1;
+        st = init_key(ctx, &ks->k[0], p, p->key, NULL, 0);
+    } else {
+        s->use_mki = p->use_mki;
+        s->mki_size = p->use_mki ? p->mki_size : 0;
+        ks->n = p->num_master_keys;
+        for (size_t i = 0; i < ks->n && !st; i++)
+            st = init_key(ctx, &ks->k[i], p, p->keys[i]->key,
+                          p->keys[i]->mki_id, s->mki_size);
+    }
+    if (st) {
+        stream_free(ctx, s);
+        return st;
+    }
+    *out = s;
+    return srtp_err_status_ok;
+}
+
+static srtp_stream_ctx_t *stream_clone(const srtp_stream_ctx_t *t, uint32_t ssrc)
+{
+    /* srtp_stream_clone, srtp.c:762-863 */
+    srtp_stream_ctx_t *s = (srtp_stream_ctx_t *)calloc(1, sizeof *s);
+    if (!s)
+        return NULL;
+    if (rdbx_init(&s->rdbx, t->rdbx.bits)) {
+        free(s);
+        return NULL;
+    }
+    s->ssrc = ssrc;
+    s->direction = t->direction;
+    s->rtp_services = t->rtp_services;
+    s->rtcp_services = t->rtcp_services;
+    s->allow_repeat_tx = t->allow_repeat_tx;
+    s->use_mki = t->use_mki;
+    s->mki_size = t->mki_size;
+    s->window_size = t->window_size;
+    s->keys = t->keys;
+    s->keys->refs++;
+    return s;
+}
+
+/* ------------------------------------------------------------------------
+ * public API: lifecycle
+ * ---------------------------------------------------------------------- */
+static int g_inited;
+
+srtp_err_status_t srtp_init(void)
+{
+    if (!srtp_gpu_available()) {
+        log_msg(srtp_log_level_error,
+                "libsrtp_mi355x: no HIP device available\n");
+        return srtp_err_status_init_fail;
+    }
+    g_inited = 1;
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_shutdown(void)
+{
+    g_inited = 0;
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t add_stream(srtp_t ctx, const srtp_policy_t *p)
+{
+    srtp_stream_ctx_t *s;
+    srtp_err_status_t st = stream_new(ctx, p, &s);
+    if (st)
+        return st;
+    switch (p->ssrc.type) {
+    case ssrc_any_outbound:
+    case ssrc_any_inbound:
+        if (ctx->templ) {
+            stream_free(ctx, s);
+            return srtp_err_status_bad_param;
+        }
+        s->direction = p->ssrc.type == ssrc_any_outbound ? DIR_SENDER
+                                                         : DIR_RECEIVER;
+        ctx->templ = s;
+        return srtp_err_status_ok;
+    case ssrc_specific:
+        if (list_insert(ctx, s)) {
+            stream_free(ctx, s);
+            return srtp_err_status_alloc_fail;
+        }
+        return srtp_err_status_ok;
+    default:
+        stream_free(ctx, s);
+        return srtp_err_status_bad_param;
+    }
+}
+
+srtp_err_status_t srtp_stream_add(srtp_t ctx, const srtp_policy_t *p)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st = valid_policy(p);
+    if (st)
+        return st;
+    return add_stream(ctx, p);
+}
+
+srtp_err_status_t srtp_create(srtp_t *session, const srtp_policy_t *policy)
+{
+    if (!session)
+        return srtp_err_status_bad_param;
+    if (policy && valid_policy(policy))
+        return srtp_err_status_bad_param;
+    srtp_t ctx = (srtp_t)calloc(1, sizeof *ctx);
+    if (!ctx)
+        return srtp_err_status_alloc_fail;
+    if (srtp_gpu_open(&ctx->gpu)) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        log_msg(srtp_log_level_error, "\n");
+        free(ctx);
+        *session = NULL;
+        return srtp_err_status_init_fail;
+    }
+    map_rebuild(ctx, 64);
+    *session = ctx;
+    for (const srtp_policy_t *p = policy; p; p = p->next) {
+        srtp_err_status_t st = srtp_stream_add(ctx, p);
+        if (st) {
+            srtp_dealloc(ctx);
+            *session = NULL;
+            return st;
+        }
+    }
+    return srtp_err_status_ok;
+}
+
+static void stage_free(stage_t *st)
+{
+    srtp_gpu_host_free(st->h_arena);
+    srtp_gpu_free(st->d_arena);
+    srtp_gpu_host_free(st->h_off);
+    srtp_gpu_free(st->d_off);
+    srtp_gpu_host_free(st->h_meta);
+    srtp_gpu_free(st->d_meta);
+    srtp_gpu_host_free(st->h_auth);
+    srtp_gpu_free(st->d_auth);
+    srtp_gpu_host_free(st->h_hdr);
+    srtp_gpu_free(st->d_hdr);
+    memset(st, 0, sizeof *st);
+}
+
+srtp_err_status_t srtp_dealloc(srtp_t ctx)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    for (size_t i = 0; i < ctx->n; i++)
+        stream_free(ctx, ctx->list[i]);
+    stream_free(ctx, ctx->templ);
+    free(ctx->list);
+    free(ctx->map.keys);
+    free(ctx->map.vals);
+    free(ctx->free_slots);
+    stage_free(&ctx->st);
+    srtp_gpu_close(ctx->gpu);
+    free(ctx);
+    return srtp_err_status_ok;
+}
+
+srtp_stream_ctx_t *srtp_get_stream(srtp_t ctx, uint32_t ssrc_net)
+{
+    uint32_t v = ((ssrc_net & 0xff) << 24) | ((ssrc_net & 0xff00) << 8) |
+                 ((ssrc_net >> 8) & 0xff00) | (ssrc_net >> 24);
+    return ctx ? map_get(ctx, v) : NULL;
+}
+
+srtp_err_status_t srtp_stream_remove(srtp_t ctx, uint32_t ssrc)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    srtp_stream_ctx_t *s = map_get(ctx, ssrc);
+    if (!s)
+        return srtp_err_status_no_ctx;
+    list_remove(ctx, s);
+    stream_free(ctx, s);
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t update_specific(srtp_t ctx, const srtp_policy_t *p)
+{
+    /* stream_update, srtp.c:3568-3617 */
+    srtp_stream_ctx_t *s = map_get(ctx, p->ssrc.value);
+    if (!s)
+        return srtp_err_status_bad_param;
+    if (s->use_mki != p->use_mki || (s->use_mki && s->mki_size != p->mki_size))
+        return srtp_err_status_bad_param;
+    uint64_t old_index = s->rdbx.index;
+    srtp_err_status_t st = srtp_stream_remove(ctx, p->ssrc.value);
+    if (st)
+        return st;
+    st = srtp_stream_add(ctx, p);
+    if (st)
+        return st;
+    s = map_get(ctx, p->ssrc.value);
+    if (!s)
+        return srtp_err_status_fail;
+    s->rdbx.index = old_index;
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t update_template(srtp_t ctx, const srtp_policy_t *p)
+{
+    /* update_template_streams, srtp.c:3430-3560 */
+    if (!ctx->templ)
+        return srtp_err_status_bad_param;
+    if (ctx->templ->use_mki != p->use_mki ||
+        (ctx->templ->use_mki && ctx->templ->mki_size != p->mki_size))
+        return srtp_err_status_bad_param;
+    srtp_stream_ctx_t *nt;
+    srtp_err_status_t st = stream_new(ctx, p, &nt);
+    if (st)
+        return st;
+    /* streams cloned from the old template are re-cloned, keeping their
+     * extended sequence number; other streams are kept as they are */
+    keyset_t *old = ctx->templ->keys;
+    for (size_t i = 0; i < ctx->n; i++) {
+        srtp_stream_ctx_t *s = ctx->list[i];
+        if (s->keys != old)
+            continue;
+        srtp_stream_ctx_t *c = stream_clone(nt, s->ssrc);
+        if (!c) {
+            stream_free(ctx, nt);
+            return srtp_err_status_alloc_fail;
+        }
+        c->rdbx.index = s->rdbx.index;
+        ctx->list[i] = c;
+        stream_free(ctx, s);
+    }
+    stream_free(ctx, ctx->templ);
+    ctx->templ = nt; /* direction stays unknown, as srtp_stream_init leaves it */
+    map_rebuild(ctx, ctx->map.cap ? ctx->map.cap : 64);
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_stream_update(srtp_t ctx, const srtp_policy_t *p)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st = valid_policy(p);
+    if (st)
+        return st;
+    switch (p->ssrc.type) {
+    case ssrc_any_outbound:
+    case ssrc_any_inbound:
+        return update_template(ctx, p);
+    case ssrc_specific:
+        return update_specific(ctx, p);
+    default:
+        return srtp_err_status_bad_param;
+    }
+}
+
+srtp_err_status_t srtp_update(srtp_t ctx, const srtp_policy_t *p)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st = valid_policy(p);
+    if (st)
+        return st;
+    for (; p; p = p->next) {
+        st = srtp_stream_update(ctx, p);
+        if (st)
+            return st;
+    }
+    return srtp_err_status_ok;
+}
+
+/* ------------------------------------------------------------------------
+ * header summary (srtp_validate_rtp_header, srtp.c:307-336)
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    uint32_t ssrc;
+    uint16_t seq;
+    uint16_t err;
+    uint32_t enc_start;
+    uint32_t len;
+} pkt_sum_t;
+
+static void summarize(const uint8_t *p, size_t len, pkt_sum_t *s)
+{
+    s->len = (uint32_t)len;
+    s->err = 0;
+    s->ssrc = 0;
+    s->seq = 0;
+    s->enc_start = 0;
+    if (len < 12) {
+        s->err = srtp_err_status_bad_param;
+        return;
+    }
+    size_t h = 12 + 4 * (size_t)(p[0] & 0x0f);
+    s->seq = (uint16_t)(p[2] << 8 | p[3]);
+    s->ssrc = (uint32_t)p[8] << 24 | (uint32_t)p[9] << 16 |
+              (uint32_t)p[10] << 8 | p[11];
+    if (len < h) {
+        s->err = srtp_err_status_bad_param;
+        return;
+    }
+    if (p[0] & 0x10) {
+        if (len < h + 4) {
+            s->err = srtp_err_status_bad_param;
+            return;
+        }
+        h += ((size_t)(p[h + 2] << 8 | p[h + 3]) + 1) * 4;
+        if (len < h) {
+            s->err = srtp_err_status_bad_param;
+            return;
+        }
+    }
+    s->enc_start = (uint32_t)h;
+}
+
+static void from_dev_hdr(const srtp_dev_hdr_t *d, pkt_sum_t *s)
+{
+    s->ssrc = d->ssrc;
+    s->seq = (uint16_t)(d->seq_len & 0xffff);
+    s->len = d->len;
+    if (d->enc_start >> 24) {
+        s->err = (uint16_t)(d->enc_start >> 24);
+        s->enc_start = 0;
+    } else {
+        s->err = 0;
+        s->enc_start = d->enc_start;
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * protect pre-pass: srtp_protect / srtp_protect_aead up to the crypto
+ * (srtp.c:2493-2712, 2088-2233).  Mutates stream state exactly as the
+ * reference does; the GPU then performs the crypto of all OK packets.
+ * ---------------------------------------------------------------------- */
+static srtp_err_status_t pre_protect(srtp_t ctx, const pkt_sum_t *s,
+                                     size_t cap, size_t mki_index,
+                                     srtp_dev_meta_t *meta, size_t *out_len)
+{
+    if (s->err)
+        return (srtp_err_status_t)s->err;
+    srtp_stream_ctx_t *st = map_get(ctx, s->ssrc);
+    if (!st) {
+        if (!ctx->templ)
+            return srtp_err_status_no_ctx;
+        st = stream_clone(ctx->templ, s->ssrc);
+        if (!st)
+            return srtp_err_status_alloc_fail;
+        if (list_insert(ctx, st)) {
+            stream_free(ctx, st);
+            return srtp_err_status_alloc_fail;
+        }
+        st->direction = DIR_SENDER;
+    }
+    if (st->direction != DIR_SENDER) {
+        if (st->direction == DIR_UNKNOWN)
+            st->direction = DIR_SENDER;
+        else
+            fire(ctx, st, event_ssrc_collision);
+    }
+    hkey_t *k;
+    if (st->use_mki) {
+        if (mki_index >= st->keys->n)
+            return srtp_err_status_bad_mki;
+        k = &st->keys->k[mki_index];
+    } else {
+        k = &st->keys->k[0];
+    }
+    int ev = key_limit_update(k);
+    if (k->family == SRTP_DEV_GCM) {
+        if (ev == 2) {
+            fire(ctx, st, event_key_hard_limit);
+            return srtp_err_status_key_expired;
+        }
+        if (ev == 1)
+            fire(ctx, st, event_key_soft_limit);
+    } else {
+        if (ev == 1)
+            fire(ctx, st, event_key_soft_limit);
+        if (ev == 2) {
+            fire(ctx, st, event_key_hard_limit);
+            return srtp_err_status_key_expired;
+        }
+    }
+    size_t tag_len = k->tag_len;
+    if (cap < s->len + st->mki_size + tag_len)
+        return srtp_err_status_buffer_small;
+    if (s->enc_start > s->len)
+        return srtp_err_status_parse_err;
+    uint64_t est;
+    int64_t delta;
+    srtp_err_status_t rc = estimate(&st->rdbx, s->seq, &est, &delta);
+    if (rc && rc != srtp_err_status_pkt_idx_adv)
+        return rc;
+    if (rc == srtp_err_status_pkt_idx_adv) {
+        rdbx_accept(&st->rdbx, est, 0, 1);
+    } else {
+        rc = rdbx_check(&st->rdbx, delta);
+        if (rc && (rc != srtp_err_status_replay_fail || !st->allow_repeat_tx))
+            return rc;
+        rdbx_add(&st->rdbx, delta);
+    }
+    if (k->family == SRTP_DEV_ICM && (st->rtp_services & sec_serv_conf)) {
+        /* aes_icm.c:317-322: at most 0xffff keystream blocks */
+        if ((s->len - s->enc_start + 15) / 16 > 0xffff)
+            return srtp_err_status_cipher_fail;
+    }
+    meta->key = k->slot;
+    meta->roc = (uint32_t)(est >> 16);
+    meta->info = s->enc_start | (k->variant << 24);
+    meta->len = s->len;
+    *out_len = s->len + tag_len + st->mki_size;
+    return srtp_err_status_ok;
+}
+
+/* ------------------------------------------------------------------------
+ * unprotect pre-pass (speculative) and post-pass (exact, in order)
+ * ---------------------------------------------------------------------- */
+typedef struct {
+    srtp_err_status_t sverdict; /* state-independent verdict              */
+    uint64_t est;               /* speculative estimate sent to the GPU    */
+    int gpu;                    /* crypto was run for this packet          */
+    int redo;
+    hkey_t *key;
+} upkt_t;
+
+/* per-batch provisional streams (unknown SSRC + template) */
+typedef struct {
+    uint32_t ssrc;
+    rdbx_t r;
+    int created; /* a speculative success created the stream */
+} prov_t;
+
+typedef struct {
+    prov_t *v;
+    size_t n, cap;
+} provset_t;
+
+static prov_t *prov_get(provset_t *ps, uint32_t ssrc, size_t win_bits)
+{
+    for (size_t i = 0; i < ps->n; i++)
+        if (ps->v[i].ssrc == ssrc)
+            return &ps->v[i];
+    if (ps->n == ps->cap) {
+        size_t nc = ps->cap ? 2 * ps->cap : 8;
+        prov_t *p = (prov_t *)realloc(ps->v, nc * sizeof(prov_t));
+        if (!p)
+            return NULL;
+        ps->v = p;
+        ps->cap = nc;
+    }
+    prov_t *p = &ps->v[ps->n++];
+    memset(p, 0, sizeof *p);
+    p->ssrc = ssrc;
+    rdbx_init(&p->r, win_bits);
+    return p;
+}
+
+static void provset_free(provset_t *ps)
+{
+    for (size_t i = 0; i < ps->n; i++)
+        free(ps->v[i].r.w);
+    free(ps->v);
+    memset(ps, 0, sizeof *ps);
+}
+
+static rdbx_t *spec_state(srtp_t ctx, srtp_stream_ctx_t *s)
+{
+    if (s->spec_epoch != ctx->epoch) {
+        if (!s->spec.w)
+            rdbx_init(&s->spec, s->rdbx.bits);
+        rdbx_copy(&s->spec, &s->rdbx);
+        s->spec_epoch = ctx->epoch;
+    }
+    return &s->spec;
+}
+
+/* MKI lookup by the packet trailer, srtp.c:1961-2016 */
+static hkey_t *mki_lookup(const srtp_stream_ctx_t *st, const uint8_t *tail_mki)
+{
+    for (size_t i = 0; i < st->keys->n; i++)
+        if (memcmp(tail_mki, st->keys->k[i].mki, st->mki_size) == 0)
+            return &st->keys->k[i];
+    return NULL;
+}
+
+/* state-independent checks after index estimation (srtp.c:2905-2990,
+ * 2298-2352).  `mki` points at the packet's MKI bytes (or NULL). */
+static srtp_err_status_t un_static(const srtp_stream_ctx_t *st,
+                                   const pkt_sum_t *s, size_t cap,
+                                   const uint8_t *mki_bytes, hkey_t **key,
+                                   srtp_dev_meta_t *meta)
+{
+    hkey_t *k = &st->keys->k[0];
+    if (st->use_mki) {
+        size_t tl = k->family == SRTP_DEV_GCM ? 0 : k->tag_len;
+        if (tl > s->len || st->mki_size > s->len - tl)
+            return srtp_err_status_bad_mki;
+        if (!mki_bytes)
+            return srtp_err_status_bad_mki;
+        k = mki_lookup(st, mki_bytes);
+        if (!k)
+            return srtp_err_status_bad_mki;
+    }
+    *key = k;
+    size_t tag_len = k->tag_len;
+    if (s->len < tag_len + st->mki_size ||
+        s->enc_start > s->len - tag_len - st->mki_size)
+        return srtp_err_status_parse_err;
+    if (k->family == SRTP_DEV_GCM) {
+        if (s->len - s->enc_start - st->mki_size < tag_len)
+            return srtp_err_status_cipher_fail;
+    }
+    if (cap < s->len - st->mki_size - tag_len)
+        return srtp_err_status_buffer_small;
+    meta->key = k->slot;
+    meta->info = s->enc_start | (k->variant << 24);
+    meta->len = (uint32_t)(s->len - tag_len - st->mki_size);
+    return srtp_err_status_ok;
+}
+
+/* speculative pre-pass for packet s; returns 1 if the GPU must run it */
+static int pre_unprotect(srtp_t ctx, provset_t *ps, const pkt_sum_t *s,
+                         size_t cap, const uint8_t *mki_bytes, upkt_t *u,
+                         srtp_dev_meta_t *meta)
+{
+    memset(u, 0, sizeof *u);
+    if (s->err) {
+        u->sverdict = (srtp_err_status_t)s->err;
+        return 0;
+    }
+    srtp_stream_ctx_t *st = map_get(ctx, s->ssrc);
+    rdbx_t *r = NULL;
+    const srtp_stream_ctx_t *kst = st;
+    uint64_t est;
+    int64_t delta = 0;
+    int adv = 0;
+    prov_t *pv = NULL;
+    if (!st) {
+        if (!ctx->templ) {
+            u->sverdict = srtp_err_status_no_ctx;
+            return 0;
+        }
+        kst = ctx->templ;
+        pv = prov_get(ps, s->ssrc, ctx->templ->rdbx.bits);
+        if (!pv) {
+            u->sverdict = srtp_err_status_alloc_fail;
+            return 0;
+        }
+        if (pv->created) {
+            r = &pv->r;
+        } else {
+            est = s->seq;
+            delta = (int64_t)est;
+        }
+    } else {
+        r = spec_state(ctx, st);
+    }
+    if (r) {
+        srtp_err_status_t rc = estimate(r, s->seq, &est, &delta);
+        if (rc && rc != srtp_err_status_pkt_idx_adv)
+            return 0; /* speculatively old; the post-pass decides */
+        adv = rc == srtp_err_status_pkt_idx_adv;
+        if (!adv && rdbx_check(r, delta))
+            return 0; /* speculatively a replay; the post-pass decides */
+    }
+    u->est = est;
+    u->sverdict = un_static(kst, s, cap, mki_bytes, &u->key, meta);
+    if (u->sverdict)
+        return 0;
+    meta->roc = (uint32_t)(est >> 16);
+    /* speculate success */
+    if (pv && !pv->created) {
+        pv->created = 1;
+        rdbx_add(&pv->r, delta);
+    } else if (r) {
+        rdbx_accept(r, est, delta, adv);
+    }
+    u->gpu = 1;
+    return 1;
+}
+
+/* exact post-pass for one packet, in batch order.  Returns the final status
+ * or -1 when the packet must be re-run (its index changed). */
+static int post_unprotect(srtp_t ctx, const pkt_sum_t *s, upkt_t *u,
+                          int auth_ok, size_t *out_len)
+{
+    if (s->err)
+        return s->err;
+    srtp_stream_ctx_t *st = map_get(ctx, s->ssrc);
+    uint64_t est;
+    int64_t delta;
+    int adv = 0;
+    srtp_stream_ctx_t *kst = st;
+    if (!st) {
+        if (!ctx->templ)
+            return srtp_err_status_no_ctx;
+        kst = ctx->templ;
+        est = s->seq;
+        delta = (int64_t)est;
+    } else {
+        srtp_err_status_t rc = estimate(&st->rdbx, s->seq, &est, &delta);
+        if (rc && rc != srtp_err_status_pkt_idx_adv)
+            return rc;
+        adv = rc == srtp_err_status_pkt_idx_adv;
+        if (!adv) {
+            rc = rdbx_check(&st->rdbx, delta);
+            if (rc)
+                return rc;
+        }
+    }
+    if (u->sverdict)
+        return u->sverdict;
+    if (!u->gpu || u->est != est)
+        return -1; /* speculation was wrong: run the crypto again */
+    hkey_t *k = u->key;
+    if (k->family == SRTP_DEV_GCM) {
+        /* srtp_unprotect_aead: key limit before the tag check */
+        int ev = key_limit_update(k);
+        if (ev == 1)
+            fire(ctx, kst, event_key_soft_limit);
+        if (ev == 2) {
+            fire(ctx, kst, event_key_hard_limit);
+            return srtp_err_status_key_expired;
+        }
+        if (!auth_ok)
+            return srtp_err_status_auth_fail;
+    } else {
+        if (!auth_ok)
+            return srtp_err_status_auth_fail;
+        int ev = key_limit_update(k);
+        if (ev == 1)
+            fire(ctx, kst, event_key_soft_limit);
+        if (ev == 2) {
+            fire(ctx, kst, event_key_hard_limit);
+            return srtp_err_status_key_expired;
+        }
+    }
+    if (kst->direction != DIR_RECEIVER) {
+        if (kst->direction == DIR_UNKNOWN)
+            kst->direction = DIR_RECEIVER;
+        else
+            fire(ctx, kst, event_ssrc_collision);
+    }
+    if (!st) {
+        st = stream_clone(ctx->templ, s->ssrc);
+        if (!st)
+            return srtp_err_status_alloc_fail;
+        if (list_insert(ctx, st)) {
+            stream_free(ctx, st);
+            return srtp_err_status_alloc_fail;
+        }
+    }
+    rdbx_accept(&st->rdbx, est, delta, adv);
+    *out_len = s->len - k->tag_len - st->mki_size;
+    return srtp_err_status_ok;
+}
+
+/* ------------------------------------------------------------------------
+ * staging (pinned host + device buffers, grown on demand)
+ * ---------------------------------------------------------------------- */
+static int stage_reserve(srtp_t ctx, size_t n, size_t arena)
+{
+    stage_t *st = &ctx->st;
+    if (arena > st->arena_cap) {
+        size_t c = st->arena_cap ? st->arena_cap : 1 << 16;
+        while (c < arena)
+            c *= 2;
+        srtp_gpu_host_free(st->h_arena);
+        srtp_gpu_free(st->d_arena);
+        st->h_arena = (uint8_t *)srtp_gpu_host_alloc(c);
+        st->d_arena = (uint8_t *)srtp_gpu_malloc(c);
+        st->arena_cap = st->h_arena && st->d_arena ? c : 0;
+        if (!st->arena_cap)
+            return -1;
+    }
+    if (n > st->n_cap) {
+        size_t c = st->n_cap ? st->n_cap : 256;
+        while (c < n)
+            c *= 2;
+#define REALLOC_PAIR(h, d, T)                                                  \
+    srtp_gpu_host_free(st->h);                                                 \
+    srtp_gpu_free(st->d);                                                      \
+    st->h = (T *)srtp_gpu_host_alloc(c * sizeof(T));                           \
+    st->d = (T *)srtp_gpu_malloc(c * sizeof(T));                               \
+    if (!st->h || !st->d)                                                      \
+        return -1;
+        REALLOC_PAIR(h_off, d_off, uint64_t)
+        REALLOC_PAIR(h_meta, d_meta, srtp_dev_meta_t)
+        REALLOC_PAIR(h_auth, d_auth, uint8_t)
+        REALLOC_PAIR(h_hdr, d_hdr, srtp_dev_hdr_t)
+#undef REALLOC_PAIR
+        st->n_cap = c;
+    }
+    return 0;
+}
+
+static uint32_t uniform_slot(const srtp_dev_meta_t *m, size_t n)
+{
+    uint32_t slot = 0xffffffffu;
+    for (size_t i = 0; i < n; i++) {
+        if (SRTP_META_STATUS(m[i].info))
+            continue;
+        if (slot == 0xffffffffu)
+            slot = m[i].key;
+        else if (slot != m[i].key)
+            return 0xffffffffu;
+    }
+    return slot;
+}
+
+static uint32_t variants_of(const srtp_dev_meta_t *m, size_t n)
+{
+    uint32_t mask = 0;
+    for (size_t i = 0; i < n; i++)
+        if (!SRTP_META_STATUS(m[i].info))
+            mask |= 1u << SRTP_META_VARIANT(m[i].info);
+    return mask;
+}
+
+static int run_gpu(srtp_t ctx, int op, size_t n, const uint8_t *in,
+                   const uint64_t *in_off, uint8_t *out,
+                   const uint64_t *out_off, const srtp_dev_meta_t *h_meta,
+                   void *stream)
+{
+    srtp_gpu_batch_t b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.in = in;
+    b.in_off = in_off;
+    b.out = out;
+    b.out_off = out_off;
+    b.meta = ctx->st.d_meta;
+    b.auth_ok = ctx->st.d_auth;
+    b.uniform_key = uniform_slot(h_meta, n);
+    b.mask = variants_of(h_meta, n);
+    b.stream = stream;
+    if (!b.mask)
+        return 0;
+    if (srtp_gpu_h2d(ctx->gpu, ctx->st.d_meta, h_meta, n * sizeof *h_meta,
+                     stream))
+        return -1;
+    srtp_gpu_set_timing(ctx->gpu, ctx->timing);
+    if (srtp_gpu_run(ctx->gpu, op, &b))
+        return -1;
+    if (ctx->timing)
+        ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
+    return 0;
+}
+
+static size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+/* ------------------------------------------------------------------------
+ * batch API over host buffers
+ * ---------------------------------------------------------------------- */
+srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
+                                     const uint8_t *const *rtp,
+                                     const size_t *rtp_len,
+                                     uint8_t *const *srtp, size_t *srtp_len,
+                                     const size_t *mki_index,
+                                     srtp_err_status_t *status)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    if (!n)
+        return srtp_err_status_ok;
+    size_t arena = 0;
+    for (size_t i = 0; i < n; i++)
+        arena += r16(rtp_len[i] + SRTP_MAX_TRAILER_LEN);
+    if (stage_reserve(ctx, n, arena))
+        return srtp_err_status_alloc_fail;
+    stage_t *sg = &ctx->st;
+    size_t *olen = (size_t *)malloc(n * sizeof(size_t));
+    if (!olen)
+        return srtp_err_status_alloc_fail;
+    size_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        pkt_sum_t s;
+        summarize(rtp[i], rtp_len[i], &s);
+        srtp_dev_meta_t *m = &sg->h_meta[i];
+        memset(m, 0, sizeof *m);
+        sg->h_off[i] = off;
+        olen[i] = 0;
+        status[i] = pre_protect(ctx, &s, srtp_len[i],
+                                mki_index ? mki_index[i] : 0, m, &olen[i]);
+        if (status[i]) {
+            m->info = (uint32_t)(status[i] & 0xff) << 16;
+        } else {
+            memcpy(sg->h_arena + off, rtp[i], rtp_len[i]);
+        }
+        off += r16(rtp_len[i] + SRTP_MAX_TRAILER_LEN);
+    }
+    srtp_err_status_t ret = srtp_err_status_ok;
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, NULL) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, NULL) ||
+        run_gpu(ctx, 0, n, sg->d_arena, sg->d_off, sg->d_arena, sg->d_off,
+                sg->h_meta, NULL) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, NULL) ||
+        srtp_gpu_sync(ctx->gpu, NULL)) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        ret = srtp_err_status_fail;
+    }
+    for (size_t i = 0; i < n; i++) {
+        if (ret) {
+            status[i] = srtp_err_status_cipher_fail;
+            continue;
+        }
+        if (status[i])
+            continue;
+        memcpy(srtp[i], sg->h_arena + sg->h_off[i], olen[i]);
+        srtp_len[i] = olen[i];
+    }
+    free(olen);
+    return ret;
+}
+
+static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
+                                        const pkt_sum_t *sum, const size_t *cap,
+                                        const uint8_t *const *mki_ptr,
+                                        const uint8_t *d_in,
+                                        const uint64_t *d_in_off,
+                                        uint8_t *d_out,
+                                        const uint64_t *d_out_off,
+                                        srtp_err_status_t *status,
+                                        size_t *olen, void *stream)
+{
+    stage_t *sg = &ctx->st;
+    upkt_t *u = (upkt_t *)calloc(n, sizeof(upkt_t));
+    int *pending = (int *)malloc(n * sizeof(int));
+    if (!u || !pending) {
+        free(u);
+        free(pending);
+        return srtp_err_status_alloc_fail;
+    }
+    for (size_t i = 0; i < n; i++)
+        pending[i] = 1;
+    size_t npend = n;
+    srtp_err_status_t ret = srtp_err_status_ok;
+    while (npend) {
+        provset_t ps;
+        memset(&ps, 0, sizeof ps);
+        ctx->epoch++;
+        for (size_t i = 0; i < n; i++) {
+            srtp_dev_meta_t *m = &sg->h_meta[i];
+            memset(m, 0, sizeof *m);
+            m->info = 0xff0000u; /* skip */
+            if (!pending[i])
+                continue;
+            if (pre_unprotect(ctx, &ps, &sum[i], cap[i],
+                              mki_ptr ? mki_ptr[i] : NULL, &u[i], m))
+                m->info &= ~0xff0000u;
+            else
+                m->info |= 0xff0000u;
+        }
+        provset_free(&ps);
+        if (run_gpu(ctx, 1, n, d_in, d_in_off, d_out, d_out_off, sg->h_meta,
+                    stream) ||
+            srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, n, stream) ||
+            srtp_gpu_sync(ctx->gpu, stream)) {
+            log_msg(srtp_log_level_error, srtp_gpu_last_error());
+            ret = srtp_err_status_fail;
+            break;
+        }
+        /* exact in-order post-pass; a packet whose estimate moved is re-run
+         * together with every later packet of its SSRC */
+        uint32_t *redo_ssrc = NULL;
+        size_t nredo = 0, redo_cap = 0;
+        size_t again = 0;
+        for (size_t i = 0; i < n; i++) {
+            if (!pending[i])
+                continue;
+            int blocked = 0;
+            for (size_t r = 0; r < nredo; r++)
+                if (redo_ssrc[r] == sum[i].ssrc && !sum[i].err) {
+                    blocked = 1;
+                    break;
+                }
+            if (blocked) {
+                again++;
+                continue;
+            }
+            int auth = u[i].gpu ? sg->h_auth[i] : 0;
+            int rc = post_unprotect(ctx, &sum[i], &u[i], auth, &olen[i]);
+            if (rc < 0) {
+                if (nredo == redo_cap) {
+                    redo_cap = redo_cap ? 2 * redo_cap : 8;
+                    redo_ssrc = (uint32_t *)realloc(redo_ssrc, redo_cap * 4);
+                }
+                redo_ssrc[nredo++] = sum[i].ssrc;
+                again++;
+                continue;
+            }
+            status[i] = (srtp_err_status_t)rc;
+            pending[i] = 0;
+        }
+        free(redo_ssrc);
+        npend = again;
+        if (npend) {
+            /* packets still pending that ran speculatively were decrypted
+             * in place under their speculative index: restore them */
+            size_t nundo = 0;
+            for (size_t i = 0; i < n; i++) {
+                srtp_dev_meta_t *m = &sg->h_meta[i];
+                if (pending[i] && u[i].gpu) {
+                    nundo++;
+                } else {
+                    m->info |= 0xff0000u;
+                }
+            }
+            if (nundo && d_out != d_in) {
+                /* out of place: the input is intact, nothing to restore */
+                nundo = 0;
+            }
+            if (nundo &&
+                (srtp_gpu_h2d(ctx->gpu, sg->d_meta, sg->h_meta,
+                              n * sizeof *sg->h_meta, stream) ||
+                 srtp_gpu_undo(ctx->gpu, n, d_out, d_out_off, sg->d_meta,
+                               stream) ||
+                 srtp_gpu_sync(ctx->gpu, stream))) {
+                ret = srtp_err_status_fail;
+                break;
+            }
+        }
+    }
+    free(u);
+    free(pending);
+    return ret;
+}
+
+srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
+                                       const uint8_t *const *srtp,
+                                       const size_t *srtp_len,
+                                       uint8_t *const *rtp, size_t *rtp_len,
+                                       srtp_err_status_t *status)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    if (!n)
+        return srtp_err_status_ok;
+    size_t arena = 0;
+    for (size_t i = 0; i < n; i++)
+        arena += r16(srtp_len[i]);
+    if (stage_reserve(ctx, n, arena))
+        return srtp_err_status_alloc_fail;
+    stage_t *sg = &ctx->st;
+    pkt_sum_t *sum = (pkt_sum_t *)malloc(n * sizeof(pkt_sum_t));
+    const uint8_t **mki = (const uint8_t **)malloc(n * sizeof(void *));
+    size_t *olen = (size_t *)calloc(n, sizeof(size_t));
+    if (!sum || !mki || !olen) {
+        free(sum);
+        free(mki);
+        free(olen);
+        return srtp_err_status_alloc_fail;
+    }
+    size_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        summarize(srtp[i], srtp_len[i], &sum[i]);
+        /* MKI bytes: the stream decides its size; point at the packet and
+         * let un_static() index from the end */
+        mki[i] = NULL;
+        sg->h_off[i] = off;
+        memcpy(sg->h_arena + off, srtp[i], srtp_len[i]);
+        off += r16(srtp_len[i]);
+    }
+    /* resolve MKI pointers now that streams are known */
+    for (size_t i = 0; i < n; i++) {
+        if (sum[i].err)
+            continue;
+        const srtp_stream_ctx_t *st = map_get(ctx, sum[i].ssrc);
+        if (!st)
+            st = ctx->templ;
+        if (!st || !st->use_mki)
+            continue;
+        const hkey_t *k0 = &st->keys->k[0];
+        size_t tl = k0->family == SRTP_DEV_GCM ? 0 : k0->tag_len;
+        if (tl <= srtp_len[i] && st->mki_size <= srtp_len[i] - tl)
+            mki[i] = srtp[i] + srtp_len[i] - tl - st->mki_size;
+    }
+    srtp_err_status_t ret = srtp_err_status_ok;
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, NULL) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, NULL))
+        ret = srtp_err_status_fail;
+    if (!ret)
+        ret = unprotect_core(ctx, n, sum, rtp_len, mki, sg->d_arena, sg->d_off,
+                             sg->d_arena, sg->d_off, status, olen, NULL);
+    if (!ret && (srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, NULL) ||
+                 srtp_gpu_sync(ctx->gpu, NULL)))
+        ret = srtp_err_status_fail;
+    for (size_t i = 0; i < n; i++) {
+        if (ret) {
+            status[i] = srtp_err_status_cipher_fail;
+            continue;
+        }
+        if (status[i])
+            continue;
+        memcpy(rtp[i], sg->h_arena + sg->h_off[i], olen[i]);
+        rtp_len[i] = olen[i];
+    }
+    free(sum);
+    free(mki);
+    free(olen);
+    return ret;
+}
+
+/* single packet == batch of one (there is no CPU crypto path) */
+srtp_err_status_t srtp_protect(srtp_t ctx, const uint8_t *rtp, size_t rtp_len,
+                               uint8_t *srtp, size_t *srtp_len,
+                               size_t mki_index)
+{
+    srtp_err_status_t st;
+    srtp_err_status_t rc = srtp_protect_batch(ctx, 1, &rtp, &rtp_len, &srtp,
+                                              srtp_len, &mki_index, &st);
+    return rc ? rc : st;
+}
+
+srtp_err_status_t srtp_unprotect(srtp_t ctx, const uint8_t *srtp,
+                                 size_t srtp_len, uint8_t *rtp, size_t *rtp_len)
+{
+    srtp_err_status_t st;
+    srtp_err_status_t rc =
+        srtp_unprotect_batch(ctx, 1, &srtp, &srtp_len, &rtp, rtp_len, &st);
+    return rc ? rc : st;
+}
+
+/* ------------------------------------------------------------------------
+ * batch API over device-resident arenas
+ * ---------------------------------------------------------------------- */
+static srtp_err_status_t dev_headers(srtp_t ctx, const srtp_device_batch_t *b,
+                                     pkt_sum_t *sum, size_t *cap)
+{
+    stage_t *sg = &ctx->st;
+    if (stage_reserve(ctx, b->n, 0))
+        return srtp_err_status_alloc_fail;
+    if (srtp_gpu_parse(ctx->gpu, b->n, b->in, b->in_off, b->in_len, sg->d_hdr,
+                       b->stream) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_hdr, sg->d_hdr, b->n * sizeof *sg->h_hdr,
+                     b->stream))
+        return srtp_err_status_fail;
+    /* capacities: the caller's out_len array */
+    uint32_t *caps = (uint32_t *)sg->h_arena;
+    if (stage_reserve(ctx, b->n, b->n * 4))
+        return srtp_err_status_alloc_fail;
+    caps = (uint32_t *)sg->h_arena;
+    if (srtp_gpu_d2h(ctx->gpu, caps, b->out_len, b->n * 4, b->stream) ||
+        srtp_gpu_sync(ctx->gpu, b->stream))
+        return srtp_err_status_fail;
+    for (size_t i = 0; i < b->n; i++) {
+        from_dev_hdr(&sg->h_hdr[i], &sum[i]);
+        cap[i] = caps[i];
+    }
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
+                                     const srtp_err_status_t *status,
+                                     const size_t *olen, const size_t *cap)
+{
+    stage_t *sg = &ctx->st;
+    /* reuse the pinned arena for the two result arrays */
+    if (stage_reserve(ctx, b->n, b->n * 8))
+        return srtp_err_status_alloc_fail;
+    int32_t *hs = (int32_t *)sg->h_arena;
+    uint32_t *hl = (uint32_t *)(sg->h_arena + b->n * 4);
+    for (size_t i = 0; i < b->n; i++) {
+        hs[i] = (int32_t)status[i];
+        hl[i] = (uint32_t)(status[i] ? cap[i] : olen[i]);
+    }
+    if (srtp_gpu_h2d(ctx->gpu, b->status, hs, b->n * 4, b->stream) ||
+        srtp_gpu_h2d(ctx->gpu, b->out_len, hl, b->n * 4, b->stream) ||
+        srtp_gpu_sync(ctx->gpu, b->stream))
+        return srtp_err_status_fail;
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_protect_device(srtp_t ctx, const srtp_device_batch_t *b)
+{
+    if (!ctx || !b)
+        return srtp_err_status_bad_param;
+    if (!b->n)
+        return srtp_err_status_ok;
+    size_t n = b->n;
+    pkt_sum_t *sum = (pkt_sum_t *)malloc(n * sizeof *sum);
+    size_t *cap = (size_t *)malloc(n * sizeof(size_t));
+    size_t *olen = (size_t *)calloc(n, sizeof(size_t));
+    srtp_err_status_t *status =
+        (srtp_err_status_t *)malloc(n * sizeof(srtp_err_status_t));
+    srtp_err_status_t ret = srtp_err_status_alloc_fail;
+    if (!sum || !cap || !olen || !status)
+        goto out;
+    ret = dev_headers(ctx, b, sum, cap);
+    if (ret)
+        goto out;
+    for (size_t i = 0; i < n; i++) {
+        srtp_dev_meta_t *m = &ctx->st.h_meta[i];
+        memset(m, 0, sizeof *m);
+        status[i] = pre_protect(ctx, &sum[i], cap[i],
+                                b->mki_index ? b->mki_index[i] : 0, m, &olen[i]);
+        if (status[i])
+            m->info = (uint32_t)(status[i] & 0xff) << 16;
+    }
+    if (run_gpu(ctx, 0, n, b->in, b->in_off, b->out, b->out_off,
+                ctx->st.h_meta, b->stream)) {
+        ret = srtp_err_status_fail;
+        goto out;
+    }
+    ret = dev_results(ctx, b, status, olen, cap);
+out:
+    free(sum);
+    free(cap);
+    free(olen);
+    free(status);
+    return ret;
+}
+
+srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
+                                        const srtp_device_batch_t *b)
+{
+    if (!ctx || !b)
+        return srtp_err_status_bad_param;
+    if (!b->n)
+        return srtp_err_status_ok;
+    size_t n = b->n;
+    pkt_sum_t *sum = (pkt_sum_t *)malloc(n * sizeof *sum);
+    size_t *cap = (size_t *)malloc(n * sizeof(size_t));
+    size_t *olen = (size_t *)calloc(n, sizeof(size_t));
+    srtp_err_status_t *status =
+        (srtp_err_status_t *)calloc(n, sizeof(srtp_err_status_t));
+    uint8_t *mkibuf = NULL;
+    const uint8_t **mki = NULL;
+    srtp_err_status_t ret = srtp_err_status_alloc_fail;
+    if (!sum || !cap || !olen || !status)
+        goto out;
+    ret = dev_headers(ctx, b, sum, cap);
+    if (ret)
+        goto out;
+    /* MKI streams: fetch each packet's MKI bytes (rare; small copies) */
+    {
+        int any_mki = ctx->templ && ctx->templ->use_mki;
+        for (size_t i = 0; i < ctx->n && !any_mki; i++)
+            any_mki = ctx->list[i]->use_mki;
+        if (any_mki) {
+            mki = (const uint8_t **)calloc(n, sizeof(void *));
+            mkibuf = (uint8_t *)calloc(n, SRTP_MAX_MKI_LEN);
+            uint64_t *offs = (uint64_t *)malloc(n * 8);
+            ret = srtp_err_status_alloc_fail;
+            if (!mki || !mkibuf || !offs) {
+                free(offs);
+                goto out;
+            }
+            ret = srtp_err_status_fail;
+            if (srtp_gpu_d2h(ctx->gpu, offs, b->in_off, n * 8, b->stream) ||
+                srtp_gpu_sync(ctx->gpu, b->stream)) {
+                free(offs);
+                goto out;
+            }
+            for (size_t i = 0; i < n; i++) {
+                if (sum[i].err)
+                    continue;
+                const srtp_stream_ctx_t *st = map_get(ctx, sum[i].ssrc);
+                if (!st)
+                    st = ctx->templ;
+                if (!st || !st->use_mki)
+                    continue;
+                const hkey_t *k0 = &st->keys->k[0];
+                size_t tl = k0->family == SRTP_DEV_GCM ? 0 : k0->tag_len;
+                if (tl > sum[i].len || st->mki_size > sum[i].len - tl)
+                    continue;
+                size_t at = sum[i].len - tl - st->mki_size;
+                if (srtp_gpu_d2h(ctx->gpu, mkibuf + i * SRTP_MAX_MKI_LEN,
+                                 b->in + offs[i] + at, st->mki_size,
+                                 b->stream)) {
+                    free(offs);
+                    goto out;
+                }
+                mki[i] = mkibuf + i * SRTP_MAX_MKI_LEN;
+            }
+            free(offs);
+            if (srtp_gpu_sync(ctx->gpu, b->stream))
+                goto out;
+        }
+    }
+    ret = unprotect_core(ctx, n, sum, cap, mki, b->in, b->in_off, b->out,
+                         b->out_off, status, olen, b->stream);
+    if (!ret)
+        ret = dev_results(ctx, b, status, olen, cap);
+out:
+    free(sum);
+    free(cap);
+    free(olen);
+    free(status);
+    free(mkibuf);
+    free((void *)mki);
+    return ret;
+}
+
+/* ------------------------------------------------------------------------
+ * RTCP (not on the GPU path yet)
+ * ---------------------------------------------------------------------- */
+srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
+                                    size_t rtcp_len, uint8_t *srtcp,
+                                    size_t *srtcp_len, size_t mki_index)
+{
+    (void)ctx;
+    (void)rtcp;
+    (void)rtcp_len;
+    (void)srtcp;
+    (void)srtcp_len;
+    (void)mki_index;
+    return srtp_err_status_no_such_op;
+}
+
+srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
+                                      size_t srtcp_len, uint8_t *rtcp,
+                                      size_t *rtcp_len)
+{
+    (void)ctx;
+    (void)srtcp;
+    (void)srtcp_len;
+    (void)rtcp;
+    (void)rtcp_len;
+    return srtp_err_status_no_such_op;
+}
+
+/* ------------------------------------------------------------------------
+ * policies and profiles (srtp.c:3665-3860, 4848-4970)
+ * ---------------------------------------------------------------------- */
+static void setp(srtp_crypto_policy_t *p, uint32_t c, size_t ckl, uint32_t a,
+                 size_t akl, size_t tag, srtp_sec_serv_t sv)
+{
+    p->cipher_type = c;
+    p->cipher_key_len = ckl;
+    p->auth_type = a;
+    p->auth_key_len = akl;
+    p->auth_tag_len = tag;
+    p->sec_serv = sv;
+}
+
+void srtp_crypto_policy_set_rtp_default(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_128, 30, SRTP_HMAC_SHA1, 20, 10, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_rtcp_default(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_128, 30, SRTP_HMAC_SHA1, 20, 10, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_cm_128_hmac_sha1_32(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_128, 30, SRTP_HMAC_SHA1, 20, 4, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_cm_128_null_auth(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_128, 30, SRTP_NULL_AUTH, 0, 0, sec_serv_conf);
+}
+void srtp_crypto_policy_set_null_cipher_hmac_sha1_80(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_NULL_CIPHER, 30, SRTP_HMAC_SHA1, 20, 10, sec_serv_auth);
+}
+void srtp_crypto_policy_set_null_cipher_hmac_null(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_NULL_CIPHER, 0, SRTP_NULL_AUTH, 0, 0, sec_serv_none);
+}
+void srtp_crypto_policy_set_aes_cm_256_hmac_sha1_80(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_256, 46, SRTP_HMAC_SHA1, 20, 10, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_cm_256_hmac_sha1_32(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_256, 46, SRTP_HMAC_SHA1, 20, 4, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_cm_256_null_auth(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_256, 46, SRTP_NULL_AUTH, 0, 0, sec_serv_conf);
+}
+void srtp_crypto_policy_set_aes_cm_192_hmac_sha1_80(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_192, 38, SRTP_HMAC_SHA1, 20, 10, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_cm_192_hmac_sha1_32(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_192, 38, SRTP_HMAC_SHA1, 20, 4, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_cm_192_null_auth(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_ICM_192, 38, SRTP_NULL_AUTH, 0, 0, sec_serv_conf);
+}
+void srtp_crypto_policy_set_aes_gcm_128_16_auth(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_GCM_128, 28, SRTP_NULL_AUTH, 0, 16, sec_serv_conf_and_auth);
+}
+void srtp_crypto_policy_set_aes_gcm_256_16_auth(srtp_crypto_policy_t *p)
+{
+    setp(p, SRTP_AES_GCM_256, 44, SRTP_NULL_AUTH, 0, 16, sec_serv_conf_and_auth);
+}
+
+srtp_err_status_t srtp_crypto_policy_set_from_profile_for_rtp(
+    srtp_crypto_policy_t *policy, srtp_profile_t profile)
+{
+    switch (profile) {
+    case srtp_profile_aes128_cm_sha1_80:
+        srtp_crypto_policy_set_rtp_default(policy);
+        break;
+    case srtp_profile_aes128_cm_sha1_32:
+        srtp_crypto_policy_set_aes_cm_128_hmac_sha1_32(policy);
+        break;
+    case srtp_profile_null_sha1_80:
+        srtp_crypto_policy_set_null_cipher_hmac_sha1_80(policy);
+        break;
+    case srtp_profile_aead_aes_128_gcm:
+        srtp_crypto_policy_set_aes_gcm_128_16_auth(policy);
+        break;
+    case srtp_profile_aead_aes_256_gcm:
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(policy);
+        break;
+    default:
+        return srtp_err_status_bad_param;
+    }
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_crypto_policy_set_from_profile_for_rtcp(
+    srtp_crypto_policy_t *policy, srtp_profile_t profile)
+{
+    switch (profile) {
+    case srtp_profile_aes128_cm_sha1_80:
+    case srtp_profile_aes128_cm_sha1_32: /* 32-bit RTCP tags not honoured */
+        srtp_crypto_policy_set_rtp_default(policy);
+        break;
+    case srtp_profile_null_sha1_80:
+        srtp_crypto_policy_set_null_cipher_hmac_sha1_80(policy);
+        break;
+    case srtp_profile_aead_aes_128_gcm:
+        srtp_crypto_policy_set_aes_gcm_128_16_auth(policy);
+        break;
+    case srtp_profile_aead_aes_256_gcm:
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(policy);
+        break;
+    default:
+        return srtp_err_status_bad_param;
+    }
+    return srtp_err_status_ok;
+}
+
+void srtp_append_salt_to_key(uint8_t *key, size_t bytes_in_key, uint8_t *salt,
+                             size_t bytes_in_salt)
+{
+    memcpy(key + bytes_in_key, salt, bytes_in_salt);
+}
+
+size_t srtp_profile_get_master_key_length(srtp_profile_t profile)
+{
+    switch (profile) {
+    case srtp_profile_aes128_cm_sha1_80:
+    case srtp_profile_aes128_cm_sha1_32:
+    case srtp_profile_null_sha1_80:
+    case srtp_profile_aead_aes_128_gcm:
+        return SRTP_AES_128_KEY_LEN;
+    case srtp_profile_aead_aes_256_gcm:
+        return SRTP_AES_256_KEY_LEN;
+    default:
+        return 0;
+    }
+}
+
+size_t srtp_profile_get_master_salt_length(srtp_profile_t profile)
+{
+    switch (profile) {
+    case srtp_profile_aes128_cm_sha1_80:
+    case srtp_profile_aes128_cm_sha1_32:
+    case srtp_profile_null_sha1_80:
+        return SRTP_SALT_LEN;
+    case srtp_profile_aead_aes_128_gcm:
+    case srtp_profile_aead_aes_256_gcm:
+        return SRTP_AEAD_SALT_LEN;
+    default:
+        return 0;
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * misc
+ * ---------------------------------------------------------------------- */
+void srtp_set_user_data(srtp_t ctx, void *data) { ctx->user_data = data; }
+void *srtp_get_user_data(srtp_t ctx) { return ctx->user_data; }
+
+srtp_err_status_t srtp_install_event_handler(srtp_event_handler_func_t func)
+{
+    g_event_handler = func; /* NULL allowed, srtp.c:1762-1772 */
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_install_log_handler(srtp_log_handler_func_t func,
+                                           void *data)
+{
+    g_log_handler = func;
+    g_log_data = data;
+    return srtp_err_status_ok;
+}
+
+const char *srtp_get_version_string(void)
+{
+    return "libsrtp3 3.0.0 (libsrtp_mi355x)";
+}
+
+unsigned int srtp_get_version(void) { return (3u << 24) | (0u << 16) | 0u; }
+
+srtp_err_status_t srtp_set_debug_module(const char *mod_name, bool v)
+{
+    (void)v;
+    return mod_name ? srtp_err_status_ok : srtp_err_status_bad_param;
+}
+
+srtp_err_status_t srtp_list_debug_modules(void) { return srtp_err_status_ok; }
+
+static srtp_err_status_t trailer_of(const srtp_stream_ctx_t *s, int is_rtp,
+                                    size_t mki_index, size_t *len)
+{
+    /* stream_get_protect_trailer_length, srtp.c:4972-5000 */
+    const hkey_t *k;
+    *len = 0;
+    if (s->use_mki) {
+        if (mki_index >= s->keys->n)
+            return srtp_err_status_bad_mki;
+        k = &s->keys->k[mki_index];
+        *len += s->mki_size;
+    } else {
+        k = &s->keys->k[0];
+    }
+    *len += k->tag_len;
+    if (!is_rtp)
+        *len += 4; /* srtcp_trailer_t */
+    return srtp_err_status_ok;
+}
+
+static srtp_err_status_t trailer_len(srtp_t ctx, int is_rtp, size_t mki_index,
+                                     size_t *length)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    int found = 0;
+    size_t best = 0, t;
+    if (ctx->templ) {
+        found = 1;
+        trailer_of(ctx->templ, is_rtp, mki_index, &best);
+    }
+    for (size_t i = 0; i < ctx->n; i++)
+        if (trailer_of(ctx->list[i], is_rtp, mki_index, &t) ==
+            srtp_err_status_ok) {
+            found = 1;
+            if (t > best)
+                best = t;
+        }
+    if (!found)
+        return srtp_err_status_bad_param;
+    *length = best;
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_get_protect_trailer_length(srtp_t session,
+                                                  size_t mki_index,
+                                                  size_t *length)
+{
+    return trailer_len(session, 1, mki_index, length);
+}
+
+srtp_err_status_t srtp_get_protect_rtcp_trailer_length(srtp_t session,
+                                                       size_t mki_index,
+                                                       size_t *length)
+{
+    return trailer_len(session, 0, mki_index, length);
+}
+
+srtp_err_status_t srtp_stream_set_roc(srtp_t session, uint32_t ssrc,
+                                      uint32_t roc)
+{
+    srtp_stream_ctx_t *s = session ? map_get(session, ssrc) : NULL;
+    if (!s)
+        return srtp_err_status_bad_param;
+    s->rdbx.pending_roc = roc;
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_stream_get_roc(srtp_t session, uint32_t ssrc,
+                                      uint32_t *roc)
+{
+    srtp_stream_ctx_t *s = session ? map_get(session, ssrc) : NULL;
+    if (!s)
+        return srtp_err_status_bad_param;
+    *roc = (uint32_t)(s->rdbx.index >> 16);
+    return srtp_err_status_ok;
+}
+
+void srtp_mi355x_set_timing(srtp_t ctx, int on)
+{
+    if (ctx)
+        ctx->timing = on;
+}
+
+double srtp_mi355x_last_kernel_ms(srtp_t ctx) { return ctx ? ctx->last_ms : 0; }
+
+int srtp_mi355x_gpu_available(void) { return srtp_gpu_available(); }
+
+/* Test hook (no GPU): drives the protect pre-pass index / replay logic of a
+ * fresh stream over a sequence of sequence numbers, as srtp_protect would
+ * (srtp.c:2662-2690).  pending_roc != 0 emulates srtp_stream_set_roc()
+ * before the first packet.  Returns per packet the status and the estimated
+ * 48-bit index (0 on error). */
+int srtp_mi355x_debug_index(size_t window, int allow_repeat_tx,
+                            uint32_t pending_roc, size_t n,
+                            const uint16_t *seq, int32_t *status,
+                            uint64_t *est_out)
+{
+    rdbx_t r;
+    if (rdbx_init(&r, window ? window : 128))
+        return -1;
+    r.pending_roc = pending_roc;
+    for (size_t i = 0; i < n; i++) {
+        uint64_t est = 0;
+        int64_t delta = 0;
+        srtp_err_status_t rc = estimate(&r, seq[i], &est, &delta);
+        est_out[i] = 0;
+        if (rc && rc != srtp_err_status_pkt_idx_adv) {
+            status[i] = rc;
+            continue;
+        }
+        if (rc == srtp_err_status_pkt_idx_adv) {
+            rdbx_accept(&r, est, 0, 1);
+        } else {
+            rc = rdbx_check(&r, delta);
+            if (rc && (rc != srtp_err_status_replay_fail || !allow_repeat_tx)) {
+                status[i] = rc;
+                continue;
+            }
+            rdbx_add(&r, delta);
+        }
+        status[i] = 0;
+        est_out[i] = est;
+    }
+    free(r.w);
+    return 0;
+}

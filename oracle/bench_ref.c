@@ -1,0 +1,107 @@
+/*
+ * bench_ref.c -- CPU baseline driver (test infrastructure): times the
+ * REFERENCE (oracle/_ref/libsrtp_ref_*.so, cisco/libsrtp built from its own
+ * sources) calling srtp_protect() once per packet, T threads with one
+ * srtp_t each, like BASELINE.md's probe.  Each thread cycles over a pool of
+ * distinct packet buffers, protecting in place with seq += 1.
+ *
+ * int ref_bench(int threads, long pkts_per_thread, int payload,
+ *               int gcm, double *seconds)  -> packets protected
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "srtp.h"
+
+typedef struct {
+    long n;
+    int payload, gcm, pool;
+    long done;
+} job_t;
+
+static const uint8_t key46[46] = {
+    0xe1, 0xf9, 0x7a, 0x0d, 0x3e, 0x01, 0x8b, 0xe0, 0xd6, 0x4f, 0xa3, 0x2c,
+    0x06, 0xde, 0x41, 0x39, 0x0e, 0xc6, 0x75, 0xad, 0x49, 0x8a, 0xfe, 0xeb,
+    0xb6, 0x96, 0x0b, 0x3a, 0xab, 0xe6, 0xc1, 0x73, 0xc3, 0x17, 0xf2, 0xda,
+    0xbe, 0x35, 0x77, 0x93, 0xb6, 0x96, 0x0b, 0x3a, 0xab, 0xe6 };
+
+static void *run(void *arg)
+{
+    job_t *j = (job_t *)arg;
+    srtp_policy_t p;
+    srtp_t s;
+    memset(&p, 0, sizeof p);
+    if (j->gcm) {
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(&p.rtp);
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(&p.rtcp);
+    } else {
+        srtp_crypto_policy_set_rtp_default(&p.rtp);
+        srtp_crypto_policy_set_rtcp_default(&p.rtcp);
+    }
+    p.ssrc.type = ssrc_any_outbound;
+    p.key = (uint8_t *)key46;
+    p.window_size = 128;
+    if (srtp_create(&s, &p))
+        return NULL;
+    size_t slot = (size_t)(12 + j->payload + 64 + 63) & ~(size_t)63;
+    uint8_t *buf = (uint8_t *)aligned_alloc(64, slot * (size_t)j->pool);
+    uint64_t x = 0x5352545030303031ULL ^ (uint64_t)(uintptr_t)j;
+    for (size_t i = 0; i < slot * (size_t)j->pool; i++) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        buf[i] = (uint8_t)x;
+    }
+    uint16_t seq = 0x1234;
+    for (long i = 0; i < j->n; i++) {
+        uint8_t *pk = buf + slot * (size_t)(i % j->pool);
+        pk[0] = 0x80;
+        pk[1] = 96;
+        pk[2] = (uint8_t)(seq >> 8);
+        pk[3] = (uint8_t)seq;
+        pk[8] = 0xca; pk[9] = 0xfe; pk[10] = 0xba; pk[11] = 0xbe;
+        size_t len = slot;
+        if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0)
+            j->done++;
+        seq++;
+    }
+    free(buf);
+    srtp_dealloc(s);
+    return NULL;
+}
+
+int ref_bench(int threads, long pkts_per_thread, int payload, int gcm,
+              double *seconds)
+{
+    static int inited;
+    if (!inited) {
+        if (srtp_init())
+            return -1;
+        inited = 1;
+    }
+    pthread_t th[256];
+    job_t jobs[256];
+    if (threads > 256)
+        threads = 256;
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int t = 0; t < threads; t++) {
+        jobs[t].n = pkts_per_thread;
+        jobs[t].payload = payload;
+        jobs[t].gcm = gcm;
+        jobs[t].pool = 4096;
+        jobs[t].done = 0;
+        pthread_create(&th[t], NULL, run, &jobs[t]);
+    }
+    long done = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        done += jobs[t].done;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    return (int)done;
+}

@@ -125,16 +125,17 @@ class Session:
         pol.ssrc_type = p["ssrc_type"]
         pol.ssrc = p["ssrc"]
         for f in ("cipher_type", "cipher_key_len", "auth_type",
-                  "auth_key_len", "auth_tag_len", "sec_serv", "mki_size",
-                  "window_size"):
+                  "auth_key_len", "auth_tag_len", "sec_serv"):
             setattr(pol, f, p[f])
-        pol.use_mki = int(p["use_mki"])
-        pol.allow_repeat_tx = int(p["allow_repeat_tx"])
+        pol.mki_size = p.get("mki_size", 0)
+        pol.window_size = p.get("window_size", 128)
+        pol.use_mki = int(p.get("use_mki", 0))
+        pol.allow_repeat_tx = int(p.get("allow_repeat_tx", 0))
         keys = [bytes.fromhex(k) if isinstance(k, str) else bytes(k)
                 for k in p["keys"]]
         mkis = [bytes.fromhex(k) if isinstance(k, str) else bytes(k)
                 for k in p.get("mki_ids", [])]
-        pol.num_master_keys = len(keys) if p["use_mki"] else 1
+        pol.num_master_keys = len(keys) if pol.use_mki else 1
         for i, k in enumerate(keys[:pol.num_master_keys]):
             b = C.create_string_buffer(k, max(64, len(k)))
             self._keep.append(b)

@@ -607,7 +607,7 @@ static int derive_keys(session_keys_t *sk, const uint8_t *master,
     uint8_t kdf_salt[14];
     memcpy(kdf_salt, tmp + kdf_keylen - 14, 14);
 
-    uint8_t ek[32], salt[14] = { 0 }, ak[20];
+    uint8_t ek[32], salt[32] = { 0 }, ak[20];
     kdf_gen(&kdf, kdf_salt, 0x00, ek, base);
     if (salt_len > 0)
         kdf_gen(&kdf, kdf_salt, 0x02, salt, salt_len);
@@ -615,7 +615,7 @@ static int derive_keys(session_keys_t *sk, const uint8_t *master,
     sk->cipher_key_len = cipher_key_len;
     sk->enc_key_len = base;
     memset(sk->salt, 0, sizeof sk->salt);
-    memcpy(sk->salt, salt, salt_len);
+    memcpy(sk->salt, salt, salt_len < 14 ? salt_len : 14);
     if (base)
         aes_expand(&sk->aes, ek, base);
     kdf_gen(&kdf, kdf_salt, 0x01, ak, auth_key_len);
