@@ -60,18 +60,48 @@ constexpr int GH_LDS_BYTES = 256 * 16 * 16;
 
 __device__ uint2 g_ttab[256];   // (T0[x], T1[x]) little-endian words
 
-DEV void load_aes_table(uint2 *lds)
+// LDS image of the AES tables, 64 KiB: for byte value x the 256-byte row
+// x holds T0[x] 32 times (bytes 0..127) then T1[x] 32 times (128..255).
+// Lane l reads copy (l & 31): a ds_read_b32 of 32 lanes touches 32 distinct
+// banks whatever the byte values are, i.e. it is never bank-conflicted.
+DEV void load_aes_table(uint2 *lds2)
 {
-    for (int e = threadIdx.x; e < 256 * 32; e += blockDim.x)
-        lds[e] = g_ttab[e >> 5];
+    uint32_t *lds = (uint32_t *)lds2;
+    for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
+        uint2 t = g_ttab[e >> 6];
+        lds[e] = (e & 32) ? t.y : t.x;
+    }
+}
+
+struct AesLds {
+    const char *lds;
+    uint32_t l0;   // (lane & 31) * 4        -> T0 copy of this lane
+    uint32_t l1;   // (lane & 31) * 4 | 128  -> T1 copy of this lane
+};
+
+DEV AesLds make_aes_lds(const void *lds)
+{
+    AesLds T;
+    T.lds = (const char *)lds;
+    T.l0 = (threadIdx.x & 31) * 4;
+    T.l1 = T.l0 | 128u;
+    return T;
+}
+
+// byte K of w -> address bits 15:8, the lane's copy offset -> bits 7:0: one
+// v_perm_b32 per lookup
+template <int K>
+DEV uint32_t t0(const AesLds &T, uint32_t w)
+{
+    uint32_t a = __builtin_amdgcn_perm(w, T.l0, 0x0c0c0000u | ((4u + K) << 8));
+    return *(const uint32_t *)(T.lds + a);
 }
 
 template <int K>
-DEV uint2 tlut(const char *lds, uint32_t w, uint32_t lane8)
+DEV uint32_t t1(const AesLds &T, uint32_t w)
 {
-    // byte K of w -> address bits 15:8, lane copy offset -> bits 7:0
-    uint32_t a = __builtin_amdgcn_perm(w, lane8, 0x0c0c0000u | ((4u + K) << 8));
-    return *(const uint2 *)(lds + a);
+    uint32_t a = __builtin_amdgcn_perm(w, T.l1, 0x0c0c0000u | ((4u + K) << 8));
+    return *(const uint32_t *)(T.lds + a);
 }
 
 // ---------------------------------------------------------------------------
@@ -95,10 +125,13 @@ struct UniKey {
     DEV uint32_t operator()(int i) const { return k->rk[i]; }
 };
 
-// AES encryption of one block held as little-endian words.
+// AES encryption of one block held as little-endian words (column c =
+// bytes 4c..4c+3).  Round: col_c = T0[s_c.b0] ^ T1[s_c+1.b1]
+//                                ^ rot16(T0[s_c+2.b2] ^ T1[s_c+3.b3]) ^ rk
+// with T2 = rot16(T0), T3 = rot16(T1).  16 ds_read_b32 + 32 VALU per round.
 template <int NR, class KEY>
 DEV void aes_block(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3,
-                   const KEY &rk, const char *lds, uint32_t lane8)
+                   const KEY &rk, const AesLds &T)
 {
     s0 ^= rk(0);
     s1 ^= rk(1);
@@ -106,45 +139,45 @@ DEV void aes_block(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3,
     s3 ^= rk(3);
 #pragma unroll
     for (int r = 1; r < NR; r++) {
-        uint2 a0 = tlut<0>(lds, s0, lane8), a1 = tlut<0>(lds, s1, lane8),
-              a2 = tlut<0>(lds, s2, lane8), a3 = tlut<0>(lds, s3, lane8);
-        uint2 b0 = tlut<1>(lds, s0, lane8), b1 = tlut<1>(lds, s1, lane8),
-              b2 = tlut<1>(lds, s2, lane8), b3 = tlut<1>(lds, s3, lane8);
-        uint2 c0 = tlut<2>(lds, s0, lane8), c1 = tlut<2>(lds, s1, lane8),
-              c2 = tlut<2>(lds, s2, lane8), c3 = tlut<2>(lds, s3, lane8);
-        uint2 d0 = tlut<3>(lds, s0, lane8), d1 = tlut<3>(lds, s1, lane8),
-              d2 = tlut<3>(lds, s2, lane8), d3 = tlut<3>(lds, s3, lane8);
-        uint32_t t0 = xor3(a0.x, b1.y, rk(4 * r + 0)) ^ rotl(c2.x ^ d3.y, 16);
-        uint32_t t1 = xor3(a1.x, b2.y, rk(4 * r + 1)) ^ rotl(c3.x ^ d0.y, 16);
-        uint32_t t2 = xor3(a2.x, b3.y, rk(4 * r + 2)) ^ rotl(c0.x ^ d1.y, 16);
-        uint32_t t3 = xor3(a3.x, b0.y, rk(4 * r + 3)) ^ rotl(c1.x ^ d2.y, 16);
-        s0 = t0;
-        s1 = t1;
-        s2 = t2;
-        s3 = t3;
+        uint32_t a0 = t0<0>(T, s0), a1 = t0<0>(T, s1), a2 = t0<0>(T, s2),
+                 a3 = t0<0>(T, s3);
+        uint32_t b0 = t1<1>(T, s0), b1 = t1<1>(T, s1), b2 = t1<1>(T, s2),
+                 b3 = t1<1>(T, s3);
+        uint32_t c0 = t0<2>(T, s0), c1 = t0<2>(T, s1), c2 = t0<2>(T, s2),
+                 c3 = t0<2>(T, s3);
+        uint32_t d0 = t1<3>(T, s0), d1 = t1<3>(T, s1), d2 = t1<3>(T, s2),
+                 d3 = t1<3>(T, s3);
+        uint32_t n0 = xor3(a0, b1, rk(4 * r + 0)) ^ rotl(c2 ^ d3, 16);
+        uint32_t n1 = xor3(a1, b2, rk(4 * r + 1)) ^ rotl(c3 ^ d0, 16);
+        uint32_t n2 = xor3(a2, b3, rk(4 * r + 2)) ^ rotl(c0 ^ d1, 16);
+        uint32_t n3 = xor3(a3, b0, rk(4 * r + 3)) ^ rotl(c1 ^ d2, 16);
+        s0 = n0;
+        s1 = n1;
+        s2 = n2;
+        s3 = n3;
     }
     // final round: S[x] is byte 1 of T0[x] and byte 2 of T1[x]
-    uint2 a0 = tlut<0>(lds, s0, lane8), a1 = tlut<0>(lds, s1, lane8),
-          a2 = tlut<0>(lds, s2, lane8), a3 = tlut<0>(lds, s3, lane8);
-    uint2 b0 = tlut<1>(lds, s0, lane8), b1 = tlut<1>(lds, s1, lane8),
-          b2 = tlut<1>(lds, s2, lane8), b3 = tlut<1>(lds, s3, lane8);
-    uint2 c0 = tlut<2>(lds, s0, lane8), c1 = tlut<2>(lds, s1, lane8),
-          c2 = tlut<2>(lds, s2, lane8), c3 = tlut<2>(lds, s3, lane8);
-    uint2 d0 = tlut<3>(lds, s0, lane8), d1 = tlut<3>(lds, s1, lane8),
-          d2 = tlut<3>(lds, s2, lane8), d3 = tlut<3>(lds, s3, lane8);
+    uint32_t a0 = t0<0>(T, s0), a1 = t0<0>(T, s1), a2 = t0<0>(T, s2),
+             a3 = t0<0>(T, s3);
+    uint32_t b0 = t1<1>(T, s0), b1 = t1<1>(T, s1), b2 = t1<1>(T, s2),
+             b3 = t1<1>(T, s3);
+    uint32_t c0 = t0<2>(T, s0), c1 = t0<2>(T, s1), c2 = t0<2>(T, s2),
+             c3 = t0<2>(T, s3);
+    uint32_t d0 = t1<3>(T, s0), d1 = t1<3>(T, s1), d2 = t1<3>(T, s2),
+             d3 = t1<3>(T, s3);
     const uint32_t LO = 0x0c0c0601u, HI = 0x06010c0cu;
-    uint32_t t0 = xor3(__builtin_amdgcn_perm(b1.y, a0.x, LO),
-                       __builtin_amdgcn_perm(d3.y, c2.x, HI), rk(4 * NR + 0));
-    uint32_t t1 = xor3(__builtin_amdgcn_perm(b2.y, a1.x, LO),
-                       __builtin_amdgcn_perm(d0.y, c3.x, HI), rk(4 * NR + 1));
-    uint32_t t2 = xor3(__builtin_amdgcn_perm(b3.y, a2.x, LO),
-                       __builtin_amdgcn_perm(d1.y, c0.x, HI), rk(4 * NR + 2));
-    uint32_t t3 = xor3(__builtin_amdgcn_perm(b0.y, a3.x, LO),
-                       __builtin_amdgcn_perm(d2.y, c1.x, HI), rk(4 * NR + 3));
-    s0 = t0;
-    s1 = t1;
-    s2 = t2;
-    s3 = t3;
+    uint32_t n0 = xor3(__builtin_amdgcn_perm(b1, a0, LO),
+                       __builtin_amdgcn_perm(d3, c2, HI), rk(4 * NR + 0));
+    uint32_t n1 = xor3(__builtin_amdgcn_perm(b2, a1, LO),
+                       __builtin_amdgcn_perm(d0, c3, HI), rk(4 * NR + 1));
+    uint32_t n2 = xor3(__builtin_amdgcn_perm(b3, a2, LO),
+                       __builtin_amdgcn_perm(d1, c0, HI), rk(4 * NR + 2));
+    uint32_t n3 = xor3(__builtin_amdgcn_perm(b0, a3, LO),
+                       __builtin_amdgcn_perm(d2, c1, HI), rk(4 * NR + 3));
+    s0 = n0;
+    s1 = n1;
+    s2 = n2;
+    s3 = n3;
 }
 
 // ---------------------------------------------------------------------------
@@ -267,15 +300,80 @@ struct IcmArgs {
     uint32_t uni;   // uniform key slot
 };
 
+#ifndef ICM_WAVES_PER_SIMD
+#define ICM_WAVES_PER_SIMD 1
+#endif
+
+// one 64-byte chunk of packet b on the general path: header words, the
+// packet tail, the ROC / padding / length words of the SHA-1 message
+template <int NR, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_chunk_generic(uint32_t b, const uint8_t *in, uint8_t *out,
+                           uint32_t L, uint32_t P, uint32_t hw, uint32_t s,
+                           uint32_t qoff, uint32_t nq, uint32_t nb, bool conf,
+                           uint32_t roc, const uint32_t cb[4], const KEY &rk,
+                           const AesLds &T, uint32_t ks_prev[4],
+                           uint32_t hst[5])
+{
+    uint32_t wv[16];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t q = 4 * b + t;
+        u32x4 v = { 0, 0, 0, 0 };
+        if (q < nq)
+            v = *(const u32x4 *)(in + 16 * q);
+        uint32_t ks_cur[4] = { 0, 0, 0, 0 };
+        const int j = (int)q - (int)qoff;
+        if (conf && j >= 0 && (uint32_t)(16 * j) < P) {
+            uint32_t jj = (uint32_t)j;
+            uint32_t x0 = cb[0], x1 = cb[1], x2 = cb[2],
+                     x3 = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+            aes_block<NR ? NR : 1>(x0, x1, x2, x3, rk, T);
+            ks_cur[0] = x0;
+            ks_cur[1] = x1;
+            ks_cur[2] = x2;
+            ks_cur[3] = x3;
+        }
+        uint32_t ks[4];
+        ks_shift(ks_prev, ks_cur, s, ks);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            if (4 * q + u < hw)
+                ks[u] = 0;   // header words are never encrypted
+        uint32_t o[4] = { v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3] };
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[u]);
+        if (16 * q + 16 <= L) {
+            u32x4 ov = { o[0], o[1], o[2], o[3] };
+            *(u32x4 *)(out + 16 * q) = ov;
+        } else if (16 * q < L) {
+            store_words_partial(out + 16 * q, o, (int)(L - 16 * q));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            ks_prev[u] = ks_cur[u];
+    }
+    if (AUTH) {
+#pragma unroll
+        for (int g = 0; g < 16; g++)
+            wv[g] = tail_word(wv[g], (int)L - (int)(64 * b + 4 * g), roc);
+        if (b == nb - 1) {
+            wv[14] = 0;
+            wv[15] = (64 + L + 4) * 8;
+        }
+        sha1_compress(hst, wv);
+    }
+}
+
+// AES-ICM + HMAC-SHA1 protect / unprotect: one lane per packet.
 template <int NR, bool AUTH, bool PROTECT, bool UNIFORM>
-__global__ __launch_bounds__(512) void k_icm_hmac(IcmArgs A)
+__global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
 {
     __shared__ uint2 s_tab[256 * 32];
     if (NR)
         load_aes_table(s_tab);
     __syncthreads();
-    const char *lds = (const char *)s_tab;
-    const uint32_t lane8 = (threadIdx.x & 31) * 8;
+    const AesLds T = make_aes_lds(s_tab);
 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.n)
@@ -299,94 +397,72 @@ __global__ __launch_bounds__(512) void k_icm_hmac(IcmArgs A)
     const uint32_t L = m.len;                 // end of auth'd region
     const uint32_t P = L - enc_start;          // bytes to en/decrypt
     const uint32_t hw = enc_start >> 2, s = hw & 3, qoff = hw >> 2;
-    const uint32_t tag_len = key->tag_len;
-    const uint32_t mki_size = key->mki_size;
     const bool conf = NR != 0 && key->conf != 0;
 
     // counter block (little-endian words), block counter j in bytes 14..15
-    uint32_t w0 = *(const uint32_t *)in;
-    uint32_t w2 = *(const uint32_t *)(in + 8);   // SSRC bytes
-    uint32_t seq = bswap(w0) & 0xffffu;
-    uint32_t cb0 = key->salt[0];
-    uint32_t cb1 = key->salt[1] ^ w2;
-    uint32_t cb2 = key->salt[2] ^ bswap(m.roc);
-    uint32_t cb3 = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
+    const uint32_t w0 = *(const uint32_t *)in;
+    const uint32_t seq = bswap(w0) & 0xffffu;
+    uint32_t cb[4];
+    cb[0] = key->salt[0];
+    cb[1] = key->salt[1] ^ *(const uint32_t *)(in + 8);   // SSRC bytes
+    cb[2] = key->salt[2] ^ bswap(m.roc);
+    cb[3] = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
 
     uint32_t hst[5];
-    if (AUTH) {
 #pragma unroll
-        for (int k = 0; k < 5; k++)
-            hst[k] = key->ipad[k];
-    }
+    for (int k = 0; k < 5; k++)
+        hst[k] = AUTH ? key->ipad[k] : 0;
 
     uint32_t ks_prev[4] = { 0, 0, 0, 0 };
-    const uint32_t nq = (L + 15) >> 4;                 // quads holding data
+    const uint32_t nq = (L + 15) >> 4;             // quads holding data
     const uint32_t nb = AUTH ? ((L + 12) >> 6) + 1 : ((nq + 3) >> 2);
-    const uint32_t nfull = L >> 6;
+    const uint32_t nfull = L >> 6;                 // chunks of pure data
+    const uint32_t bclean = (qoff + 4) >> 2;       // first chunk past header
 
     for (uint32_t b = 0; b < nb; b++) {
-        uint32_t wv[16];
-        const bool full = b < nfull;
+        if (b >= bclean && b < nfull) {
+            // steady state: 64 bytes of payload, no header, no tail --
+            // 4 AES blocks, XOR, 64-byte store, one SHA-1 compression
+            const uint8_t *ip = in + 64 * b;
+            uint8_t *op = out + 64 * b;
+            uint32_t wv[16];
 #pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const uint32_t q = 4 * b + t;
-            u32x4 v = { 0, 0, 0, 0 };
-            if (full || q < nq)
-                v = *(const u32x4 *)(in + 16 * q);
-            uint32_t ks_cur[4] = { 0, 0, 0, 0 };
-            const int j = (int)q - (int)qoff;
-            if (conf && j >= 0 && (uint32_t)(16 * j) < P) {
-                uint32_t jj = (uint32_t)j;
-                uint32_t x0 = cb0, x1 = cb1, x2 = cb2,
-                         x3 = cb3 ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
-                aes_block<NR ? NR : 1>(x0, x1, x2, x3, rk, lds, lane8);
-                ks_cur[0] = x0;
-                ks_cur[1] = x1;
-                ks_cur[2] = x2;
-                ks_cur[3] = x3;
-            }
-            uint32_t ks[4];
-            ks_shift(ks_prev, ks_cur, s, ks);
-            if (q <= qoff) {   // header words are never encrypted
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (4 * q + u < hw)
-                        ks[u] = 0;
-            }
-            uint32_t o[4] = { v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2],
-                              v.w ^ ks[3] };
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                wv[4 * t + u] = bswap(PROTECT ? o[u] : v[u]);
-            // store
-            if (full || 16 * q + 16 <= L) {
-                u32x4 ov = { o[0], o[1], o[2], o[3] };
-                *(u32x4 *)(out + 16 * q) = ov;
-            } else if (16 * q < L) {
-                store_words_partial(out + 16 * q, o, (int)(L - 16 * q));
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                ks_prev[u] = ks_cur[u];
-        }
-        if (AUTH) {
-            if (!full) {
-                const uint32_t roc = m.roc;
-                const bool last = b == nb - 1;
-#pragma unroll
-                for (int g = 0; g < 16; g++) {
-                    int rem = (int)L - (int)(64 * b + 4 * g);
-                    wv[g] = tail_word(wv[g], rem, roc);
+            for (int t = 0; t < 4; t++) {
+                const uint32_t jj = 4 * b + t - qoff;
+                u32x4 v = *(const u32x4 *)(ip + 16 * t);
+                uint32_t x0 = cb[0], x1 = cb[1], x2 = cb[2],
+                         x3 = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+                if (conf) {
+                    aes_block<NR ? NR : 1>(x0, x1, x2, x3, rk, T);
+                } else {
+                    x0 = x1 = x2 = x3 = 0;
                 }
-                if (last) {
-                    wv[14] = 0;
-                    wv[15] = (64 + L + 4) * 8;
+                uint32_t ks_cur[4] = { x0, x1, x2, x3 }, ks[4];
+                ks_shift(ks_prev, ks_cur, s, ks);
+                u32x4 o = { v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2],
+                            v.w ^ ks[3] };
+                *(u32x4 *)(op + 16 * t) = o;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    wv[4 * t + u] = bswap(PROTECT ? o[u] : v[u]);
+                    ks_prev[u] = ks_cur[u];
                 }
             }
-            sha1_compress(hst, wv);
+            if (AUTH)
+                sha1_compress(hst, wv);
+        } else {
+#ifndef ICM_EXPERIMENT_NO_GENERIC
+            icm_chunk_generic<NR, AUTH, PROTECT>(b, in, out, L, P, hw, s, qoff,
+                                                 nq, nb, conf, m.roc, cb, rk,
+                                                 T, ks_prev, hst);
+#else
+            hst[0] ^= b;   // timing experiments only: wrong output
+#endif
         }
     }
 
+    const uint32_t tag_len = key->tag_len;
+    const uint32_t mki_size = key->mki_size;
     if (!AUTH) {
         if (PROTECT && mki_size) {
             for (uint32_t u = 0; u < mki_size; u++)
@@ -523,7 +599,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
     }
     __syncthreads();
     const char *lds = (const char *)s_tab;
-    const uint32_t lane8 = (threadIdx.x & 31) * 8;
+    const AesLds T = make_aes_lds(s_tab);
 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= A.n)
@@ -537,10 +613,10 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
     typename std::conditional<UNIFORM, UniKey<NR>, LaneKey<NR>>::type rk;
     rk.load(key);
 
-    GhTab<UNIFORM> T;
-    T.lds = lds + AES_LDS_BYTES - 0x10000;   // the 0x10000 comes from lane16
-    T.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
-    T.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
+    GhTab<UNIFORM> G;
+    G.lds = lds + AES_LDS_BYTES - 0x10000;   // the 0x10000 comes from lane16
+    G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
+    G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
 
     const uint8_t *in = A.in + A.in_off[i];
     uint8_t *out = A.out + A.out_off[i];
@@ -574,7 +650,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
                 *(uint32_t *)(out + 4 * wi) = vu;
             x[u] ^= bswap(vu);
         }
-        ghash_mul(x, T);
+        ghash_mul(x, G);
     }
 
     const uint32_t nblk = (P + 15) >> 4;
@@ -588,7 +664,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
         else
             v = load_partial(pin + 16 * j, rem);
         uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = bswap(j + 2);
-        aes_block<NR>(k0, k1, k2, k3, rk, lds, lane8);
+        aes_block<NR>(k0, k1, k2, k3, rk, T);
         u32x4 o = { v.x ^ k0, v.y ^ k1, v.z ^ k2, v.w ^ k3 };
         u32x4 ctv = PROTECT ? o : v;
         if (rem < 16) {   // zero-pad the last ciphertext block for GHASH
@@ -605,7 +681,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
         x[1] ^= bswap(ctv.y);
         x[2] ^= bswap(ctv.z);
         x[3] ^= bswap(ctv.w);
-        ghash_mul(x, T);
+        ghash_mul(x, G);
         if (rem >= 16) {
             *(u32x4a4 *)(pout + 16 * j) = o;
         } else {
@@ -616,10 +692,10 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
     // length block: [len(A)]64 || [len(C)]64 in bits
     x[1] ^= enc_start * 8;
     x[3] ^= P * 8;
-    ghash_mul(x, T);
+    ghash_mul(x, G);
     // tag = E(J0) ^ S
     uint32_t e0 = c0, e1 = c1, e2 = c2, e3 = bswap(1u);
-    aes_block<NR>(e0, e1, e2, e3, rk, lds, lane8);
+    aes_block<NR>(e0, e1, e2, e3, rk, T);
     uint32_t tagw[4] = { bswap(x[0]) ^ e0, bswap(x[1]) ^ e1, bswap(x[2]) ^ e2,
                          bswap(x[3]) ^ e3 };   // little-endian words of tag
     if (PROTECT) {
@@ -649,7 +725,7 @@ struct GlobalKey {
 
 template <int NR>
 DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
-                  uint8_t *p, const char *lds, uint32_t lane8)
+                  uint8_t *p, const AesLds &T)
 {
     GlobalKey rk{ key };
     const uint32_t enc_start = SRTP_META_ENC_START(m.info);
@@ -676,7 +752,7 @@ DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
             x3 = bswap(j + 2);
         else
             x3 = c3base ^ ((j >> 8) << 16) ^ ((j & 0xffu) << 24);
-        aes_block<NR>(x0, x1, x2, x3, rk, lds, lane8);
+        aes_block<NR>(x0, x1, x2, x3, rk, T);
         uint32_t ks[4] = { x0, x1, x2, x3 };
         for (uint32_t b = 0; b < 16 && 16 * j + b < P; b++)
             p[enc_start + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
@@ -701,15 +777,14 @@ __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
     const srtp_dev_key_t *key = keys + m.key;
     if (!key->conf || key->family == SRTP_DEV_NULL)
         return;
-    const char *lds = (const char *)s_tab;
-    const uint32_t lane8 = (threadIdx.x & 31) * 8;
+    const AesLds T = make_aes_lds(s_tab);
     uint8_t *p = arena + off[i];
     if (key->rounds == 10)
-        undo_one<10>(key, m, p, lds, lane8);
+        undo_one<10>(key, m, p, T);
     else if (key->rounds == 12)
-        undo_one<12>(key, m, p, lds, lane8);
+        undo_one<12>(key, m, p, T);
     else
-        undo_one<14>(key, m, p, lds, lane8);
+        undo_one<14>(key, m, p, T);
 }
 
 // ---------------------------------------------------------------------------

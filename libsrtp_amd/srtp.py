@@ -12,7 +12,9 @@ import os
 import subprocess
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsrtp_mi355x.so")
+# LIBSRTP_MI355X_LIB: timing experiments point at alternative builds
+LIB_PATH = os.environ.get("LIBSRTP_MI355X_LIB",
+                          os.path.join(HERE, "libsrtp_mi355x.so"))
 
 
 def build():
