@@ -204,6 +204,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
     assert int((status != 0).sum()) == 0
+    dev_b, host_b = sess.prepass_stats()
 
     total_pk = n * a.steps * world
     value = total_pk / dt
@@ -242,6 +243,7 @@ def main():
                      "kernel": kname, "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": algo_bytes},
         "cpu_baseline": cpu,
+        "prepass": {"device_batches": dev_b, "host_batches": host_b},
     }
     print(json.dumps(out))
 

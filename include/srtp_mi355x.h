@@ -344,6 +344,12 @@ srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
  * the last batch, measured with HIP events on the stream they ran on. */
 void srtp_mi355x_set_timing(srtp_t ctx, int on);
 double srtp_mi355x_last_kernel_ms(srtp_t ctx);
+/* device-API batches completed by the GPU pre-pass / by the host pre-pass
+ * (the latter: streams needing a template clone, MKI, a pending ROC, a
+ * receiver-direction stream, non-advancing sequence numbers, or keys near
+ * their usage limit -- DESIGN.md "Device pre-pass") */
+void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
+                               uint64_t *host_batches);
 /* 1 when a HIP device is usable from this process */
 int srtp_mi355x_gpu_available(void);
 

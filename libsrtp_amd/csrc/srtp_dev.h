@@ -97,6 +97,8 @@ typedef struct srtp_gpu_batch {
     uint32_t uniform_key;   /* slot when every packet uses one key, else ~0 */
     uint32_t mask;          /* bitmask of kernel variants present (hint)   */
     void *stream;           /* hipStream_t or NULL for the context stream */
+    const uint32_t *abort;  /* device word; non-zero -> kernels do nothing
+                               (device pre-pass fell back), or NULL     */
 } srtp_gpu_batch_t;
 
 int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b);
@@ -111,6 +113,62 @@ int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
 int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
                    const uint64_t *in_off, const uint32_t *in_len,
                    srtp_dev_hdr_t *hdr_out, void *stream);
+
+/* ---- device pre-pass (DESIGN.md "Device pre-pass") --------------------
+ * A device mirror of the session's streams lets srtp_protect_device run the
+ * in-order index / replay / key-usage pre-pass on the GPU.  The host stays
+ * authoritative: it uploads the table, the GPU advances it, and the host
+ * pulls it back before any host-side use of stream state. */
+enum {
+    SRTP_DS_ELIGIBLE = 1, /* sender/unknown direction, no MKI, no pending ROC */
+    SRTP_DS_ICM_CONF = 2  /* AES-ICM encrypting: 2^16 keystream-block limit */
+};
+
+typedef struct srtp_dev_stream {
+    uint32_t ssrc;
+    uint32_t key;       /* key slot of the stream's (only) session key      */
+    uint32_t variant;   /* SRTP_VARIANT of that key                          */
+    uint32_t flags;     /* SRTP_DS_*                                         */
+    uint32_t trailer;   /* tag + MKI bytes appended by protect               */
+    uint32_t win_bits;  /* replay window bits (multiple of 32)               */
+    uint32_t win_off;   /* word offset of the window in the window arena     */
+    uint32_t pad;
+    uint64_t index;     /* rdbx index (ROC << 16 | SEQ)                      */
+    uint64_t uses;      /* packets charged to the key since the upload       */
+} srtp_dev_stream_t;
+
+/* the table: streams[ns], window arena (nwords), SSRC hash (hcap a power of
+ * two, open addressing with the host's hash, hval ~0 = empty slot) */
+int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
+                       uint32_t ns, const uint32_t *win, uint32_t nwords,
+                       const uint32_t *hkey, const uint32_t *hval,
+                       uint32_t hcap);
+int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
+                         uint32_t *win);
+
+typedef struct srtp_gpu_pp_batch {
+    size_t n;
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    uint8_t *out;
+    const uint64_t *out_off;
+    uint32_t *out_len;      /* in: capacity, out: protected length */
+    int32_t *status;
+    void *stream;
+    uint32_t uniform_key;   /* as srtp_gpu_batch_t */
+    uint32_t mask;
+} srtp_gpu_pp_batch_t;
+
+/* pre-pass + crypto for protect.  *fallback = 1: nothing was written (no
+ * packet, status or stream state) and the batch must take the host path. */
+int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+                        int *fallback);
+
+/* plumbing between the two HIP translation units */
+void **srtp_gpu_pp_slot(srtp_gpu_t *g);
+void *srtp_gpu_stream_of(srtp_gpu_t *g);
+void srtp_gpu_pp_free(void *pp);
 
 /* memory helpers */
 void *srtp_gpu_malloc(size_t bytes);

@@ -112,6 +112,7 @@ struct srtp_stream_ctx_t_ {
     /* per-batch speculative shadow (unprotect pre-pass) */
     uint64_t spec_epoch;
     rdbx_t spec;
+    uint32_t dev_sid;   /* id in the device stream table (dev_build) */
 };
 
 typedef struct {
@@ -132,6 +133,22 @@ typedef struct {
     size_t n_cap;
 } stage_t;
 
+/* device mirror of the stream table for the device pre-pass
+ * (srtp_prepass.hip); see dev_build / dev_pull */
+typedef struct {
+    int valid;              /* device table mirrors the host streams       */
+    int dirty;              /* device state is newer than the host's       */
+    uint32_t ns;
+    srtp_stream_ctx_t **sv; /* stream id -> stream                         */
+    srtp_dev_stream_t *hs;  /* host image of the table                     */
+    uint32_t *hwin;         /* host image of the window arena              */
+    uint32_t nwords;
+    uint64_t num_left_min;  /* over the keys of eligible streams           */
+    uint64_t uses_bound;    /* packets run on the device since the upload  */
+    uint32_t uniform, mask;
+    uint64_t fast_batches, host_batches;
+} devtab_t;
+
 struct srtp_ctx_t_ {
     srtp_stream_ctx_t *templ;
     srtp_stream_ctx_t **list; /* insertion order, like the reference list */
@@ -147,7 +164,10 @@ struct srtp_ctx_t_ {
     uint64_t epoch;
     int timing;
     double last_ms;
+    devtab_t dt;
 };
+
+static void dev_pull(srtp_t ctx);
 
 /* ------------------------------------------------------------------------
  * SSRC map
@@ -818,6 +838,7 @@ static srtp_err_status_t add_stream(srtp_t ctx, const srtp_policy_t *p)
 
 srtp_err_status_t srtp_stream_add(srtp_t ctx, const srtp_policy_t *p)
 {
+    dev_pull(ctx);
     if (!ctx)
         return srtp_err_status_bad_param;
     srtp_err_status_t st = valid_policy(p);
@@ -882,6 +903,9 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
     free(ctx->map.vals);
     free(ctx->free_slots);
     stage_free(&ctx->st);
+    free(ctx->dt.sv);
+    free(ctx->dt.hs);
+    free(ctx->dt.hwin);
     srtp_gpu_close(ctx->gpu);
     free(ctx);
     return srtp_err_status_ok;
@@ -891,13 +915,17 @@ srtp_stream_ctx_t *srtp_get_stream(srtp_t ctx, uint32_t ssrc_net)
 {
     uint32_t v = ((ssrc_net & 0xff) << 24) | ((ssrc_net & 0xff00) << 8) |
                  ((ssrc_net >> 8) & 0xff00) | (ssrc_net >> 24);
-    return ctx ? map_get(ctx, v) : NULL;
+    if (!ctx)
+        return NULL;
+    dev_pull(ctx);
+    return map_get(ctx, v);
 }
 
 srtp_err_status_t srtp_stream_remove(srtp_t ctx, uint32_t ssrc)
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    dev_pull(ctx);
     srtp_stream_ctx_t *s = map_get(ctx, ssrc);
     if (!s)
         return srtp_err_status_no_ctx;
@@ -966,6 +994,7 @@ srtp_err_status_t srtp_stream_update(srtp_t ctx, const srtp_policy_t *p)
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    dev_pull(ctx);
     srtp_err_status_t st = valid_policy(p);
     if (st)
         return st;
@@ -1487,6 +1516,7 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    dev_pull(ctx);
     if (!n)
         return srtp_err_status_ok;
     size_t arena = 0;
@@ -1660,6 +1690,7 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    dev_pull(ctx);
     if (!n)
         return srtp_err_status_ok;
     size_t arena = 0;
@@ -1797,12 +1828,171 @@ static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
     return srtp_err_status_ok;
 }
 
+/* ------------------------------------------------------------------------
+ * device stream table (DESIGN.md "Device pre-pass")
+ * ---------------------------------------------------------------------- */
+static int dev_build(srtp_t ctx)
+{
+    devtab_t *dt = &ctx->dt;
+    uint32_t ns = (uint32_t)ctx->n;
+    size_t nwords = 0;
+    for (size_t i = 0; i < ctx->n; i++)
+        nwords += ctx->list[i]->rdbx.bits / 32;
+    free(dt->sv);
+    free(dt->hs);
+    free(dt->hwin);
+    dt->sv = (srtp_stream_ctx_t **)calloc(ns + 1, sizeof(void *));
+    dt->hs = (srtp_dev_stream_t *)calloc(ns + 1, sizeof(srtp_dev_stream_t));
+    dt->hwin = (uint32_t *)calloc(nwords + 1, 4);
+    size_t hcap = ctx->map.cap ? ctx->map.cap : 1;
+    uint32_t *hk = (uint32_t *)calloc(hcap, 4);
+    uint32_t *hv = (uint32_t *)malloc(hcap * 4);
+    int rc = -1;
+    if (!dt->sv || !dt->hs || !dt->hwin || !hk || !hv)
+        goto out;
+    dt->num_left_min = UINT64_MAX;
+    dt->uniform = 0xffffffffu;
+    dt->mask = 0;
+    int first = 1;
+    uint32_t woff = 0;
+    for (uint32_t sid = 0; sid < ns; sid++) {
+        srtp_stream_ctx_t *st = ctx->list[sid];
+        const hkey_t *k = &st->keys->k[0];
+        srtp_dev_stream_t *d = &dt->hs[sid];
+        dt->sv[sid] = st;
+        st->dev_sid = sid;
+        d->ssrc = st->ssrc;
+        d->key = k->slot;
+        d->variant = k->variant;
+        d->flags = 0;
+        if (!st->use_mki && st->rdbx.pending_roc == 0 &&
+            st->direction != DIR_RECEIVER) {
+            d->flags |= SRTP_DS_ELIGIBLE;
+            if (k->num_left < dt->num_left_min)
+                dt->num_left_min = k->num_left;
+            if (first)
+                dt->uniform = k->slot;
+            else if (dt->uniform != k->slot)
+                dt->uniform = 0xffffffffu;
+            first = 0;
+            dt->mask |= 1u << k->variant;
+        }
+        if (k->family == SRTP_DEV_ICM && (st->rtp_services & sec_serv_conf))
+            d->flags |= SRTP_DS_ICM_CONF;
+        d->trailer = (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
+        d->win_bits = (uint32_t)st->rdbx.bits;
+        d->win_off = woff;
+        d->index = st->rdbx.index;
+        d->uses = 0;
+        memcpy(dt->hwin + woff, st->rdbx.w, st->rdbx.bits / 8);
+        woff += (uint32_t)(st->rdbx.bits / 32);
+    }
+    for (size_t h = 0; h < hcap; h++) {
+        hv[h] = 0xffffffffu;
+        if (ctx->map.cap && ctx->map.vals[h]) {
+            hk[h] = ctx->map.keys[h];
+            hv[h] = ctx->map.vals[h]->dev_sid;
+        }
+    }
+    if (srtp_gpu_pp_upload(ctx->gpu, dt->hs, ns, dt->hwin, woff, hk, hv,
+                           (uint32_t)hcap))
+        goto out;
+    dt->ns = ns;
+    dt->nwords = woff;
+    dt->uses_bound = 0;
+    dt->valid = 1;
+    dt->dirty = 0;
+    rc = 0;
+out:
+    free(hk);
+    free(hv);
+    return rc;
+}
+
+/* bring the device-advanced stream state back into the host streams and
+ * drop the mirror (the caller is about to use or change host state) */
+static void dev_pull(srtp_t ctx)
+{
+    devtab_t *dt = &ctx->dt;
+    if (!dt->valid)
+        return;
+    dt->valid = 0;
+    if (!dt->dirty)
+        return;
+    dt->dirty = 0;
+    if (srtp_gpu_pp_download(ctx->gpu, dt->hs, dt->hwin)) {
+        log_msg(srtp_log_level_error, "device stream table download failed");
+        return;
+    }
+    for (uint32_t sid = 0; sid < dt->ns; sid++) {
+        srtp_stream_ctx_t *st = dt->sv[sid];
+        const srtp_dev_stream_t *d = &dt->hs[sid];
+        st->rdbx.index = d->index;
+        memcpy(st->rdbx.w, dt->hwin + d->win_off, st->rdbx.bits / 8);
+        if (d->uses) {
+            st->keys->k[0].num_left -= d->uses;
+            if (st->direction == DIR_UNKNOWN)
+                st->direction = DIR_SENDER;
+        }
+    }
+}
+
+/* the device pre-pass; returns 1 when the batch was completed on the GPU,
+ * 0 when the host path must run it, -1 on a device error */
+static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
+{
+    devtab_t *dt = &ctx->dt;
+    if (!ctx->n || b->n > 0x7fffffffu)
+        return 0;
+    if (!dt->valid && dev_build(ctx))
+        return -1;
+    /* no key can reach its soft limit inside this batch (key.c:74-90) */
+    if (dt->num_left_min == UINT64_MAX ||
+        dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT)
+        return 0;
+    srtp_gpu_pp_batch_t pb;
+    memset(&pb, 0, sizeof pb);
+    pb.n = b->n;
+    pb.in = b->in;
+    pb.in_off = b->in_off;
+    pb.in_len = b->in_len;
+    pb.out = b->out;
+    pb.out_off = b->out_off;
+    pb.out_len = b->out_len;
+    pb.status = b->status;
+    pb.stream = b->stream;
+    pb.uniform_key = dt->uniform;
+    pb.mask = dt->mask;
+    int fallback = 1;
+    srtp_gpu_set_timing(ctx->gpu, ctx->timing);
+    if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))
+        return -1;
+    if (fallback)
+        return 0;
+    if (ctx->timing)
+        ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
+    dt->uses_bound += b->n;
+    dt->dirty = 1;
+    return 1;
+}
+
 srtp_err_status_t srtp_protect_device(srtp_t ctx, const srtp_device_batch_t *b)
 {
     if (!ctx || !b)
         return srtp_err_status_bad_param;
     if (!b->n)
         return srtp_err_status_ok;
+    int fast = protect_device_fast(ctx, b);
+    if (fast < 0) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        return srtp_err_status_fail;
+    }
+    if (fast) {
+        ctx->dt.fast_batches++;
+        return srtp_err_status_ok;
+    }
+    ctx->dt.host_batches++;
+    dev_pull(ctx);
     size_t n = b->n;
     pkt_sum_t *sum = (pkt_sum_t *)malloc(n * sizeof *sum);
     size_t *cap = (size_t *)malloc(n * sizeof(size_t));
@@ -1842,8 +2032,10 @@ srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
 {
     if (!ctx || !b)
         return srtp_err_status_bad_param;
+    dev_pull(ctx);
     if (!b->n)
         return srtp_err_status_ok;
+    ctx->dt.host_batches++;
     size_t n = b->n;
     pkt_sum_t *sum = (pkt_sum_t *)malloc(n * sizeof *sum);
     size_t *cap = (size_t *)malloc(n * sizeof(size_t));
@@ -2197,6 +2389,8 @@ srtp_err_status_t srtp_get_protect_rtcp_trailer_length(srtp_t session,
 srtp_err_status_t srtp_stream_set_roc(srtp_t session, uint32_t ssrc,
                                       uint32_t roc)
 {
+    if (session)
+        dev_pull(session);
     srtp_stream_ctx_t *s = session ? map_get(session, ssrc) : NULL;
     if (!s)
         return srtp_err_status_bad_param;
@@ -2207,6 +2401,8 @@ srtp_err_status_t srtp_stream_set_roc(srtp_t session, uint32_t ssrc,
 srtp_err_status_t srtp_stream_get_roc(srtp_t session, uint32_t ssrc,
                                       uint32_t *roc)
 {
+    if (session)
+        dev_pull(session);
     srtp_stream_ctx_t *s = session ? map_get(session, ssrc) : NULL;
     if (!s)
         return srtp_err_status_bad_param;
@@ -2223,6 +2419,15 @@ void srtp_mi355x_set_timing(srtp_t ctx, int on)
 double srtp_mi355x_last_kernel_ms(srtp_t ctx) { return ctx ? ctx->last_ms : 0; }
 
 int srtp_mi355x_gpu_available(void) { return srtp_gpu_available(); }
+
+void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
+                               uint64_t *host_batches)
+{
+    if (device_batches)
+        *device_batches = ctx ? ctx->dt.fast_batches : 0;
+    if (host_batches)
+        *host_batches = ctx ? ctx->dt.host_batches : 0;
+}
 
 /* Test hook (no GPU): drives the protect pre-pass index / replay logic of a
  * fresh stream over a sequence of sequence numbers, as srtp_protect would

@@ -31,6 +31,7 @@
 #include <type_traits>
 
 #include "srtp_dev.h"
+#include "srtp_rtp_hdr.h"
 
 #define DEV __device__ __forceinline__
 
@@ -118,11 +119,20 @@ struct LaneKey {
     DEV uint32_t operator()(int i) const { return rk[i]; }
 };
 
+// The schedule is read once at kernel entry, before any store, into SGPRs:
+// left as loads at the use sites, the compiler must assume the packet stores
+// may alias the key table and re-fetches 11 dwordx4 per AES block through
+// the vector memory path (measured: ~1000 VMEM reads per wave).
 template <int NR>
 struct UniKey {
-    const srtp_dev_key_t *k;
-    DEV void load(const srtp_dev_key_t *kk) { k = kk; }
-    DEV uint32_t operator()(int i) const { return k->rk[i]; }
+    uint32_t rk[4 * (NR + 1)];
+    DEV void load(const srtp_dev_key_t *k)
+    {
+#pragma unroll
+        for (int i = 0; i < 4 * (NR + 1); i++)
+            rk[i] = __builtin_amdgcn_readfirstlane(k->rk[i]);
+    }
+    DEV uint32_t operator()(int i) const { return rk[i]; }
 };
 
 // AES encryption of one block held as little-endian words (column c =
@@ -296,6 +306,7 @@ struct IcmArgs {
     const srtp_dev_meta_t *meta;
     const srtp_dev_key_t *keys;
     uint8_t *auth_ok;
+    const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;   // uniform key slot
 };
@@ -370,6 +381,8 @@ template <int NR, bool AUTH, bool PROTECT, bool UNIFORM>
 __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
 {
     __shared__ uint2 s_tab[256 * 32];
+    if (A.abort && *A.abort)
+        return;
     if (NR)
         load_aes_table(s_tab);
     __syncthreads();
@@ -562,6 +575,7 @@ struct GcmArgs {
     const srtp_dev_key_t *keys;
     const uint32_t *ghash;   // 1024 words per GCM key
     uint8_t *auth_ok;
+    const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;
 };
@@ -589,6 +603,8 @@ template <int NR, bool PROTECT, bool UNIFORM>
 __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
 {
     __shared__ uint2 s_tab[(AES_LDS_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 8];
+    if (A.abort && *A.abort)
+        return;
     load_aes_table(s_tab);
     if (UNIFORM) {
         const u32x4 *src =
@@ -797,37 +813,7 @@ __global__ void k_parse(const uint8_t *in, const uint64_t *in_off,
     if (i >= n)
         return;
     const uint64_t off = in_off[i];
-    const uint32_t len = in_len[i];
-    const uint8_t *p = in + off;
-    srtp_dev_hdr_t h;
-    h.len = len;
-    h.ssrc = 0;
-    h.seq_len = 0;
-    uint32_t err = 0, es = 0;
-    if ((off & 15) != 0) {
-        err = 2;
-    } else if (len < 12) {
-        err = 2;
-    } else {
-        uint32_t w0 = bswap(*(const uint32_t *)p);
-        h.ssrc = bswap(*(const uint32_t *)(p + 8));
-        h.seq_len = w0 & 0xffffu;
-        es = 12 + 4 * ((w0 >> 24) & 0xfu);
-        if (len < es) {
-            err = 2;
-        } else if ((w0 >> 28) & 1) {
-            if (len < es + 4) {
-                err = 2;
-            } else {
-                uint32_t xw = bswap(*(const uint32_t *)(p + es));
-                es += ((xw & 0xffffu) + 1) * 4;
-                if (len < es)
-                    err = 2;
-            }
-        }
-    }
-    h.enc_start = err ? (err << 24) : es;
-    hdr[i] = h;
+    hdr[i] = srtp_parse_rtp(in + off, off, in_len[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -901,6 +887,7 @@ struct srtp_gpu {
     hipEvent_t ev0, ev1;
     int timing;
     float last_ms;
+    void *pp;   // device pre-pass state (srtp_prepass.hip)
 };
 
 // variant mask bits: which kernel instantiations the batch needs
@@ -919,6 +906,7 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.meta = b->meta;
     A.keys = g->d_keys;
     A.auth_ok = b->auth_ok;
+    A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
     dim3 grid((unsigned)((b->n + 511) / 512)), block(512);
@@ -944,6 +932,7 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.keys = g->d_keys;
     A.ghash = g->d_ghash;
     A.auth_ok = b->auth_ok;
+    A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
     dim3 grid((unsigned)((b->n + 511) / 512)), block(512);
@@ -978,6 +967,9 @@ static int run_dir(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
 extern "C" {
 
 const char *srtp_gpu_last_error(void) { return g_err; }
+
+void **srtp_gpu_pp_slot(srtp_gpu_t *g) { return &g->pp; }
+void *srtp_gpu_stream_of(srtp_gpu_t *g) { return (void *)g->stream; }
 
 int srtp_gpu_available(void)
 {
@@ -1020,6 +1012,7 @@ void srtp_gpu_close(srtp_gpu_t *g)
     if (!g)
         return;
     (void)hipStreamSynchronize(g->stream);
+    srtp_gpu_pp_free(g->pp);
     (void)hipFree(g->d_keys);
     (void)hipFree(g->d_ghash);
     (void)hipEventDestroy(g->ev0);

@@ -1,0 +1,575 @@
+// srtp_prepass.hip -- the protect pre-pass of srtp_protect_device on the GPU.
+//
+// The host pre-pass (srtp_host.c pre_protect, following srtp/srtp.c:
+// 2493-2712 and 2088-2233) walks the batch in order: stream lookup, key
+// usage (crypto/kernel/key.c:74-90), index estimate and replay update
+// (srtp.c:2038-2081, crypto/replay/rdbx.c:112-145, 227-270).  Per stream
+// those steps form a chain: packet k's index is packet k-1's index plus the
+// 16-bit sequence advance, as long as every advance is in [1, 2^15) -- the
+// range where rdbx's index_guess returns exactly prev + d.  Under that
+// condition the whole batch reduces to
+//   classify (parse, SSRC hash lookup)  -> stable radix sort by stream
+//   -> segmented inclusive scan of advances (first packet: the exact
+//      estimate from the stream's stored index)  -> replay window update
+//   -> commit (meta, status, out_len, stream state)
+// and every packet's result equals the sequential reference's.  Anything
+// outside the condition (unknown SSRC needing a template clone, a stream
+// with MKI / pending ROC / receiver direction, a non-advancing sequence)
+// raises the abort word: nothing is committed, the crypto kernels exit,
+// and the host runs its exact path on the untouched state.  Key-limit
+// events cannot occur on this path: the host only takes it while every key
+// has more than SOFT_LIMIT uses left after the batch.
+
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "srtp_dev.h"
+#include "srtp_rtp_hdr.h"
+
+namespace {
+
+constexpr uint32_t SEQ_MEDIAN = 32768;
+constexpr uint32_t ST_BAD_PARAM = 2, ST_CIPHER_FAIL = 8, ST_PARSE_ERR = 21,
+                   ST_BUFFER_SMALL = 28;
+constexpr uint32_t NOCHAIN = 0xffffffffu;
+
+// abort reasons (bits of the abort word; any bit -> host path)
+enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4 };
+
+struct PpState {
+    // stream table
+    srtp_dev_stream_t *st = nullptr;
+    uint32_t ns = 0, ns_cap = 0;
+    uint32_t *win = nullptr, *wnew = nullptr;
+    uint32_t nwords = 0, nwords_cap = 0;
+    uint32_t *hkey = nullptr, *hval = nullptr;
+    uint32_t hcap = 0, hcap_cap = 0;
+    uint32_t *bcount = nullptr;     // packets charged per stream (batch)
+    uint32_t *seg_first = nullptr;  // sorted position of a stream's first
+    uint64_t *new_index = nullptr;  // per stream, 0 = no chain packet
+    // per-packet scratch
+    size_t n_cap = 0;
+    srtp_dev_hdr_t *hdr = nullptr;
+    uint32_t *pstat = nullptr;      // status code of the packet
+    uint32_t *skey = nullptr, *skey2 = nullptr, *perm = nullptr,
+             *perm2 = nullptr;
+    uint64_t *val = nullptr, *est = nullptr;
+    srtp_dev_meta_t *meta = nullptr;
+    void *cub = nullptr;
+    size_t cub_bytes = 0;
+    uint32_t *abort = nullptr;      // device word
+    uint32_t *h_abort = nullptr;    // pinned
+};
+
+__device__ __forceinline__ uint32_t map_hash(uint32_t k, uint32_t mask)
+{
+    // srtp_host.c map_hash
+    uint32_t h = k * 0x9e3779b1u;
+    h ^= h >> 15;
+    return h & mask;
+}
+
+struct ClassifyArgs {
+    const uint8_t *in;
+    const uint64_t *in_off;
+    const uint32_t *in_len;
+    const uint32_t *cap;
+    const srtp_dev_stream_t *st;
+    const uint32_t *hkey, *hval;
+    uint32_t hmask;
+    uint32_t n;
+    srtp_dev_hdr_t *hdr;
+    uint32_t *pstat, *skey, *perm, *bcount, *abort;
+};
+
+// parse, stream lookup, the per-packet checks of pre_protect that do not
+// depend on stream state (srtp_host.c pre_protect; srtp.c:2515-2600)
+__global__ void k_pp_classify(ClassifyArgs A)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= A.n)
+        return;
+    const uint64_t off = A.in_off[i];
+    const uint32_t len = A.in_len[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
+    A.hdr[i] = h;
+    A.perm[i] = i;
+    uint32_t code = 0, key = NOCHAIN;
+    if (h.enc_start >> 24) {
+        code = h.enc_start >> 24;   // header does not parse: no stream touched
+    } else {
+        uint32_t sid = NOCHAIN;
+        uint32_t p = map_hash(h.ssrc, A.hmask);
+        for (uint32_t probe = 0; probe <= A.hmask; probe++) {
+            const uint32_t v = A.hval[p];
+            if (v == NOCHAIN)
+                break;
+            if (A.hkey[p] == h.ssrc) {
+                sid = v;
+                break;
+            }
+            p = (p + 1) & A.hmask;
+        }
+        if (sid == NOCHAIN) {
+            atomicOr(A.abort, AB_UNKNOWN_SSRC);   // template clone: host
+        } else {
+            const srtp_dev_stream_t &S = A.st[sid];
+            if (!(S.flags & SRTP_DS_ELIGIBLE))
+                atomicOr(A.abort, AB_INELIGIBLE);
+            // key usage (key.c:74) of packets that leave the chain here;
+            // chain packets are counted per stream from the sorted segment
+            // bounds (k_pp_seg_end) -- one atomic per packet on a hot
+            // stream's counter would serialise the whole batch in L2
+            if (A.cap[i] < len + S.trailer) {
+                code = ST_BUFFER_SMALL;
+                atomicAdd(&A.bcount[sid], 1u);
+            } else if (h.enc_start > len) {
+                code = ST_PARSE_ERR;
+                atomicAdd(&A.bcount[sid], 1u);
+            } else {
+                key = sid;
+                // aes_icm.c:317-322: at most 0xffff keystream blocks
+                if ((S.flags & SRTP_DS_ICM_CONF) &&
+                    (len - h.enc_start + 15) / 16 > 0xffffu)
+                    code = ST_CIPHER_FAIL;   // index still advances
+            }
+        }
+    }
+    A.pstat[i] = code;
+    A.skey[i] = key;
+}
+
+// sorted position k: the advance over the previous packet of the stream,
+// or for a stream's first packet the exact estimate from its stored index
+// (srtp_host.c estimate / index_guess = rdbx.c:112-145, 280-299)
+__global__ void k_pp_delta(const uint32_t *skey2, const uint32_t *perm2,
+                           const srtp_dev_hdr_t *hdr,
+                           const srtp_dev_stream_t *st, uint32_t ns,
+                           uint32_t n, uint64_t *val, uint32_t *seg_first,
+                           uint32_t *abort)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint32_t s = skey2[k];
+    if (s >= ns) {
+        val[k] = 0;
+        return;
+    }
+    const uint32_t seq = hdr[perm2[k]].seq_len & 0xffffu;
+    if (k > 0 && skey2[k - 1] == s) {
+        const uint32_t pseq = hdr[perm2[k - 1]].seq_len & 0xffffu;
+        const uint32_t d = (seq - pseq) & 0xffffu;
+        if (d == 0 || d >= SEQ_MEDIAN)
+            atomicOr(abort, AB_SEQUENCE);
+        val[k] = d;
+        return;
+    }
+    seg_first[s] = k;
+    const uint64_t idx = st[s].index;
+    uint64_t est;
+    int64_t delta;
+    if (idx > SEQ_MEDIAN) {
+        const uint32_t lroc = (uint32_t)(idx >> 16);
+        const uint32_t lseq = (uint32_t)(idx & 0xffffu);
+        uint32_t roc = lroc;
+        int64_t diff = (int64_t)seq - (int64_t)lseq;
+        if (lseq < SEQ_MEDIAN) {
+            if ((int)seq - (int)lseq > (int)SEQ_MEDIAN) {
+                roc = lroc - 1;
+                diff -= 65536;
+            }
+        } else if ((int)lseq - (int)SEQ_MEDIAN > (int)seq) {
+            roc = lroc + 1;
+            diff += 65536;
+        }
+        est = ((uint64_t)roc << 16) | seq;
+        delta = diff;
+    } else {
+        est = seq;
+        delta = (int64_t)seq - (int64_t)idx;
+    }
+    if (delta < 1)
+        atomicOr(abort, AB_SEQUENCE);   // replay check / repeat: host path
+    val[k] = est;
+}
+
+__global__ void k_pp_seg_end(const uint32_t *skey2, const uint64_t *est,
+                             uint32_t ns, uint32_t n,
+                             const uint32_t *seg_first, uint32_t *bcount,
+                             uint64_t *new_index)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint32_t s = skey2[k];
+    if (s < ns && (k + 1 == n || skey2[k + 1] != s)) {
+        new_index[s] = est[k];
+        atomicAdd(&bcount[s], k - seg_first[s] + 1);
+    }
+}
+
+// window of stream s shifted by its advance (rdbx_add's bitvector shift,
+// crypto/math/datatypes.c bitvector_left_shift)
+__global__ void k_pp_window(const srtp_dev_stream_t *st, uint32_t ns,
+                            const uint64_t *new_index, const uint32_t *win,
+                            uint32_t *wnew)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns || new_index[s] == 0)
+        return;
+    const srtp_dev_stream_t S = st[s];
+    const uint64_t adv = new_index[s] - S.index;
+    const uint32_t words = S.win_bits >> 5;
+    const uint32_t *w = win + S.win_off;
+    uint32_t *o = wnew + S.win_off;
+    if (adv >= S.win_bits) {
+        for (uint32_t i = 0; i < words; i++)
+            o[i] = 0;
+        return;
+    }
+    const uint32_t base = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+    for (uint32_t i = 0; i < words; i++) {
+        const uint32_t a = i + base < words ? w[i + base] : 0u;
+        const uint32_t b = i + base + 1 < words ? w[i + base + 1] : 0u;
+        o[i] = bi ? (a >> bi) | (b << (32 - bi)) : a;
+    }
+}
+
+// the replay bit of every chain packet still inside the window, then the
+// per-packet commit (sorted order k -> packet perm2[k])
+__global__ void k_pp_setbits(const uint32_t *skey2, const uint64_t *est,
+                             const srtp_dev_stream_t *st, uint32_t ns,
+                             uint32_t n, const uint64_t *new_index,
+                             uint32_t *wnew)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint32_t s = skey2[k];
+    if (s >= ns)
+        return;
+    const uint64_t dist = new_index[s] - est[k];
+    const uint32_t bits = st[s].win_bits;
+    if (dist < bits) {
+        const uint32_t bit = bits - 1 - (uint32_t)dist;
+        atomicOr(&wnew[st[s].win_off + (bit >> 5)], 1u << (bit & 31));
+    }
+}
+
+struct CommitArgs {
+    const uint32_t *skey2, *perm2, *pstat;
+    const uint64_t *est;
+    const srtp_dev_hdr_t *hdr;
+    const srtp_dev_stream_t *st;
+    uint32_t ns, n;
+    const uint32_t *abort;
+    srtp_dev_meta_t *meta;
+    int32_t *status;
+    uint32_t *out_len;
+};
+
+__global__ void k_pp_commit_pkt(CommitArgs A)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.n || *A.abort)
+        return;
+    const uint32_t i = A.perm2[k];
+    const uint32_t s = A.skey2[k];
+    const uint32_t code = A.pstat[i];
+    srtp_dev_meta_t m;
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;
+    if (s < A.ns && code == 0) {
+        const srtp_dev_stream_t &S = A.st[s];
+        const srtp_dev_hdr_t h = A.hdr[i];
+        m.key = S.key;
+        m.roc = (uint32_t)(A.est[k] >> 16);
+        m.info = h.enc_start | (S.variant << 24);
+        m.len = h.len;
+        A.out_len[i] = h.len + S.trailer;
+    }
+    A.meta[i] = m;
+    A.status[i] = (int32_t)code;   // error packets keep out_len = capacity
+}
+
+__global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
+                                   const uint64_t *new_index,
+                                   const uint32_t *bcount, const uint32_t *wnew,
+                                   uint32_t *win, const uint32_t *abort)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns || *abort)
+        return;
+    st[s].uses += bcount[s];
+    const uint64_t ni = new_index[s];
+    if (ni == 0)
+        return;
+    st[s].index = ni;
+    const uint32_t off = st[s].win_off, words = st[s].win_bits >> 5;
+    for (uint32_t w = 0; w < words; w++)
+        win[off + w] = wnew[off + w];
+}
+
+static thread_local char pp_err[256];
+
+int pp_fail(hipError_t e, const char *what)
+{
+    snprintf(pp_err, sizeof pp_err, "%s: %s", what, hipGetErrorString(e));
+    fprintf(stderr, "srtp_mi355x: %s\n", pp_err);
+    return -1;
+}
+
+#define PPCHK(x)                                                               \
+    do {                                                                       \
+        hipError_t e_ = (x);                                                   \
+        if (e_ != hipSuccess)                                                  \
+            return pp_fail(e_, #x);                                            \
+    } while (0)
+
+template <class T>
+int regrow(T **p, uint32_t *cap, uint32_t need)
+{
+    if (need <= *cap && *p)
+        return 0;
+    uint32_t nc = *cap ? *cap : 64;
+    while (nc < need)
+        nc *= 2;
+    if (*p)
+        PPCHK(hipFree(*p));
+    *p = nullptr;
+    PPCHK(hipMalloc((void **)p, (size_t)nc * sizeof(T)));
+    *cap = nc;
+    return 0;
+}
+
+PpState *pp_of(srtp_gpu_t *g)
+{
+    void **slot = srtp_gpu_pp_slot(g);
+    if (!*slot)
+        *slot = new PpState();
+    return (PpState *)*slot;
+}
+
+int reserve_packets(PpState *P, size_t n, hipStream_t stream)
+{
+    if (n <= P->n_cap)
+        return 0;
+    size_t c = P->n_cap ? P->n_cap : 4096;
+    while (c < n)
+        c *= 2;
+    void *old[] = { P->hdr, P->pstat, P->skey, P->skey2, P->perm,
+                    P->perm2, P->val, P->est, P->meta, P->cub };
+    for (void *o : old)
+        if (o)
+            PPCHK(hipFree(o));
+    PPCHK(hipMalloc((void **)&P->hdr, c * sizeof(srtp_dev_hdr_t)));
+    PPCHK(hipMalloc((void **)&P->pstat, c * 4));
+    PPCHK(hipMalloc((void **)&P->skey, c * 4));
+    PPCHK(hipMalloc((void **)&P->skey2, c * 4));
+    PPCHK(hipMalloc((void **)&P->perm, c * 4));
+    PPCHK(hipMalloc((void **)&P->perm2, c * 4));
+    PPCHK(hipMalloc((void **)&P->val, c * 8));
+    PPCHK(hipMalloc((void **)&P->est, c * 8));
+    PPCHK(hipMalloc((void **)&P->meta, c * sizeof(srtp_dev_meta_t)));
+    // temp storage for the largest sort and scan of c items
+    size_t a = 0, b = 0;
+    PPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, a, P->skey, P->skey2,
+                                             P->perm, P->perm2, (int)c, 0, 32,
+                                             stream));
+    PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
+        nullptr, b, P->skey2, P->val, P->est, hipcub::Sum(), (int)c,
+        hipcub::Equality(), stream));
+    P->cub_bytes = a > b ? a : b;
+    PPCHK(hipMalloc(&P->cub, P->cub_bytes));
+    P->n_cap = c;
+    return 0;
+}
+
+}   // namespace
+
+extern "C" {
+
+void srtp_gpu_pp_free(void *p)
+{
+    PpState *P = (PpState *)p;
+    if (!P)
+        return;
+    void *bufs[] = { P->st, P->win, P->wnew, P->hkey, P->hval, P->bcount,
+                     P->seg_first,
+                     P->new_index, P->hdr, P->pstat, P->skey, P->skey2,
+                     P->perm, P->perm2, P->val, P->est, P->meta, P->cub,
+                     P->abort };
+    for (void *b : bufs)
+        if (b)
+            (void)hipFree(b);
+    if (P->h_abort)
+        (void)hipHostFree(P->h_abort);
+    delete P;
+}
+
+int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
+                       uint32_t ns, const uint32_t *win, uint32_t nwords,
+                       const uint32_t *hkey, const uint32_t *hval,
+                       uint32_t hcap)
+{
+    PpState *P = pp_of(g);
+    hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
+    uint32_t c1 = P->ns_cap, c2 = P->ns_cap, c5 = P->ns_cap,
+             c3 = P->nwords_cap;
+    if (regrow(&P->st, &P->ns_cap, ns + 1) ||
+        regrow(&P->bcount, &c1, ns + 1) || regrow(&P->new_index, &c2, ns + 1) ||
+        regrow(&P->seg_first, &c5, ns + 1) ||
+        regrow(&P->win, &P->nwords_cap, nwords + 1) ||
+        regrow(&P->wnew, &c3, nwords + 1))
+        return -1;
+    if (hcap > P->hcap_cap || !P->hkey) {
+        uint32_t c4 = P->hcap_cap;
+        if (regrow(&P->hkey, &P->hcap_cap, hcap) || regrow(&P->hval, &c4, hcap))
+            return -1;
+    }
+    if (!P->abort) {
+        PPCHK(hipMalloc((void **)&P->abort, 4));
+        PPCHK(hipHostMalloc((void **)&P->h_abort, 4, hipHostMallocDefault));
+    }
+    P->ns = ns;
+    P->nwords = nwords;
+    P->hcap = hcap;
+    PPCHK(hipMemcpyAsync(P->st, streams, ns * sizeof *streams,
+                         hipMemcpyHostToDevice, stream));
+    if (nwords) {
+        PPCHK(hipMemcpyAsync(P->win, win, nwords * 4ull, hipMemcpyHostToDevice,
+                             stream));
+        PPCHK(hipMemcpyAsync(P->wnew, win, nwords * 4ull,
+                             hipMemcpyHostToDevice, stream));
+    }
+    PPCHK(hipMemcpyAsync(P->hkey, hkey, hcap * 4ull, hipMemcpyHostToDevice,
+                         stream));
+    PPCHK(hipMemcpyAsync(P->hval, hval, hcap * 4ull, hipMemcpyHostToDevice,
+                         stream));
+    PPCHK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
+                         uint32_t *win)
+{
+    PpState *P = pp_of(g);
+    hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
+    PPCHK(hipMemcpyAsync(streams, P->st, P->ns * sizeof *streams,
+                         hipMemcpyDeviceToHost, stream));
+    if (P->nwords)
+        PPCHK(hipMemcpyAsync(win, P->win, P->nwords * 4ull,
+                             hipMemcpyDeviceToHost, stream));
+    PPCHK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+                        int *fallback)
+{
+    *fallback = 1;
+    PpState *P = pp_of(g);
+    const size_t n = b->n;
+    if (!n) {
+        *fallback = 0;
+        return 0;
+    }
+    if (!P->st || !P->ns || n > 0x7fffffffu)
+        return 0;
+    hipStream_t stream = b->stream ? (hipStream_t)b->stream
+                                   : (hipStream_t)srtp_gpu_stream_of(g);
+    if (reserve_packets(P, n, stream))
+        return -1;
+    const uint32_t N = (uint32_t)n, ns = P->ns;
+    const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
+
+    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
+    PPCHK(hipMemsetAsync(P->bcount, 0, ns * 4ull, stream));
+    PPCHK(hipMemsetAsync(P->new_index, 0, ns * 8ull, stream));
+
+    ClassifyArgs C;
+    C.in = b->in;
+    C.in_off = b->in_off;
+    C.in_len = b->in_len;
+    C.cap = b->out_len;
+    C.st = P->st;
+    C.hkey = P->hkey;
+    C.hval = P->hval;
+    C.hmask = P->hcap - 1;
+    C.n = N;
+    C.hdr = P->hdr;
+    C.pstat = P->pstat;
+    C.skey = P->skey;
+    C.perm = P->perm;
+    C.bcount = P->bcount;
+    C.abort = P->abort;
+    hipLaunchKernelGGL(k_pp_classify, gp, blk, 0, stream, C);
+    PPCHK(hipGetLastError());
+
+    // stable sort by stream id; NOCHAIN keys truncate to all-ones > any sid
+    int end_bit = 1;
+    while ((1u << end_bit) <= ns && end_bit < 32)
+        end_bit++;
+    size_t tb = P->cub_bytes;
+    PPCHK(hipcub::DeviceRadixSort::SortPairs(P->cub, tb, P->skey, P->skey2,
+                                             P->perm, P->perm2, (int)N, 0,
+                                             end_bit, stream));
+    hipLaunchKernelGGL(k_pp_delta, gp, blk, 0, stream, P->skey2, P->perm2,
+                       P->hdr, P->st, ns, N, P->val, P->seg_first, P->abort);
+    PPCHK(hipGetLastError());
+    tb = P->cub_bytes;
+    PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
+        P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
+        hipcub::Equality(), stream));
+    hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est, ns,
+                       N, P->seg_first, P->bcount, P->new_index);
+    hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
+                       P->new_index, P->win, P->wnew);
+    hipLaunchKernelGGL(k_pp_setbits, gp, blk, 0, stream, P->skey2, P->est,
+                       P->st, ns, N, P->new_index, P->wnew);
+    CommitArgs K;
+    K.skey2 = P->skey2;
+    K.perm2 = P->perm2;
+    K.pstat = P->pstat;
+    K.est = P->est;
+    K.hdr = P->hdr;
+    K.st = P->st;
+    K.ns = ns;
+    K.n = N;
+    K.abort = P->abort;
+    K.meta = P->meta;
+    K.status = b->status;
+    K.out_len = b->out_len;
+    hipLaunchKernelGGL(k_pp_commit_pkt, gp, blk, 0, stream, K);
+    hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
+                       P->new_index, P->bcount, P->wnew, P->win, P->abort);
+    PPCHK(hipGetLastError());
+
+    srtp_gpu_batch_t cb = {};
+    cb.n = n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;
+    cb.auth_ok = nullptr;
+    cb.uniform_key = b->uniform_key;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = P->abort;
+    if (srtp_gpu_run(g, 0, &cb))
+        return -1;
+    PPCHK(hipMemcpyAsync(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost,
+                         stream));
+    PPCHK(hipStreamSynchronize(stream));
+    *fallback = *P->h_abort != 0;
+    return 0;
+}
+
+}   // extern "C"

@@ -1,0 +1,55 @@
+// srtp_rtp_hdr.h -- device-side RTP header parse shared by the parse kernel
+// and the device pre-pass.  Follows srtp_get_rtp_hdr_len / the extension
+// walk of srtp/srtp.c:1872-1905 (protect) as restated in oracle/srtp_oracle.c.
+#ifndef SRTP_RTP_HDR_H
+#define SRTP_RTP_HDR_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "srtp_dev.h"
+
+__device__ __forceinline__ uint32_t srtp_bswap32(uint32_t x)
+{
+    return __builtin_amdgcn_perm(0u, x, 0x00010203u);
+}
+
+// summary of packet p (len bytes, arena offset off): enc_start holds the
+// header length, or (status << 24) when the header does not parse
+// (srtp_err_status_bad_param, as the reference's length checks return)
+__device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
+                                                         uint64_t off,
+                                                         uint32_t len)
+{
+    srtp_dev_hdr_t h;
+    h.len = len;
+    h.ssrc = 0;
+    h.seq_len = 0;
+    uint32_t err = 0, es = 0;
+    if ((off & 15) != 0) {
+        err = 2;
+    } else if (len < 12) {
+        err = 2;
+    } else {
+        uint32_t w0 = srtp_bswap32(*(const uint32_t *)p);
+        h.ssrc = srtp_bswap32(*(const uint32_t *)(p + 8));
+        h.seq_len = w0 & 0xffffu;
+        es = 12 + 4 * ((w0 >> 24) & 0xfu);
+        if (len < es) {
+            err = 2;
+        } else if ((w0 >> 28) & 1) {
+            if (len < es + 4) {
+                err = 2;
+            } else {
+                uint32_t xw = srtp_bswap32(*(const uint32_t *)(p + es));
+                es += ((xw & 0xffffu) + 1) * 4;
+                if (len < es)
+                    err = 2;
+            }
+        }
+    }
+    h.enc_start = err ? (err << 24) : es;
+    return h;
+}
+
+#endif

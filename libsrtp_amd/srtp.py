@@ -139,6 +139,8 @@ def lib():
         "srtp_mi355x_set_timing": ([P, C.c_int], None),
         "srtp_mi355x_last_kernel_ms": ([P], C.c_double),
         "srtp_mi355x_gpu_available": ([], C.c_int),
+        "srtp_mi355x_prepass_stats": ([P, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)], None),
         "srtp_get_version_string": ([], C.c_char_p),
     }
     for name, (args, res) in sig.items():
@@ -344,6 +346,12 @@ class Session:
 
     def last_kernel_ms(self):
         return self.L.srtp_mi355x_last_kernel_ms(self.h)
+
+    def prepass_stats(self):
+        """(device-API batches done by the GPU pre-pass, by the host)"""
+        d, h = C.c_uint64(), C.c_uint64()
+        self.L.srtp_mi355x_prepass_stats(self.h, C.byref(d), C.byref(h))
+        return d.value, h.value
 
     def close(self):
         if self.h:
