@@ -190,6 +190,57 @@ DEV void aes_block(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3,
     s3 = n3;
 }
 
+// NB independent blocks advanced round by round together: the NB*16 table
+// reads of a round are issued back to back, so one wave keeps NB times the
+// LDS requests in flight across the ~100-cycle read latency of a round.
+template <int NB, int NR, class KEY>
+DEV void aes_blocks(uint32_t (&s)[NB][4], const KEY &rk, const AesLds &T)
+{
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            s[j][c] ^= rk(c);
+#pragma unroll
+    for (int r = 1; r < NR; r++) {
+        uint32_t a[NB][4], b[NB][4], c[NB][4], d[NB][4];
+#pragma unroll
+        for (int j = 0; j < NB; j++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                a[j][q] = t0<0>(T, s[j][q]);
+                b[j][q] = t1<1>(T, s[j][q]);
+                c[j][q] = t0<2>(T, s[j][q]);
+                d[j][q] = t1<3>(T, s[j][q]);
+            }
+#pragma unroll
+        for (int j = 0; j < NB; j++)
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                s[j][q] = xor3(a[j][q], b[j][(q + 1) & 3], rk(4 * r + q)) ^
+                          rotl(c[j][(q + 2) & 3] ^ d[j][(q + 3) & 3], 16);
+    }
+    const uint32_t LO = 0x0c0c0601u, HI = 0x06010c0cu;
+    uint32_t a[NB][4], b[NB][4], c[NB][4], d[NB][4];
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            a[j][q] = t0<0>(T, s[j][q]);
+            b[j][q] = t1<1>(T, s[j][q]);
+            c[j][q] = t0<2>(T, s[j][q]);
+            d[j][q] = t1<3>(T, s[j][q]);
+        }
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            s[j][q] = xor3(__builtin_amdgcn_perm(b[j][(q + 1) & 3], a[j][q], LO),
+                           __builtin_amdgcn_perm(d[j][(q + 3) & 3],
+                                                 c[j][(q + 2) & 3], HI),
+                           rk(4 * NR + q));
+}
+
 // ---------------------------------------------------------------------------
 // SHA-1 compression (FIPS 180-4), W[] big-endian message words (clobbered)
 DEV void sha1_compress(uint32_t h[5], uint32_t w[16])
@@ -314,63 +365,92 @@ struct IcmArgs {
 #ifndef ICM_WAVES_PER_SIMD
 #define ICM_WAVES_PER_SIMD 1
 #endif
+#ifndef ICM_NB
+#define ICM_NB 2   // AES blocks interleaved per round in the steady state
+#endif
 
-// one 64-byte chunk of packet b on the general path: header words, the
-// packet tail, the ROC / padding / length words of the SHA-1 message
+// One 64-byte chunk b of a packet in its general form: header words that
+// are not encrypted, quads past the end of the data, the partial last quad
+// (kept in tailq, stored once after the chunk loop: a byte-wise store here,
+// unrolled per quad, costs ~65 VGPRs), and the ROC / terminator / length
+// words of the SHA-1 message tail (sha1.c srtp_sha1_final).
 template <int NR, bool AUTH, bool PROTECT, class KEY>
-DEV void icm_chunk_generic(uint32_t b, const uint8_t *in, uint8_t *out,
-                           uint32_t L, uint32_t P, uint32_t hw, uint32_t s,
-                           uint32_t qoff, uint32_t nq, uint32_t nb, bool conf,
-                           uint32_t roc, const uint32_t cb[4], const KEY &rk,
-                           const AesLds &T, uint32_t ks_prev[4],
-                           uint32_t hst[5])
+DEV void icm_chunk(uint32_t b, const uint8_t *in, uint8_t *out, uint32_t L,
+                   uint32_t hw, uint32_t s, uint32_t qoff, uint32_t nq,
+                   uint32_t nb, uint32_t bclean, bool conf, uint32_t roc,
+                   const uint32_t cb[4], const KEY &rk, const AesLds &T,
+                   uint32_t ks_prev[4], uint32_t hst[5], uint32_t tailq[4])
 {
+    const uint32_t q0 = 4 * b;
+    const uint8_t *ip = in + 16 * q0;
+    uint8_t *op = out + 16 * q0;
+    u32x4 v[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        v[t] = u32x4{ 0, 0, 0, 0 };
+        if (q0 + t < nq)
+            v[t] = *(const u32x4 *)(ip + 16 * t);
+    }
+    uint32_t ks[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t jj = q0 + t - qoff;
+        ks[t][0] = cb[0];
+        ks[t][1] = cb[1];
+        ks[t][2] = cb[2];
+        ks[t][3] = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+    }
+    if (conf) {
+#pragma unroll
+        for (int g = 0; g < 4; g += ICM_NB)
+            aes_blocks<ICM_NB, NR ? NR : 1>(
+                *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), rk, T);
+    } else {
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+    }
     uint32_t wv[16];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-        const uint32_t q = 4 * b + t;
-        u32x4 v = { 0, 0, 0, 0 };
-        if (q < nq)
-            v = *(const u32x4 *)(in + 16 * q);
-        uint32_t ks_cur[4] = { 0, 0, 0, 0 };
-        const int j = (int)q - (int)qoff;
-        if (conf && j >= 0 && (uint32_t)(16 * j) < P) {
-            uint32_t jj = (uint32_t)j;
-            uint32_t x0 = cb[0], x1 = cb[1], x2 = cb[2],
-                     x3 = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
-            aes_block<NR ? NR : 1>(x0, x1, x2, x3, rk, T);
-            ks_cur[0] = x0;
-            ks_cur[1] = x1;
-            ks_cur[2] = x2;
-            ks_cur[3] = x3;
+        const uint32_t q = q0 + t;
+        uint32_t kk[4];
+        ks_shift(ks_prev, ks[t], s, kk);
+        if (b < bclean) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (4 * q + u < hw)
+                    kk[u] = 0;   // header words are never encrypted
         }
-        uint32_t ks[4];
-        ks_shift(ks_prev, ks_cur, s, ks);
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            if (4 * q + u < hw)
-                ks[u] = 0;   // header words are never encrypted
-        uint32_t o[4] = { v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2], v.w ^ ks[3] };
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[u]);
+        uint32_t o[4] = { v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
+                          v[t].w ^ kk[3] };
         if (16 * q + 16 <= L) {
-            u32x4 ov = { o[0], o[1], o[2], o[3] };
-            *(u32x4 *)(out + 16 * q) = ov;
+            *(u32x4 *)(op + 16 * t) = u32x4{ o[0], o[1], o[2], o[3] };
         } else if (16 * q < L) {
-            store_words_partial(out + 16 * q, o, (int)(L - 16 * q));
+            // the one partial quad: stored after the loop (a byte-wise
+            // store here, unrolled per quad, costs ~65 VGPRs)
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                tailq[u] = o[u];
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-            ks_prev[u] = ks_cur[u];
+        for (int u = 0; u < 4; u++) {
+            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
+            ks_prev[u] = ks[t][u];
+        }
     }
     if (AUTH) {
+        if (64 * b + 64 > L) {
+            // message tail: ROC, the 0x80 terminator, zero padding and
+            // the bit length (sha1.c srtp_sha1_final)
 #pragma unroll
-        for (int g = 0; g < 16; g++)
-            wv[g] = tail_word(wv[g], (int)L - (int)(64 * b + 4 * g), roc);
-        if (b == nb - 1) {
-            wv[14] = 0;
-            wv[15] = (64 + L + 4) * 8;
+            for (int g = 0; g < 16; g++)
+                wv[g] = tail_word(wv[g], (int)L - (int)(64 * b + 4 * g),
+                                  roc);
+            if (b == nb - 1) {
+                wv[14] = 0;
+                wv[15] = (64 + L + 4) * 8;
+            }
         }
         sha1_compress(hst, wv);
     }
@@ -408,7 +488,6 @@ __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
     uint8_t *out = A.out + A.out_off[i];
     const uint32_t enc_start = SRTP_META_ENC_START(m.info);
     const uint32_t L = m.len;                 // end of auth'd region
-    const uint32_t P = L - enc_start;          // bytes to en/decrypt
     const uint32_t hw = enc_start >> 2, s = hw & 3, qoff = hw >> 2;
     const bool conf = NR != 0 && key->conf != 0;
 
@@ -429,50 +508,72 @@ __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
     uint32_t ks_prev[4] = { 0, 0, 0, 0 };
     const uint32_t nq = (L + 15) >> 4;             // quads holding data
     const uint32_t nb = AUTH ? ((L + 12) >> 6) + 1 : ((nq + 3) >> 2);
-    const uint32_t nfull = L >> 6;                 // chunks of pure data
     const uint32_t bclean = (qoff + 4) >> 2;       // first chunk past header
 
-    for (uint32_t b = 0; b < nb; b++) {
-        if (b >= bclean && b < nfull) {
-            // steady state: 64 bytes of payload, no header, no tail --
-            // 4 AES blocks, XOR, 64-byte store, one SHA-1 compression
-            const uint8_t *ip = in + 64 * b;
-            uint8_t *op = out + 64 * b;
-            uint32_t wv[16];
+    // One code path for every 64-byte chunk (header, payload, tail): the
+    // header / tail / padding handling sits in branches that are not taken
+    // in the steady state, so the loop keeps the register footprint of the
+    // plain payload chunk (<= 128 VGPRs -> 4 waves per SIMD).  Keystream
+    // blocks over header quads or past the payload are computed and masked
+    // or never stored.
+    uint32_t tailq[4] = { 0, 0, 0, 0 };
+    // header chunks, then the payload chunks (branch-free: no header word,
+    // no tail, full 16-byte loads and stores), then the tail chunks
+    const uint32_t nfull = L >> 6;
+    uint32_t b = 0;
+    for (; b < bclean && b < nb; b++)
+        icm_chunk<NR, AUTH, PROTECT>(b, in, out, L, hw, s, qoff, nq, nb, bclean,
+                                     conf, m.roc, cb, rk, T, ks_prev, hst,
+                                     tailq);
+    for (; b < nfull; b++) {
+        const uint8_t *ip = in + 64 * b;
+        uint8_t *op = out + 64 * b;
+        u32x4 v[4];
 #pragma unroll
-            for (int t = 0; t < 4; t++) {
-                const uint32_t jj = 4 * b + t - qoff;
-                u32x4 v = *(const u32x4 *)(ip + 16 * t);
-                uint32_t x0 = cb[0], x1 = cb[1], x2 = cb[2],
-                         x3 = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
-                if (conf) {
-                    aes_block<NR ? NR : 1>(x0, x1, x2, x3, rk, T);
-                } else {
-                    x0 = x1 = x2 = x3 = 0;
-                }
-                uint32_t ks_cur[4] = { x0, x1, x2, x3 }, ks[4];
-                ks_shift(ks_prev, ks_cur, s, ks);
-                u32x4 o = { v.x ^ ks[0], v.y ^ ks[1], v.z ^ ks[2],
-                            v.w ^ ks[3] };
-                *(u32x4 *)(op + 16 * t) = o;
+        for (int t = 0; t < 4; t++)
+            v[t] = *(const u32x4 *)(ip + 16 * t);
+        uint32_t ks[4][4];
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    wv[4 * t + u] = bswap(PROTECT ? o[u] : v[u]);
-                    ks_prev[u] = ks_cur[u];
-                }
-            }
-            if (AUTH)
-                sha1_compress(hst, wv);
-        } else {
-#ifndef ICM_EXPERIMENT_NO_GENERIC
-            icm_chunk_generic<NR, AUTH, PROTECT>(b, in, out, L, P, hw, s, qoff,
-                                                 nq, nb, conf, m.roc, cb, rk,
-                                                 T, ks_prev, hst);
-#else
-            hst[0] ^= b;   // timing experiments only: wrong output
-#endif
+        for (int t = 0; t < 4; t++) {
+            const uint32_t jj = 4 * b + t - qoff;
+            ks[t][0] = cb[0];
+            ks[t][1] = cb[1];
+            ks[t][2] = cb[2];
+            ks[t][3] = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
         }
+        if (conf) {
+#pragma unroll
+            for (int g = 0; g < 4; g += ICM_NB)
+                aes_blocks<ICM_NB, NR ? NR : 1>(
+                    *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), rk, T);
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+        }
+        uint32_t wv[16];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            uint32_t kk[4];
+            ks_shift(ks_prev, ks[t], s, kk);
+            u32x4 o = { v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
+                        v[t].w ^ kk[3] };
+            *(u32x4 *)(op + 16 * t) = o;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
+                ks_prev[u] = ks[t][u];
+            }
+        }
+        if (AUTH)
+            sha1_compress(hst, wv);
     }
+    for (; b < nb; b++)
+        icm_chunk<NR, AUTH, PROTECT>(b, in, out, L, hw, s, qoff, nq, nb, bclean,
+                                     conf, m.roc, cb, rk, T, ks_prev, hst,
+                                     tailq);
+    if (L & 15)
+        store_words_partial(out + (L & ~15u), tailq, (int)(L & 15));
 
     const uint32_t tag_len = key->tag_len;
     const uint32_t mki_size = key->mki_size;

@@ -1,0 +1,53 @@
+"""N>1 orchestration of bench.py on the CPU (gloo, world size 2): the
+barrier-bracketed timing takes the MAX over ranks, and every rank gets its
+own stream (weak scaling, no shared state, no data-path collective)."""
+import os
+import socket
+import time
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    calls = []
+
+    def step():
+        time.sleep(0.02 * (rank + 1))    # rank 1 is the slow one
+        calls.append(1)
+        return rank
+
+    dt, res = bench.timed_steps(step, steps=3, warmup=2, world=world)
+    q.put((rank, dt, len(calls), res, bench.rank_ssrc(rank)))
+    dist.destroy_process_group()
+
+
+def test_timed_steps_world2_takes_max_over_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, dt0, n0, res0, s0), (r1, dt1, n1, res1, s1) = out
+    assert n0 == n1 == 5                  # warmup 2 + timed 3 on each rank
+    assert res0 == [0] * 3 and res1 == [1] * 3
+    assert dt0 == pytest.approx(dt1)      # both report the max ...
+    assert dt1 >= 3 * 0.04                # ... which is the slow rank's time
+    assert s0 != s1                       # one stream per rank

@@ -2,6 +2,7 @@
 # Builds timing-experiment variants of libsrtp_mi355x.so into exp_build/<name>/
 # usage: tools/build_variants.sh name "-DFLAG ..." [name "-D..."]...
 set -e
+make -s -C "$(cd "$(dirname "$0")/.." && pwd)/libsrtp_amd"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
@@ -11,6 +12,6 @@ while [ $# -ge 2 ]; do
   gcc -O2 -fPIC -std=gnu11 -I$ROOT/include -I$ROOT/libsrtp_amd/csrc -c $ROOT/libsrtp_amd/csrc/srtp_host.c -o $d/h.o
   gcc -O2 -fPIC -std=gnu11 -I$ROOT/include -I$ROOT/libsrtp_amd/csrc -c $ROOT/libsrtp_amd/csrc/host_crypto.c -o $d/c.o
   wait
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libsrtp_mi355x.so $d/k.o $d/h.o $d/c.o
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libsrtp_mi355x.so $d/k.o $d/h.o $d/c.o $ROOT/libsrtp_amd/build/srtp_prepass.o
   echo built $name
 done

@@ -1,0 +1,202 @@
+/*
+ * e2e_bench.c -- host-memory (PCIe-inclusive) rates of the protect path, for
+ * DESIGN.md "End-to-end rate".  The packets start and end in host memory, as
+ * they do behind a socket:
+ *
+ *   batch   srtp_protect_batch() over per-packet host pointers (the libsrtp
+ *           call shape: the library stages into pinned memory, copies H2D,
+ *           runs the host pre-pass and the kernels, copies D2H and out)
+ *   pinned  the application keeps a pinned packet arena: hipMemcpyAsync H2D,
+ *           srtp_protect_device() (GPU pre-pass + kernels), hipMemcpyAsync D2H
+ *
+ *   usage: e2e_bench [packets] [payload] [iters]
+ *   prints one JSON line.
+ */
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "srtp_mi355x.h"
+
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec + t.tv_nsec * 1e-9;
+}
+
+static uint64_t sm_state = 0x5352545030303031ull; /* splitmix64 "SRTP0001" */
+static uint64_t splitmix64(void)
+{
+    uint64_t z = (sm_state += 0x9e3779b97f4a7c15ull);
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+#define CHECK(x)                                                               \
+    do {                                                                       \
+        if ((x) != 0) {                                                        \
+            fprintf(stderr, "%s:%d: %s failed\n", __FILE__, __LINE__, #x);     \
+            exit(1);                                                           \
+        }                                                                      \
+    } while (0)
+
+static srtp_t make_session(uint8_t *key)
+{
+    srtp_policy_t p;
+    memset(&p, 0, sizeof p);
+    srtp_crypto_policy_set_rtp_default(&p.rtp);
+    srtp_crypto_policy_set_rtp_default(&p.rtcp);
+    p.ssrc.type = ssrc_specific;
+    p.ssrc.value = 0xcafebabe;
+    p.key = key;
+    p.window_size = 128;
+    srtp_t s;
+    CHECK(srtp_create(&s, &p));
+    return s;
+}
+
+static void fill(uint8_t *pk, size_t slot, size_t n, size_t len, uint32_t seq0)
+{
+    for (size_t i = 0; i < n; i++) {
+        uint8_t *p = pk + i * slot;
+        uint32_t seq = (seq0 + (uint32_t)i) & 0xffff;
+        p[0] = 0x80;
+        p[1] = 96;
+        p[2] = (uint8_t)(seq >> 8);
+        p[3] = (uint8_t)seq;
+        memset(p + 4, 0, 4);
+        p[8] = 0xca;
+        p[9] = 0xfe;
+        p[10] = 0xba;
+        p[11] = 0xbe;
+    }
+    (void)len;
+}
+
+int main(int argc, char **argv)
+{
+    size_t n = argc > 1 ? strtoul(argv[1], 0, 0) : (1u << 20);
+    size_t payload = argc > 2 ? strtoul(argv[2], 0, 0) : 1400;
+    int iters = argc > 3 ? atoi(argv[3]) : 5;
+    size_t len = 12 + payload, slot = (len + 10 + 15) & ~(size_t)15;
+    uint8_t key[30];
+    for (int i = 0; i < 30; i++)
+        key[i] = (uint8_t)splitmix64();
+    CHECK(srtp_init());
+
+    /* ---- pinned arena + device API ----------------------------------- */
+    uint8_t *h_arena, *d_arena;
+    uint64_t *h_off, *d_off;
+    uint32_t *h_len, *h_cap, *d_len, *d_olen;
+    int32_t *d_st;
+    CHECK(hipHostMalloc((void **)&h_arena, n * slot, 0));
+    CHECK(hipHostMalloc((void **)&h_off, n * 8, 0));
+    CHECK(hipHostMalloc((void **)&h_len, n * 4, 0));
+    CHECK(hipHostMalloc((void **)&h_cap, n * 4, 0));
+    CHECK(hipMalloc((void **)&d_arena, n * slot));
+    CHECK(hipMalloc((void **)&d_off, n * 8));
+    CHECK(hipMalloc((void **)&d_len, n * 4));
+    CHECK(hipMalloc((void **)&d_olen, n * 4));
+    CHECK(hipMalloc((void **)&d_st, n * 4));
+    for (size_t i = 0; i < n * slot; i += 8) {
+        uint64_t r = splitmix64();
+        memcpy(h_arena + i, &r, n * slot - i < 8 ? n * slot - i : 8);
+    }
+    for (size_t i = 0; i < n; i++) {
+        h_off[i] = i * slot;
+        h_len[i] = (uint32_t)len;
+        h_cap[i] = (uint32_t)slot;
+    }
+    hipStream_t st;
+    CHECK(hipStreamCreate(&st));
+    CHECK(hipMemcpy(d_off, h_off, n * 8, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(d_len, h_len, n * 4, hipMemcpyHostToDevice));
+    srtp_t s1 = make_session(key);
+    srtp_device_batch_t b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.in = d_arena;
+    b.in_off = d_off;
+    b.in_len = d_len;
+    b.out = d_arena;
+    b.out_off = d_off;
+    b.out_len = d_olen;
+    b.status = d_st;
+    b.stream = st;
+    uint32_t seq0 = 0x1234;
+    double t_pinned = 0;
+    for (int it = -1; it < iters; it++) {
+        fill(h_arena, slot, n, len, seq0);
+        seq0 += (uint32_t)n;
+        double t0 = now();
+        CHECK(hipMemcpyAsync(d_arena, h_arena, n * slot, hipMemcpyHostToDevice,
+                             st));
+        CHECK(hipMemcpyAsync(d_olen, h_cap, n * 4, hipMemcpyHostToDevice, st));
+        CHECK(srtp_protect_device(s1, &b));
+        CHECK(hipMemcpyAsync(h_arena, d_arena, n * slot, hipMemcpyDeviceToHost,
+                             st));
+        CHECK(hipStreamSynchronize(st));
+        if (it >= 0)
+            t_pinned += now() - t0;
+    }
+    t_pinned /= iters;
+    /* verify lengths came back */
+    CHECK(hipMemcpy(h_len, d_olen, n * 4, hipMemcpyDeviceToHost));
+    if (h_len[0] != len + 10) {
+        fprintf(stderr, "unexpected out_len %u\n", h_len[0]);
+        return 1;
+    }
+    uint64_t dev_b = 0, host_b = 0;
+    srtp_mi355x_prepass_stats(s1, &dev_b, &host_b);
+
+    /* ---- libsrtp-shaped batch over host pointers --------------------- */
+    srtp_t s2 = make_session(key);
+    uint8_t *pk = (uint8_t *)malloc(n * slot);
+    const uint8_t **in = (const uint8_t **)malloc(n * sizeof(void *));
+    uint8_t **out = (uint8_t **)malloc(n * sizeof(void *));
+    size_t *il = (size_t *)malloc(n * sizeof(size_t));
+    size_t *ol = (size_t *)malloc(n * sizeof(size_t));
+    srtp_err_status_t *sts = (srtp_err_status_t *)malloc(n * sizeof(*sts));
+    memcpy(pk, h_arena, n * slot);
+    for (size_t i = 0; i < n; i++) {
+        in[i] = pk + i * slot;
+        out[i] = pk + i * slot;
+        il[i] = len;
+    }
+    seq0 = 0x1234;
+    double t_batch = 0;
+    for (int it = -1; it < iters; it++) {
+        fill(pk, slot, n, len, seq0);
+        seq0 += (uint32_t)n;
+        for (size_t i = 0; i < n; i++)
+            ol[i] = slot;
+        double t0 = now();
+        CHECK(srtp_protect_batch(s2, n, in, il, out, ol, NULL, sts));
+        if (it >= 0)
+            t_batch += now() - t0;
+        if (sts[0] || ol[0] != len + 10) {
+            fprintf(stderr, "batch status %d len %zu\n", sts[0], ol[0]);
+            return 1;
+        }
+    }
+    t_batch /= iters;
+    double bytes = (double)n * (2.0 * len + 10);
+    printf("{\"packets\": %zu, \"payload\": %zu, \"iters\": %d, "
+           "\"pinned_device_api\": {\"pkt_per_s\": %.1f, \"ms\": %.3f, "
+           "\"algorithmic_GBps\": %.2f, \"pcie_bytes\": %.0f, "
+           "\"device_prepass_batches\": %llu, \"host_prepass_batches\": %llu}, "
+           "\"host_batch_api\": {\"pkt_per_s\": %.1f, \"ms\": %.3f, "
+           "\"algorithmic_GBps\": %.2f}}\n",
+           n, payload, iters, n / t_pinned, t_pinned * 1e3,
+           bytes / t_pinned / 1e9, 2.0 * n * slot + 8.0 * n,
+           (unsigned long long)dev_b, (unsigned long long)host_b,
+           n / t_batch, t_batch * 1e3, bytes / t_batch / 1e9);
+    srtp_dealloc(s1);
+    srtp_dealloc(s2);
+    return 0;
+}
