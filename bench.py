@@ -33,6 +33,8 @@ sys.path.insert(0, ROOT)
 
 CONFIGS = {
     # name: (cipher policy dict, payload bytes, packets per GPU, tag bytes)
+    # g711 = BASELINE configs[3]: 64k SSRC streams, a distinct master key per
+    # stream (SURVEY §8d "primary"), packets round-robin over the streams
     "icm128": (dict(cipher_type=1, cipher_key_len=30, auth_type=3,
                     auth_key_len=20, auth_tag_len=10, sec_serv=3), 1400,
                1 << 20, 10),
@@ -46,12 +48,29 @@ CONFIGS = {
 WORKLOAD = {
     "icm128": "AES-128-ICM + HMAC-SHA1-80 protect, 1M packets x 1400B, 1 stream",
     "gcm256": "AES-256-GCM-16 protect, 1M packets x 1400B per GPU, 1 stream",
-    "g711": "AES-128-ICM + HMAC-SHA1-80 protect, 8M packets x 160B, 1 stream",
+    "g711": "AES-128-ICM + HMAC-SHA1-80 protect, 8M packets x 160B, "
+            "64k SSRC streams (distinct keys, round-robin)",
 }
 # master key: test/srtp_driver.c test_key (46 bytes) -- any key works
 TEST_KEY = ("e1f97a0d3e018be0d64fa32c06de41390ec675ad498afeebb6960b3aabe6"
             "c173c317f2dabe357793b6960b3aabe6")
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+STREAMS = {"icm128": 1, "gcm256": 1, "g711": 65536}
+
+
+def stream_keys(n, seed=0x5352545030303031):
+    """distinct 46-byte master keys (hex) from splitmix64, one per stream"""
+    out, x = [], seed
+    for _ in range(n):
+        b = bytearray()
+        while len(b) < 46:
+            x = (x + 0x9e3779b97f4a7c15) & (2**64 - 1)
+            z = x
+            z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & (2**64 - 1)
+            z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & (2**64 - 1)
+            b += (z ^ (z >> 31)).to_bytes(8, "little")
+        out.append(bytes(b[:46]).hex())
+    return out
 
 
 def parse():
@@ -179,10 +198,17 @@ def main():
 
     pol, payload, npk, tag = CONFIGS[a.config]
     n = a.packets or npk
+    nstreams = STREAMS[a.config]
     ssrc = rank_ssrc(rank)
-    policy = dict(pol, ssrc_type=1, ssrc=ssrc, window_size=128,
-                  allow_repeat_tx=0, keys=[TEST_KEY])
-    sess = L.Session([policy])
+    if nstreams == 1:
+        policies = [dict(pol, ssrc_type=1, ssrc=ssrc, window_size=128,
+                         allow_repeat_tx=0, keys=[TEST_KEY])]
+    else:
+        base = (0x10000000 + (rank << 20)) & 0xffffffff
+        policies = [dict(pol, ssrc_type=1, ssrc=base + k, window_size=128,
+                         allow_repeat_tx=0, keys=[key])
+                    for k, key in enumerate(stream_keys(nstreams, rank + 1))]
+    sess = L.Session(policies)
 
     # packet arena in HBM: slot = roundup16(rtp_len + tag)
     rtp_len = 12 + payload
@@ -194,25 +220,32 @@ def main():
     arena[:, 0] = 0x80
     arena[:, 1] = 96
     arena[:, 4:8] = 0
-    arena[:, 8:12] = torch.tensor(list(ssrc.to_bytes(4, "big")),
-                                  dtype=torch.uint8, device=dev)
+    idx = torch.arange(n, dtype=torch.int64, device=dev)
+    if nstreams == 1:
+        arena[:, 8:12] = torch.tensor(list(ssrc.to_bytes(4, "big")),
+                                      dtype=torch.uint8, device=dev)
+    else:
+        pk_ssrc = base + idx % nstreams         # round-robin over streams
+        for k in range(4):
+            arena[:, 8 + k] = ((pk_ssrc >> (24 - 8 * k)) & 0xff).to(torch.uint8)
+    pk_seq = idx // nstreams                     # per-stream packet number
+    per_stream = (n + nstreams - 1) // nstreams
     flat = arena.view(-1)
     off = torch.arange(n, dtype=torch.int64, device=dev) * slot
     in_len = torch.full((n,), rtp_len, dtype=torch.int32, device=dev)
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
-    idx = torch.arange(n, dtype=torch.int64, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     sess.set_timing(True)
 
     seq_base = [0x1234]
 
     def step():
-        seq = (idx + seq_base[0]) & 0xffff
+        seq = (pk_seq + seq_base[0]) & 0xffff
         arena[:, 2] = (seq >> 8).to(torch.uint8)
         arena[:, 3] = (seq & 0xff).to(torch.uint8)
         out_len.fill_(slot)
-        seq_base[0] += n
+        seq_base[0] += per_stream
         st = sess.protect_device(flat, off, in_len, flat, off, out_len,
                                  status, stream=stream)
         if st != 0:
@@ -251,6 +284,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (random payloads, seq advanced per step)",
         "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": n,
+                   "streams_per_gpu": nstreams,
                    "payload_bytes": payload, "rtp_bytes": rtp_len,
                    "srtp_bytes": rtp_len + tag, "parallelism": "dp%d" % world},
         "payload_GBps": value * payload / 1e9,
@@ -261,7 +295,8 @@ def main():
                      "kernel": kname, "kernel_ms": kernel_ms,
                      "algorithmic_bytes_per_launch": algo_bytes},
         "cpu_baseline": cpu,
-        "prepass": {"device_batches": dev_b, "host_batches": host_b},
+        "prepass": {"device_batches": dev_b, "host_batches": host_b,
+                    "last_abort": sess.prepass_last_abort()},
     }
     print(json.dumps(out))
 

@@ -350,6 +350,11 @@ double srtp_mi355x_last_kernel_ms(srtp_t ctx);
  * their usage limit -- DESIGN.md "Device pre-pass") */
 void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
                                uint64_t *host_batches);
+/* why the most recent srtp_protect_device fallback left the device
+ * pre-pass (0: none so far): 1 unknown SSRC (template clone), 2 stream with MKI / pending ROC
+ * / receiver direction, 4 sequence number not advancing by 1..2^15-1,
+ * 64 empty session, 128 a key near its usage limit */
+int srtp_mi355x_prepass_last_abort(srtp_t ctx);
 /* 1 when a HIP device is usable from this process */
 int srtp_mi355x_gpu_available(void);
 

@@ -160,8 +160,10 @@ typedef struct srtp_gpu_pp_batch {
     uint32_t mask;
 } srtp_gpu_pp_batch_t;
 
-/* pre-pass + crypto for protect.  *fallback = 1: nothing was written (no
- * packet, status or stream state) and the batch must take the host path. */
+/* pre-pass + crypto for protect.  *fallback != 0: nothing was written (no
+ * packet, status or stream state) and the batch must take the host path;
+ * the value is the abort reason: 1 unknown SSRC, 2 ineligible stream,
+ * 4 sequence outside the chain domain (bits may combine). */
 int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
                         int *fallback);
 

@@ -147,6 +147,7 @@ typedef struct {
     uint64_t uses_bound;    /* packets run on the device since the upload  */
     uint32_t uniform, mask;
     uint64_t fast_batches, host_batches;
+    int last_abort;         /* reason of the most recent fallback         */
 } devtab_t;
 
 struct srtp_ctx_t_ {
@@ -168,6 +169,11 @@ struct srtp_ctx_t_ {
 };
 
 static void dev_pull(srtp_t ctx);
+
+/* the session's own stream: host-buffer batches run on it.  Device-API
+ * batches run on the caller's stream, NULL meaning the HIP null stream
+ * (PyTorch's default stream handle is 0). */
+#define HS(ctx) srtp_gpu_stream_of((ctx)->gpu)
 
 /* ------------------------------------------------------------------------
  * SSRC map
@@ -1546,12 +1552,12 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
         off += r16(rtp_len[i] + SRTP_MAX_TRAILER_LEN);
     }
     srtp_err_status_t ret = srtp_err_status_ok;
-    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, NULL) ||
-        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, NULL) ||
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, HS(ctx)) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, HS(ctx)) ||
         run_gpu(ctx, 0, n, sg->d_arena, sg->d_off, sg->d_arena, sg->d_off,
-                sg->h_meta, NULL) ||
-        srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, NULL) ||
-        srtp_gpu_sync(ctx->gpu, NULL)) {
+                sg->h_meta, HS(ctx)) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, HS(ctx)) ||
+        srtp_gpu_sync(ctx->gpu, HS(ctx))) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         ret = srtp_err_status_fail;
     }
@@ -1733,14 +1739,14 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
             mki[i] = srtp[i] + srtp_len[i] - tl - st->mki_size;
     }
     srtp_err_status_t ret = srtp_err_status_ok;
-    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, NULL) ||
-        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, NULL))
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, HS(ctx)) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, HS(ctx)))
         ret = srtp_err_status_fail;
     if (!ret)
         ret = unprotect_core(ctx, n, sum, rtp_len, mki, sg->d_arena, sg->d_off,
-                             sg->d_arena, sg->d_off, status, olen, NULL);
-    if (!ret && (srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, NULL) ||
-                 srtp_gpu_sync(ctx->gpu, NULL)))
+                             sg->d_arena, sg->d_off, status, olen, HS(ctx));
+    if (!ret && (srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, HS(ctx)) ||
+                 srtp_gpu_sync(ctx->gpu, HS(ctx))))
         ret = srtp_err_status_fail;
     for (size_t i = 0; i < n; i++) {
         if (ret) {
@@ -1942,14 +1948,18 @@ static void dev_pull(srtp_t ctx)
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
 {
     devtab_t *dt = &ctx->dt;
-    if (!ctx->n || b->n > 0x7fffffffu)
+    if (!ctx->n || b->n > 0x7fffffffu) {
+        dt->last_abort = 64;
         return 0;
+    }
     if (!dt->valid && dev_build(ctx))
         return -1;
     /* no key can reach its soft limit inside this batch (key.c:74-90) */
     if (dt->num_left_min == UINT64_MAX ||
-        dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT)
+        dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT) {
+        dt->last_abort = 128;
         return 0;
+    }
     srtp_gpu_pp_batch_t pb;
     memset(&pb, 0, sizeof pb);
     pb.n = b->n;
@@ -1967,8 +1977,10 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))
         return -1;
-    if (fallback)
+    if (fallback) {
+        dt->last_abort = fallback;
         return 0;
+    }
     if (ctx->timing)
         ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
     dt->uses_bound += b->n;
@@ -2419,6 +2431,11 @@ void srtp_mi355x_set_timing(srtp_t ctx, int on)
 double srtp_mi355x_last_kernel_ms(srtp_t ctx) { return ctx ? ctx->last_ms : 0; }
 
 int srtp_mi355x_gpu_available(void) { return srtp_gpu_available(); }
+
+int srtp_mi355x_prepass_last_abort(srtp_t ctx)
+{
+    return ctx ? ctx->dt.last_abort : 0;
+}
 
 void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
                                uint64_t *host_batches)

@@ -1163,7 +1163,7 @@ int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b)
 {
     if (b->n == 0)
         return 0;
-    hipStream_t st = b->stream ? (hipStream_t)b->stream : g->stream;
+    hipStream_t st = (hipStream_t)b->stream;   // NULL = the null stream
     if (g->timing)
         HIPCHK(hipEventRecord(g->ev0, st));
     int rc = op == 0 ? run_dir<true>(g, b, st) : run_dir<false>(g, b, st);
@@ -1181,7 +1181,7 @@ int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
 {
     if (!n)
         return 0;
-    hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     hipLaunchKernelGGL(k_undo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        st, arena, off, meta, g->d_keys, (uint32_t)n);
     HIPCHK(hipGetLastError());
@@ -1194,7 +1194,7 @@ int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
 {
     if (!n)
         return 0;
-    hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     hipLaunchKernelGGL(k_parse, dim3((unsigned)((n + 255) / 256)), dim3(256),
                        0, st, in, in_off, in_len, hdr_out, (uint32_t)n);
     HIPCHK(hipGetLastError());
@@ -1235,7 +1235,7 @@ int srtp_gpu_h2d(srtp_gpu_t *g, void *dst, const void *src, size_t n,
 {
     if (!n)
         return 0;
-    hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
     return 0;
 }
@@ -1245,14 +1245,14 @@ int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
 {
     if (!n)
         return 0;
-    hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
     return 0;
 }
 
 int srtp_gpu_sync(srtp_gpu_t *g, void *stream)
 {
-    hipStream_t st = stream ? (hipStream_t)stream : g->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     HIPCHK(hipStreamSynchronize(st));
     return 0;
 }

@@ -332,6 +332,29 @@ int pp_fail(hipError_t e, const char *what)
             return pp_fail(e_, #x);                                            \
     } while (0)
 
+// SRTP_PP_DEBUG=1: synchronise and check after every pre-pass step, naming
+// the step that failed (debug aid; off by default)
+bool pp_debug()
+{
+    static int on = -1;
+    if (on < 0) {
+        const char *e = getenv("SRTP_PP_DEBUG");
+        on = e && *e == '1';
+    }
+    return on;
+}
+
+int pp_step(hipStream_t st, const char *what)
+{
+    if (!pp_debug())
+        return 0;
+    hipError_t e = hipStreamSynchronize(st);
+    if (e == hipSuccess)
+        e = hipGetLastError();
+    fprintf(stderr, "srtp_pp: %-14s %s\n", what, hipGetErrorString(e));
+    return e == hipSuccess ? 0 : pp_fail(e, what);
+}
+
 template <class T>
 int regrow(T **p, uint32_t *cap, uint32_t need)
 {
@@ -482,9 +505,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     }
     if (!P->st || !P->ns || n > 0x7fffffffu)
         return 0;
-    hipStream_t stream = b->stream ? (hipStream_t)b->stream
-                                   : (hipStream_t)srtp_gpu_stream_of(g);
-    if (reserve_packets(P, n, stream))
+    hipStream_t stream = (hipStream_t)b->stream;   // NULL = the null stream
+    if (reserve_packets(P, n, stream) || pp_step(stream, "reserve"))
         return -1;
     const uint32_t N = (uint32_t)n, ns = P->ns;
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
@@ -511,6 +533,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     C.abort = P->abort;
     hipLaunchKernelGGL(k_pp_classify, gp, blk, 0, stream, C);
     PPCHK(hipGetLastError());
+    if (pp_step(stream, "classify"))
+        return -1;
 
     // stable sort by stream id; NOCHAIN keys truncate to all-ones > any sid
     int end_bit = 1;
@@ -520,19 +544,31 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     PPCHK(hipcub::DeviceRadixSort::SortPairs(P->cub, tb, P->skey, P->skey2,
                                              P->perm, P->perm2, (int)N, 0,
                                              end_bit, stream));
+    if (pp_step(stream, "sort"))
+        return -1;
     hipLaunchKernelGGL(k_pp_delta, gp, blk, 0, stream, P->skey2, P->perm2,
                        P->hdr, P->st, ns, N, P->val, P->seg_first, P->abort);
     PPCHK(hipGetLastError());
+    if (pp_step(stream, "delta"))
+        return -1;
     tb = P->cub_bytes;
     PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
         P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
         hipcub::Equality(), stream));
+    if (pp_step(stream, "scan"))
+        return -1;
     hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est, ns,
                        N, P->seg_first, P->bcount, P->new_index);
+    if (pp_step(stream, "seg_end"))
+        return -1;
     hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
                        P->new_index, P->win, P->wnew);
+    if (pp_step(stream, "window"))
+        return -1;
     hipLaunchKernelGGL(k_pp_setbits, gp, blk, 0, stream, P->skey2, P->est,
                        P->st, ns, N, P->new_index, P->wnew);
+    if (pp_step(stream, "setbits"))
+        return -1;
     CommitArgs K;
     K.skey2 = P->skey2;
     K.perm2 = P->perm2;
@@ -547,9 +583,13 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     K.status = b->status;
     K.out_len = b->out_len;
     hipLaunchKernelGGL(k_pp_commit_pkt, gp, blk, 0, stream, K);
+    if (pp_step(stream, "commit_pkt"))
+        return -1;
     hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
                        P->new_index, P->bcount, P->wnew, P->win, P->abort);
     PPCHK(hipGetLastError());
+    if (pp_step(stream, "commit_stream"))
+        return -1;
 
     srtp_gpu_batch_t cb = {};
     cb.n = n;
@@ -565,10 +605,12 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     cb.abort = P->abort;
     if (srtp_gpu_run(g, 0, &cb))
         return -1;
+    if (pp_step(stream, "crypto"))
+        return -1;
     PPCHK(hipMemcpyAsync(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost,
                          stream));
     PPCHK(hipStreamSynchronize(stream));
-    *fallback = *P->h_abort != 0;
+    *fallback = (int)*P->h_abort;   // abort reason bits (AB_*), 0 = done
     return 0;
 }
 

@@ -141,6 +141,7 @@ def lib():
         "srtp_mi355x_gpu_available": ([], C.c_int),
         "srtp_mi355x_prepass_stats": ([P, C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)], None),
+        "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
         "srtp_get_version_string": ([], C.c_char_p),
     }
     for name, (args, res) in sig.items():
@@ -346,6 +347,10 @@ class Session:
 
     def last_kernel_ms(self):
         return self.L.srtp_mi355x_last_kernel_ms(self.h)
+
+    def prepass_last_abort(self):
+        """reason bits of the most recent device pre-pass fallback (0: none)"""
+        return self.L.srtp_mi355x_prepass_last_abort(self.h)
 
     def prepass_stats(self):
         """(device-API batches done by the GPU pre-pass, by the host)"""

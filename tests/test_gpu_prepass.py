@@ -186,3 +186,58 @@ def test_receiver_stream_collision_falls_back():
     pk = [rtp_packet(rng, 0x42, 11 + k, 30) for k in range(5)]
     _check(rx_l, rx_o, pk, [len(p) + 16 for p in pk])
     assert rx_l.prepass_stats()[0] == 0
+
+
+def test_many_streams_round_robin_stay_on_device():
+    """The G.711 bench shape scaled down: 2048 streams with distinct keys,
+    packets round-robin, three consecutive batches -- all on the device
+    pre-pass, bytes equal to the oracle's."""
+    _gpu()
+    rng = random.Random(77)
+    ns, per = 2048, 6
+    ssrcs = [0x10000000 + k for k in range(ns)]
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k) for k, s in
+            enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq0 = 0x1234
+    for b in range(3):
+        pk = [rtp_packet(rng, ssrcs[i % ns], (seq0 + i // ns) & 0xffff, 160)
+              for i in range(ns * per)]
+        _check(lib, orc, pk, [len(p) + 16 for p in pk])
+        assert lib.prepass_last_abort() == 0, (b, lib.prepass_last_abort())
+        seq0 += per
+    assert lib.prepass_stats() == (3, 0)
+
+
+def test_device_api_orders_after_torch_default_stream():
+    """stream=NULL is the HIP null stream (PyTorch's default stream handle
+    is 0): headers and capacities written by torch kernels right before the
+    call must be what the pre-pass reads.  Regression: NULL once meant the
+    session's own non-blocking stream and raced with those writes."""
+    _gpu()
+    import torch
+    n, payload, ns = 1 << 21, 20, 4096
+    pol = [policy("icm128_hmac80", ssrc=0x10000000 + k, seed=k)
+           for k in range(ns)]
+    lib = L.Session(pol)
+    slot = (12 + payload + 10 + 15) & ~15
+    dev = torch.device("cuda", 0)
+    idx = torch.arange(n, dtype=torch.int64, device=dev)
+    for b in range(3):
+        arena = torch.randint(0, 256, (n, slot), dtype=torch.uint8, device=dev)
+        arena[:, 0], arena[:, 1] = 0x80, 96
+        ss = 0x10000000 + idx % ns
+        for k in range(4):
+            arena[:, 8 + k] = ((ss >> (24 - 8 * k)) & 0xff).to(torch.uint8)
+        seq = (0x1234 + b * (n // ns) + idx // ns) & 0xffff
+        arena[:, 2] = (seq >> 8).to(torch.uint8)
+        arena[:, 3] = (seq & 0xff).to(torch.uint8)
+        off = idx * slot
+        ln = torch.full((n,), 12 + payload, dtype=torch.int32, device=dev)
+        cap = torch.full((n,), slot, dtype=torch.int32, device=dev)
+        st = torch.full((n,), -1, dtype=torch.int32, device=dev)
+        flat = arena.view(-1)
+        assert lib.protect_device(flat, off, ln, flat, off, cap, st) == 0
+        assert int((st != 0).sum()) == 0, b
+        assert bool((cap == 12 + payload + 10).all()), b
+    assert lib.prepass_stats() == (3, 0), lib.prepass_last_abort()
