@@ -54,56 +54,90 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
-// LDS tables.  One static array: [0, 64K) AES (T0,T1) x 32 copies,
-// [64K, 128K) GHASH M8 x 16 copies (GCM kernels only).
-constexpr int AES_LDS_BYTES = 256 * 32 * 8;
-constexpr int GH_LDS_BYTES = 256 * 16 * 16;
+// LDS T-tables.  Tk[x] = rotl(T0[x], 8k), T0[x] = (2s, s, s, 3s) bytes LE,
+// s = S[x].  Every table is replicated 32 times so that lane l always reads
+// copy l & 31: a ds_read_b32 of 32 lanes touches 32 distinct banks whatever
+// the byte values are (never bank-conflicted).  Byte address of Tk[x] for
+// lane l:  (k >> 1) << 16 | x << 8 | (k & 1) << 7 | (l & 31) << 2
+// i.e. [0, 64K) holds (T0, T1) rows, [64K, 128K) (T2, T3) rows.  The address
+// of a lookup is ONE v_perm_b32: byte K of the state word -> bits 15:8, the
+// lane's template (table bits + copy offset) -> bytes 0 and 2.
+//   TAB4 = true : all four tables (128 KiB); a MixColumns column is
+//                 xor3(xor3(T0,T1,T2), T3, rk) = 2 VALU
+//   TAB4 = false: T0, T1 only (64 KiB, leaves LDS for the GHASH table);
+//                 T2/T3 are rotations: xor3(T0,T1,rk) ^ rotl16(T0' ^ T1')
+constexpr int AES_TAB2_BYTES = 256 * 32 * 8;           // 64 KiB
+constexpr int AES_TAB4_BYTES = 2 * AES_TAB2_BYTES;     // 128 KiB
+constexpr int GH_LDS_BYTES = 256 * 16 * 16;            // 64 KiB
 
-__device__ uint2 g_ttab[256];   // (T0[x], T1[x]) little-endian words
+__device__ uint32_t g_t0[256];   // T0[x], little-endian word
 
-// LDS image of the AES tables, 64 KiB: for byte value x the 256-byte row
-// x holds T0[x] 32 times (bytes 0..127) then T1[x] 32 times (128..255).
-// Lane l reads copy (l & 31): a ds_read_b32 of 32 lanes touches 32 distinct
-// banks whatever the byte values are, i.e. it is never bank-conflicted.
-DEV void load_aes_table(uint2 *lds2)
+template <bool TAB4>
+DEV void load_aes_tables(void *lds)
 {
-    uint32_t *lds = (uint32_t *)lds2;
-    for (int e = threadIdx.x; e < 256 * 64; e += blockDim.x) {
-        uint2 t = g_ttab[e >> 6];
-        lds[e] = (e & 32) ? t.y : t.x;
+    // 16-byte stores: the 4 dwords of a store are 4 copies of one entry
+    u32x4 *d = (u32x4 *)lds;
+    constexpr int N = (TAB4 ? AES_TAB4_BYTES : AES_TAB2_BYTES) / 16;
+    for (int e = threadIdx.x; e < N; e += blockDim.x) {
+        const int tab = ((e >> 12) << 1) | ((e >> 3) & 1);
+        const uint32_t v = rotl(g_t0[(e >> 4) & 255], 8 * tab);
+        d[e] = u32x4{ v, v, v, v };
     }
 }
 
 struct AesLds {
     const char *lds;
-    uint32_t l0;   // (lane & 31) * 4        -> T0 copy of this lane
-    uint32_t l1;   // (lane & 31) * 4 | 128  -> T1 copy of this lane
+    uint32_t L[2];   // lane templates of tables (0,1) and (2,3): bytes 0, 2
 };
 
 DEV AesLds make_aes_lds(const void *lds)
 {
     AesLds T;
     T.lds = (const char *)lds;
-    T.l0 = (threadIdx.x & 31) * 4;
-    T.l1 = T.l0 | 128u;
+    const uint32_t c = (threadIdx.x & 31) * 4;
+    T.L[0] = c;
+    T.L[1] = 0x10000u | c;
     return T;
 }
 
-// byte K of w -> address bits 15:8, the lane's copy offset -> bits 7:0: one
-// v_perm_b32 per lookup
-template <int K>
-DEV uint32_t t0(const AesLds &T, uint32_t w)
+// address of T_TAB[byte K of w] for an even TAB; odd tables sit +128 bytes
+// further (the ds_read immediate offset)
+template <int TAB, int K>
+DEV uint32_t ta(const AesLds &T, uint32_t w)
 {
-    uint32_t a = __builtin_amdgcn_perm(w, T.l0, 0x0c0c0000u | ((4u + K) << 8));
+    return __builtin_amdgcn_perm(w, T.L[TAB >> 1], 0x0c020000u | ((4u + K) << 8));
+}
+
+DEV uint32_t lds_rd(const AesLds &T, uint32_t a)
+{
     return *(const uint32_t *)(T.lds + a);
 }
 
-template <int K>
-DEV uint32_t t1(const AesLds &T, uint32_t w)
+template <int TAB, int K>
+DEV uint32_t tl(const AesLds &T, uint32_t w)
 {
-    uint32_t a = __builtin_amdgcn_perm(w, T.l1, 0x0c0c0000u | ((4u + K) << 8));
-    return *(const uint32_t *)(T.lds + a);
+    return *(const uint32_t *)(T.lds + ta<TAB, K>(T, w) + (TAB & 1) * 128);
 }
+
+// T2 / T3 lookups: direct with four tables, else T0 / T1 to be rotated
+template <bool TAB4, int K>
+DEV uint32_t tl2(const AesLds &T, uint32_t w) { return tl<TAB4 ? 2 : 0, K>(T, w); }
+template <bool TAB4, int K>
+DEV uint32_t tl3(const AesLds &T, uint32_t w) { return tl<TAB4 ? 3 : 1, K>(T, w); }
+
+// one MixColumns output column from its four lookups (c, d as returned by
+// tl2 / tl3) and the round key word
+template <bool TAB4>
+DEV uint32_t mixcol(uint32_t a, uint32_t b, uint32_t c, uint32_t d,
+                    uint32_t rk)
+{
+    if (TAB4)
+        return xor3(xor3(a, b, c), d, rk);
+    return xor3(a, b, rk) ^ rotl(c ^ d, 16);
+}
+
+template <bool TAB4>
+DEV uint32_t rot2(uint32_t x) { return TAB4 ? x : rotl(x, 16); }
 
 // ---------------------------------------------------------------------------
 // key material access: uniform (scalar loads, SGPRs) or per lane (VGPRs)
@@ -135,102 +169,55 @@ struct UniKey {
     DEV uint32_t operator()(int i) const { return rk[i]; }
 };
 
-// AES encryption of one block held as little-endian words (column c =
-// bytes 4c..4c+3).  Round: col_c = T0[s_c.b0] ^ T1[s_c+1.b1]
-//                                ^ rot16(T0[s_c+2.b2] ^ T1[s_c+3.b3]) ^ rk
-// with T2 = rot16(T0), T3 = rot16(T1).  16 ds_read_b32 + 32 VALU per round.
-template <int NR, class KEY>
-DEV void aes_block(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3,
-                   const KEY &rk, const AesLds &T)
-{
-    s0 ^= rk(0);
-    s1 ^= rk(1);
-    s2 ^= rk(2);
-    s3 ^= rk(3);
-#pragma unroll
-    for (int r = 1; r < NR; r++) {
-        uint32_t a0 = t0<0>(T, s0), a1 = t0<0>(T, s1), a2 = t0<0>(T, s2),
-                 a3 = t0<0>(T, s3);
-        uint32_t b0 = t1<1>(T, s0), b1 = t1<1>(T, s1), b2 = t1<1>(T, s2),
-                 b3 = t1<1>(T, s3);
-        uint32_t c0 = t0<2>(T, s0), c1 = t0<2>(T, s1), c2 = t0<2>(T, s2),
-                 c3 = t0<2>(T, s3);
-        uint32_t d0 = t1<3>(T, s0), d1 = t1<3>(T, s1), d2 = t1<3>(T, s2),
-                 d3 = t1<3>(T, s3);
-        uint32_t n0 = xor3(a0, b1, rk(4 * r + 0)) ^ rotl(c2 ^ d3, 16);
-        uint32_t n1 = xor3(a1, b2, rk(4 * r + 1)) ^ rotl(c3 ^ d0, 16);
-        uint32_t n2 = xor3(a2, b3, rk(4 * r + 2)) ^ rotl(c0 ^ d1, 16);
-        uint32_t n3 = xor3(a3, b0, rk(4 * r + 3)) ^ rotl(c1 ^ d2, 16);
-        s0 = n0;
-        s1 = n1;
-        s2 = n2;
-        s3 = n3;
-    }
-    // final round: S[x] is byte 1 of T0[x] and byte 2 of T1[x]
-    uint32_t a0 = t0<0>(T, s0), a1 = t0<0>(T, s1), a2 = t0<0>(T, s2),
-             a3 = t0<0>(T, s3);
-    uint32_t b0 = t1<1>(T, s0), b1 = t1<1>(T, s1), b2 = t1<1>(T, s2),
-             b3 = t1<1>(T, s3);
-    uint32_t c0 = t0<2>(T, s0), c1 = t0<2>(T, s1), c2 = t0<2>(T, s2),
-             c3 = t0<2>(T, s3);
-    uint32_t d0 = t1<3>(T, s0), d1 = t1<3>(T, s1), d2 = t1<3>(T, s2),
-             d3 = t1<3>(T, s3);
-    const uint32_t LO = 0x0c0c0601u, HI = 0x06010c0cu;
-    uint32_t n0 = xor3(__builtin_amdgcn_perm(b1, a0, LO),
-                       __builtin_amdgcn_perm(d3, c2, HI), rk(4 * NR + 0));
-    uint32_t n1 = xor3(__builtin_amdgcn_perm(b2, a1, LO),
-                       __builtin_amdgcn_perm(d0, c3, HI), rk(4 * NR + 1));
-    uint32_t n2 = xor3(__builtin_amdgcn_perm(b3, a2, LO),
-                       __builtin_amdgcn_perm(d1, c0, HI), rk(4 * NR + 2));
-    uint32_t n3 = xor3(__builtin_amdgcn_perm(b0, a3, LO),
-                       __builtin_amdgcn_perm(d2, c1, HI), rk(4 * NR + 3));
-    s0 = n0;
-    s1 = n1;
-    s2 = n2;
-    s3 = n3;
-}
-
-// NB independent blocks advanced round by round together: the NB*16 table
-// reads of a round are issued back to back, so one wave keeps NB times the
-// LDS requests in flight across the ~100-cycle read latency of a round.
-template <int NB, int NR, class KEY>
-DEV void aes_blocks(uint32_t (&s)[NB][4], const KEY &rk, const AesLds &T)
+// Rounds R0 .. NR-1 and the final round of NB independent blocks, advanced
+// round by round together (the NB*16 table reads of a round are issued back
+// to back).  State: little-endian words, column c = bytes 4c..4c+3.
+//   col_q = T0[s_q.b0] ^ T1[s_q+1.b1] ^ T2[s_q+2.b2] ^ T3[s_q+3.b3] ^ rk
+// Final round: S[x] is byte r of T(r+2 mod 4)[x], so row r of the output
+// column is taken from that table (TAB4), or byte 1 of T0 / byte 2 of T1.
+template <int NB, int NR, bool TAB4, class KEY>
+DEV void aes_rounds(uint32_t (&s)[NB][4], const KEY &rk, const AesLds &T,
+                    int r0)
 {
 #pragma unroll
-    for (int j = 0; j < NB; j++)
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-            s[j][c] ^= rk(c);
-#pragma unroll
-    for (int r = 1; r < NR; r++) {
+    for (int r = r0; r < NR; r++) {
         uint32_t a[NB][4], b[NB][4], c[NB][4], d[NB][4];
 #pragma unroll
         for (int j = 0; j < NB; j++)
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                a[j][q] = t0<0>(T, s[j][q]);
-                b[j][q] = t1<1>(T, s[j][q]);
-                c[j][q] = t0<2>(T, s[j][q]);
-                d[j][q] = t1<3>(T, s[j][q]);
+                a[j][q] = tl<0, 0>(T, s[j][q]);
+                b[j][q] = tl<1, 1>(T, s[j][q]);
+                c[j][q] = tl2<TAB4, 2>(T, s[j][q]);
+                d[j][q] = tl3<TAB4, 3>(T, s[j][q]);
             }
 #pragma unroll
         for (int j = 0; j < NB; j++)
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                s[j][q] = xor3(a[j][q], b[j][(q + 1) & 3], rk(4 * r + q)) ^
-                          rotl(c[j][(q + 2) & 3] ^ d[j][(q + 3) & 3], 16);
+                s[j][q] = mixcol<TAB4>(a[j][q], b[j][(q + 1) & 3],
+                                       c[j][(q + 2) & 3], d[j][(q + 3) & 3],
+                                       rk(4 * r + q));
     }
-    const uint32_t LO = 0x0c0c0601u, HI = 0x06010c0cu;
     uint32_t a[NB][4], b[NB][4], c[NB][4], d[NB][4];
 #pragma unroll
     for (int j = 0; j < NB; j++)
 #pragma unroll
         for (int q = 0; q < 4; q++) {
-            a[j][q] = t0<0>(T, s[j][q]);
-            b[j][q] = t1<1>(T, s[j][q]);
-            c[j][q] = t0<2>(T, s[j][q]);
-            d[j][q] = t1<3>(T, s[j][q]);
+            if (TAB4) {
+                a[j][q] = tl<2, 0>(T, s[j][q]);   // S at byte 0
+                b[j][q] = tl<3, 1>(T, s[j][q]);   // S at byte 1
+                c[j][q] = tl<0, 2>(T, s[j][q]);   // S at byte 2
+                d[j][q] = tl<1, 3>(T, s[j][q]);   // S at byte 3
+            } else {
+                a[j][q] = tl<0, 0>(T, s[j][q]);   // S at byte 1
+                b[j][q] = tl<1, 1>(T, s[j][q]);   // S at byte 2
+                c[j][q] = tl<0, 2>(T, s[j][q]);
+                d[j][q] = tl<1, 3>(T, s[j][q]);
+            }
         }
+    const uint32_t LO = TAB4 ? 0x0c0c0500u : 0x0c0c0601u;
+    const uint32_t HI = TAB4 ? 0x07020c0cu : 0x06010c0cu;
 #pragma unroll
     for (int j = 0; j < NB; j++)
 #pragma unroll
@@ -239,6 +226,104 @@ DEV void aes_blocks(uint32_t (&s)[NB][4], const KEY &rk, const AesLds &T)
                            __builtin_amdgcn_perm(d[j][(q + 3) & 3],
                                                  c[j][(q + 2) & 3], HI),
                            rk(4 * NR + q));
+}
+
+// full AES encryption of NB blocks
+template <int NB, int NR, bool TAB4, class KEY>
+DEV void aes_blocks(uint32_t (&s)[NB][4], const KEY &rk, const AesLds &T)
+{
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+            s[j][c] ^= rk(c);
+    aes_rounds<NB, NR, TAB4>(s, rk, T, 1);
+}
+
+template <int NR, bool TAB4, class KEY>
+DEV void aes_block(uint32_t &s0, uint32_t &s1, uint32_t &s2, uint32_t &s3,
+                   const KEY &rk, const AesLds &T)
+{
+    uint32_t s[1][4] = { { s0, s1, s2, s3 } };
+    aes_blocks<1, NR, TAB4>(s, rk, T);
+    s0 = s[0][0];
+    s1 = s[0][1];
+    s2 = s[0][2];
+    s3 = s[0][3];
+}
+
+// ---------------------------------------------------------------------------
+// Counter-mode caching.  Both SRTP counter modes vary only the last bytes of
+// the counter block within a packet: ICM the 16-bit block counter in bytes
+// 14..15 (aes_icm.c:266-282, the IV's bytes 14..15 are zero), GCM the 32-bit
+// BE counter in bytes 12..15 (inc32).  For the blocks of one "epoch" (all
+// bytes but byte 15 fixed -- 256 blocks = 4 KiB of payload) the state after
+// round 1 differs only in column 0, through one T3 lookup on byte 15, and
+// after round 2 every column differs only through one lookup on that column.
+// So rounds 1 and 2 cost 1 + 4 table reads per block instead of 32.
+struct CtrCache {
+    uint32_t a3;      // LDS address of T3[byte 15 of (ctr ^ rk0)] for jlo = 0
+    uint32_t k1;      // round-1 column 0 without its T3 term
+    uint32_t k2[4];   // round-2 columns without their column-0 term
+};
+
+// c: the counter block with byte 15 = 0 (little-endian words)
+template <int NR, bool TAB4, class KEY>
+DEV CtrCache ctr_cache(const uint32_t c[4], const KEY &rk, const AesLds &T)
+{
+    const uint32_t s0 = c[0] ^ rk(0), s1 = c[1] ^ rk(1), s2 = c[2] ^ rk(2),
+                   s3 = c[3] ^ rk(3);
+    CtrCache C;
+    C.a3 = ta<TAB4 ? 3 : 1, 3>(T, s3) | 128u;
+    C.k1 = xor3(tl<0, 0>(T, s0), tl<1, 1>(T, s1), rk(4)) ^
+           rot2<TAB4>(tl2<TAB4, 2>(T, s2));
+    const uint32_t u1 = mixcol<TAB4>(tl<0, 0>(T, s1), tl<1, 1>(T, s2),
+                                     tl2<TAB4, 2>(T, s3), tl3<TAB4, 3>(T, s0),
+                                     rk(5));
+    const uint32_t u2 = mixcol<TAB4>(tl<0, 0>(T, s2), tl<1, 1>(T, s3),
+                                     tl2<TAB4, 2>(T, s0), tl3<TAB4, 3>(T, s1),
+                                     rk(6));
+    const uint32_t u3 = mixcol<TAB4>(tl<0, 0>(T, s3), tl<1, 1>(T, s0),
+                                     tl2<TAB4, 2>(T, s1), tl3<TAB4, 3>(T, s2),
+                                     rk(7));
+    C.k2[0] = xor3(tl<1, 1>(T, u1), rk(8),
+                   rot2<TAB4>(tl2<TAB4, 2>(T, u2)) ^
+                       rot2<TAB4>(tl3<TAB4, 3>(T, u3)));
+    C.k2[1] = xor3(tl<0, 0>(T, u1), tl<1, 1>(T, u2), rk(9)) ^
+              rot2<TAB4>(tl2<TAB4, 2>(T, u3));
+    C.k2[2] = xor3(tl<0, 0>(T, u2), tl<1, 1>(T, u3), rk(10)) ^
+              rot2<TAB4>(tl3<TAB4, 3>(T, u1));
+    C.k2[3] = xor3(tl<0, 0>(T, u3), rk(11),
+                   rot2<TAB4>(tl2<TAB4, 2>(T, u1)) ^
+                       rot2<TAB4>(tl3<TAB4, 3>(T, u2)));
+    return C;
+}
+
+// NB counter blocks of the cached epoch; jb[j] = (byte 15 of block j) << 8
+template <int NB, int NR, bool TAB4, class KEY>
+DEV void aes_ctr(uint32_t (&s)[NB][4], const uint32_t (&jb)[NB],
+                 const CtrCache &C, const KEY &rk, const AesLds &T)
+{
+    uint32_t u0[NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++)
+        u0[j] = C.k1 ^ rot2<TAB4>(lds_rd(T, C.a3 ^ jb[j]));
+    uint32_t a[NB], b[NB], c[NB], d[NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        a[j] = tl<0, 0>(T, u0[j]);
+        b[j] = tl<1, 1>(T, u0[j]);
+        c[j] = tl2<TAB4, 2>(T, u0[j]);
+        d[j] = tl3<TAB4, 3>(T, u0[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        s[j][0] = C.k2[0] ^ a[j];
+        s[j][1] = C.k2[1] ^ rot2<TAB4>(d[j]);
+        s[j][2] = C.k2[2] ^ rot2<TAB4>(c[j]);
+        s[j][3] = C.k2[3] ^ b[j];
+    }
+    aes_rounds<NB, NR, TAB4>(s, rk, T, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -362,50 +447,73 @@ struct IcmArgs {
     uint32_t uni;   // uniform key slot
 };
 
-#ifndef ICM_WAVES_PER_SIMD
-#define ICM_WAVES_PER_SIMD 1
-#endif
 #ifndef ICM_NB
 #define ICM_NB 2   // AES blocks interleaved per round in the steady state
 #endif
+#ifndef ICM_COOP
+#define ICM_COOP 1   // wave-cooperative coalesced loads / aligned stores
+#endif
+
+// per-packet constants of the chunk loop
+struct IcmPkt {
+    const uint8_t *in;
+    uint8_t *out;
+    uint32_t L;        // end of the authenticated region (header + payload)
+    uint32_t hw;       // header words (enc_start / 4)
+    uint32_t s;        // hw & 3: keystream word shift inside a 16-byte quad
+    uint32_t qoff;     // hw >> 2: quads before the first keystream block
+    uint32_t nq;       // quads holding data
+    uint32_t nb;       // 64-byte chunks (incl. the SHA-1 tail)
+    uint32_t bclean;   // first chunk past the header
+    uint32_t P;        // payload bytes
+    uint32_t roc;
+    bool conf;
+    uint32_t cb[4];    // counter block, block counter (bytes 14..15) zero
+};
 
 // One 64-byte chunk b of a packet in its general form: header words that
 // are not encrypted, quads past the end of the data, the partial last quad
 // (kept in tailq, stored once after the chunk loop: a byte-wise store here,
 // unrolled per quad, costs ~65 VGPRs), and the ROC / terminator / length
-// words of the SHA-1 message tail (sha1.c srtp_sha1_final).
-template <int NR, bool AUTH, bool PROTECT, class KEY>
-DEV void icm_chunk(uint32_t b, const uint8_t *in, uint8_t *out, uint32_t L,
-                   uint32_t hw, uint32_t s, uint32_t qoff, uint32_t nq,
-                   uint32_t nb, uint32_t bclean, bool conf, uint32_t roc,
-                   const uint32_t cb[4], const KEY &rk, const AesLds &T,
-                   uint32_t ks_prev[4], uint32_t hst[5], uint32_t tailq[4])
+// words of the SHA-1 message tail (sha1.c srtp_sha1_final).  Full AES for
+// the keystream blocks that any payload byte uses.
+template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_chunk(uint32_t b, const IcmPkt &p, const KEY &rk,
+                   const AesLds &T, uint32_t ks_prev[4], uint32_t hst[5],
+                   uint32_t tailq[4], u32x4 (&oq)[4])
 {
     const uint32_t q0 = 4 * b;
-    const uint8_t *ip = in + 16 * q0;
-    uint8_t *op = out + 16 * q0;
+    const uint8_t *ip = p.in + 16 * q0;
+    uint8_t *op = p.out + 16 * q0;
     u32x4 v[4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         v[t] = u32x4{ 0, 0, 0, 0 };
-        if (q0 + t < nq)
+        if (q0 + t < p.nq)
             v[t] = *(const u32x4 *)(ip + 16 * t);
     }
     uint32_t ks[4][4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
-        const uint32_t jj = q0 + t - qoff;
-        ks[t][0] = cb[0];
-        ks[t][1] = cb[1];
-        ks[t][2] = cb[2];
-        ks[t][3] = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+        const uint32_t jj = q0 + t - p.qoff;
+        ks[t][0] = p.cb[0];
+        ks[t][1] = p.cb[1];
+        ks[t][2] = p.cb[2];
+        ks[t][3] = p.cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
     }
-    if (conf) {
+    if constexpr (NR > 0) {
+        if (p.conf) {
 #pragma unroll
-        for (int g = 0; g < 4; g += ICM_NB)
-            aes_blocks<ICM_NB, NR ? NR : 1>(
-                *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), rk, T);
-    } else {
+            for (int g = 0; g < 4; g += ICM_NB) {
+                const int jf = (int)(q0 + g) - (int)p.qoff;
+                if (jf + ICM_NB - 1 >= 0 && 16 * jf < (int)p.P)
+                    aes_blocks<ICM_NB, NR, TAB4>(
+                        *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), rk,
+                        T);
+            }
+        }
+    }
+    if (NR == 0 || !p.conf) {
 #pragma unroll
         for (int t = 0; t < 4; t++)
             ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
@@ -415,20 +523,20 @@ DEV void icm_chunk(uint32_t b, const uint8_t *in, uint8_t *out, uint32_t L,
     for (int t = 0; t < 4; t++) {
         const uint32_t q = q0 + t;
         uint32_t kk[4];
-        ks_shift(ks_prev, ks[t], s, kk);
-        if (b < bclean) {
+        ks_shift(ks_prev, ks[t], p.s, kk);
+        if (b < p.bclean) {
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                if (4 * q + u < hw)
+                if (4 * q + u < p.hw)
                     kk[u] = 0;   // header words are never encrypted
         }
         uint32_t o[4] = { v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
                           v[t].w ^ kk[3] };
-        if (16 * q + 16 <= L) {
+        oq[t] = u32x4{ o[0], o[1], o[2], o[3] };
+        if (16 * q + 16 <= p.L) {
             *(u32x4 *)(op + 16 * t) = u32x4{ o[0], o[1], o[2], o[3] };
-        } else if (16 * q < L) {
-            // the one partial quad: stored after the loop (a byte-wise
-            // store here, unrolled per quad, costs ~65 VGPRs)
+        } else if (16 * q < p.L) {
+            // the one partial quad: stored after the loop
 #pragma unroll
             for (int u = 0; u < 4; u++)
                 tailq[u] = o[u];
@@ -440,37 +548,318 @@ DEV void icm_chunk(uint32_t b, const uint8_t *in, uint8_t *out, uint32_t L,
         }
     }
     if (AUTH) {
-        if (64 * b + 64 > L) {
+        if (64 * b + 64 > p.L) {
             // message tail: ROC, the 0x80 terminator, zero padding and
             // the bit length (sha1.c srtp_sha1_final)
 #pragma unroll
             for (int g = 0; g < 16; g++)
-                wv[g] = tail_word(wv[g], (int)L - (int)(64 * b + 4 * g),
-                                  roc);
-            if (b == nb - 1) {
+                wv[g] = tail_word(wv[g], (int)p.L - (int)(64 * b + 4 * g),
+                                  p.roc);
+            if (b == p.nb - 1) {
                 wv[14] = 0;
-                wv[15] = (64 + L + 4) * 8;
+                wv[15] = (64 + p.L + 4) * 8;
             }
         }
         sha1_compress(hst, wv);
     }
 }
 
-// AES-ICM + HMAC-SHA1 protect / unprotect: one lane per packet.
-template <int NR, bool AUTH, bool PROTECT, bool UNIFORM>
-__global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
+// A payload chunk in the steady state: four full 16-byte quads, no header
+// word, no message tail, all keystream blocks in the cached counter epoch,
+// and the keystream word shift S (= header words mod 4) a compile-time
+// constant, so aligning the keystream to the quads is register renaming.
+// The chunk's data v was loaded ICM_PF chunks earlier (icm_steady_run).
+template <int S, int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_steady(uint32_t b, const IcmPkt &p, const u32x4 (&v)[4],
+                    const CtrCache &C, const KEY &rk, const AesLds &T,
+                    uint32_t ks_prev[4], uint32_t hst[5])
 {
-    __shared__ uint2 s_tab[256 * 32];
-    if (A.abort && *A.abort)
-        return;
-    if (NR)
-        load_aes_table(s_tab);
-    __syncthreads();
-    const AesLds T = make_aes_lds(s_tab);
+    uint8_t *op = p.out + 64 * b;
+    uint32_t ks[4][4];
+#ifdef ICM_EXP_NOAES   // timing experiment only: no keystream
+    if constexpr (false) {
+#else
+    if constexpr (NR > 0) {
+#endif
+        if (p.conf) {
+            const uint32_t jb0 = ((4 * b - p.qoff) & 0xffu) << 8;
+#pragma unroll
+            for (int g = 0; g < 4; g += ICM_NB) {
+                uint32_t jb[ICM_NB];
+#pragma unroll
+                for (int j = 0; j < ICM_NB; j++)
+                    jb[j] = jb0 + ((uint32_t)(g + j) << 8);
+                aes_ctr<ICM_NB, NR, TAB4>(
+                    *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), jb, C,
+                    rk, T);
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+    }
+    uint32_t wv[16];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        u32x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t k = u >= S ? ks[t][u - S]
+                                      : (t ? ks[t - 1][u - S + 4]
+                                           : ks_prev[u - S + 4]);
+            o[u] = v[t][u] ^ k;
+        }
+        *(u32x4 *)(op + 16 * t) = o;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        ks_prev[u] = ks[3][u];
+#ifdef ICM_EXP_NOSHA   // timing experiment only: fold instead of compress
+    if (AUTH)
+        hst[0] ^= xor3(wv[0], wv[5], wv[10]) ^ wv[15];
+#else
+    if (AUTH)
+        sha1_compress(hst, wv);
+#endif
+}
 
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n)
-        return;
+#ifndef ICM_PF
+#define ICM_PF 1   // chunks of packet data loaded ahead of their use
+#endif
+
+DEV void load_chunk(u32x4 (&v)[4], const uint8_t *ip)
+{
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+        v[t] = *(const u32x4 *)(ip + 16 * t);
+}
+
+// The steady chunks [b, e) with the packet data loaded ICM_PF chunks ahead:
+// one lane's loads are 16-byte pieces of its own packet (64 lanes, 64
+// cache lines per wave instruction), so the HBM latency is hidden only if
+// loads stay in flight across the AES + SHA-1 work of whole chunks.
+template <int S, int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_steady_run(uint32_t &b, uint32_t e, const IcmPkt &p,
+                        const CtrCache &C, const KEY &rk, const AesLds &T,
+                        uint32_t ks_prev[4], uint32_t hst[5])
+{
+    u32x4 ring[ICM_PF][4];
+#pragma unroll
+    for (int k = 0; k < ICM_PF; k++)
+        if (b + k < e)
+            load_chunk(ring[k], p.in + 64 * (b + k));
+    for (; b < e; b++) {
+        u32x4 cur[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            cur[t] = ring[0][t];
+#pragma unroll
+        for (int k = 0; k + 1 < ICM_PF; k++)
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                ring[k][t] = ring[k + 1][t];
+        if (b + ICM_PF < e)
+            load_chunk(ring[ICM_PF - 1], p.in + 64 * (b + ICM_PF));
+        icm_steady<S, NR, TAB4, AUTH, PROTECT>(b, p, cur, C, rk, T, ks_prev,
+                                               hst);
+    }
+}
+
+
+// ---------------------------------------------------------------------------
+// Wave-cooperative steady state (uniform-key batches).  One lane per packet
+// makes every wave instruction touch 64 packets 1424 B apart: measured on
+// MI355X (tools/memtest.hip) such a copy streams at 2.2-2.7 TB/s, and the
+// stores are the worse half -- a 64-B chunk of a packet is rarely 64-B
+// aligned, so every aligned 64-B segment is written in two pieces ~1 us
+// apart.  Here the four lanes of a lane-quad move 64 contiguous bytes of ONE
+// packet per instruction, and stores are whole aligned 64-B segments:
+//   * lane L owns packet 16*(L&3) + (L>>2) of the wave's 64, so quad m holds
+//     packets m, 16+m, 32+m, 48+m and every exchange stays inside the quad;
+//   * load instruction j: lanes 4m..4m+3 read chunk b (64 B) of packet
+//     16j+m; a 4x4 transpose of 16-B elements (DPP quad_perm + selects)
+//     hands each lane its own packet's chunk;
+//   * the output of chunk b-1 and b, funnel-shifted by the packet's 16-B
+//     misalignment r0, is aligned segment b; transposed back, instruction j
+//     stores segment b of packet 16j+m as 64 contiguous aligned bytes.
+// Measured copy rates of these shapes: quad loads 4.9 TB/s read-only,
+// quad + aligned copy 3.6-3.8 TB/s, vs 2.4 / 2.65 for lane-per-packet.
+template <int CTRL>
+DEV uint32_t qperm(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+
+// m ? a : b on all lanes (a bit-select: written as a ternary the compiler
+// turns the DPP operand into an exec-masked branch, and a DPP read from a
+// lane that is masked off returns 0)
+DEV uint32_t bsel(uint32_t m, uint32_t a, uint32_t b)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, m, 0xE4);
+}
+
+typedef const u32x4 __attribute__((address_space(1))) *gcptr;
+typedef u32x4 __attribute__((address_space(1))) *gptr;
+
+template <int J>
+DEV uint64_t qbcast64(uint64_t v)   // value of lane (L & ~3) + J
+{
+    constexpr int C = J | (J << 2) | (J << 4) | (J << 6);
+    const uint32_t lo = qperm<C>((uint32_t)v), hi = qperm<C>((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Y[t] of lane j (in its quad) = X[j] of lane t: 4x4 transpose of 16-B
+// elements inside each lane quad, in two 2x2 stages
+DEV void quad_transpose(u32x4 (&x)[4])
+{
+    const uint32_t q = threadIdx.x & 3;
+    const uint32_t j1 = 0u - ((q >> 1) & 1), j0 = 0u - (q & 1);   // masks
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+        const uint32_t x0 = x[0][c], x1 = x[1][c], x2 = x[2][c], x3 = x[3][c];
+        const uint32_t p0 = qperm<0x4E>(x0), p1 = qperm<0x4E>(x1),
+                       p2 = qperm<0x4E>(x2), p3 = qperm<0x4E>(x3);
+        const uint32_t z0 = bsel(j1, p2, x0), z2 = bsel(j1, x2, p0);
+        const uint32_t z1 = bsel(j1, p3, x1), z3 = bsel(j1, x3, p1);
+        const uint32_t r0 = qperm<0xB1>(z0), r1 = qperm<0xB1>(z1),
+                       r2 = qperm<0xB1>(z2), r3 = qperm<0xB1>(z3);
+        x[0][c] = bsel(j0, r1, z0);
+        x[1][c] = bsel(j0, z1, r0);
+        x[2][c] = bsel(j0, r3, z2);
+        x[3][c] = bsel(j0, z3, r2);
+    }
+}
+
+// aligned segment = quads [4 - r0, 8 - r0) of prev ++ cur
+DEV void seg_funnel(const u32x4 (&prev)[4], const u32x4 (&cur)[4], uint32_t r0,
+                    u32x4 (&seg)[4])
+{
+    const uint32_t a = 0u - ((r0 >> 1) & 1), c = 0u - (r0 & 1);   // masks
+    u32x4 e[5];   // e[k + 1] = C[4 - 2a + k], k = -1..3
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        e[0][u] = bsel(a, prev[1][u], prev[3][u]);
+        e[1][u] = bsel(a, prev[2][u], cur[0][u]);
+        e[2][u] = bsel(a, prev[3][u], cur[1][u]);
+        e[3][u] = bsel(a, cur[0][u], cur[2][u]);
+        e[4][u] = bsel(a, cur[1][u], cur[3][u]);
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            seg[t][u] = bsel(c, e[t][u], e[t + 1][u]);
+}
+
+// per-lane targets of the cooperative loads / stores: for j = 0..3 the
+// packet owned by lane (L & ~3) + j
+struct CoopPtr {
+    const uint8_t *in[4];    // + 16 * (L & 3): this lane's quad of a chunk
+    uint8_t *seg[4];         // aligned segment 0 base + 16 * (L & 3)
+};
+
+template <int S, int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_coop_run(uint32_t &b, uint32_t e, const IcmPkt &p,
+                      const CtrCache &C, const KEY &rk, const AesLds &T,
+                      uint32_t ks_prev[4], uint32_t hst[5], u32x4 (&prev)[4],
+                      const CoopPtr &cp, uint32_t r0)
+{
+    u32x4 nx[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        nx[j] = *(gcptr)(cp.in[j] + 64 * b);
+    for (; b < e; b++) {
+        u32x4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            v[j] = nx[j];
+        if (b + 1 < e) {
+#pragma unroll
+            for (int j = 0; j < 4; j++)
+                nx[j] = *(gcptr)(cp.in[j] + 64 * (b + 1));
+        }
+        quad_transpose(v);
+        uint32_t ks[4][4];
+        if constexpr (NR > 0) {
+            if (p.conf) {
+                const uint32_t jb0 = ((4 * b - p.qoff) & 0xffu) << 8;
+#pragma unroll
+                for (int g = 0; g < 4; g += ICM_NB) {
+                    uint32_t jb[ICM_NB];
+#pragma unroll
+                    for (int j = 0; j < ICM_NB; j++)
+                        jb[j] = jb0 + ((uint32_t)(g + j) << 8);
+                    aes_ctr<ICM_NB, NR, TAB4>(
+                        *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), jb,
+                        C, rk, T);
+                }
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+        }
+        u32x4 o[4];
+        uint32_t wv[16];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t k = u >= S ? ks[t][u - S]
+                                          : (t ? ks[t - 1][u - S + 4]
+                                               : ks_prev[u - S + 4]);
+                o[t][u] = v[t][u] ^ k;
+                wv[4 * t + u] = bswap(PROTECT ? o[t][u] : v[t][u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            ks_prev[u] = ks[3][u];
+        u32x4 sg[4];
+        seg_funnel(prev, o, r0, sg);
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            prev[t] = o[t];
+        quad_transpose(sg);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            *(gptr)(cp.seg[j] + 64 * b) = sg[j];
+        if (AUTH)
+            sha1_compress(hst, wv);
+    }
+    // quads 4e - r0 .. 4e - 1 (the head of segment e) are not stored yet
+#pragma unroll
+    for (int t = 1; t < 4; t++)
+        if (4 - (int)r0 <= t)
+            *(u32x4 *)(p.out + 16 * (4 * e - 4 + t)) = prev[t];
+}
+
+// all 64 lanes active and in the same steady state: the cooperative path
+DEV bool wave_uniform(uint32_t x)
+{
+    return __builtin_amdgcn_ballot_w64(x == (uint32_t)__builtin_amdgcn_readfirstlane(x)) ==
+           ~0ull;
+}
+
+// one packet, front to back: header chunks, steady payload chunks, tail
+// chunks, partial quad, outer hash, tag (srtp.c:2694-2818 protect,
+// 2987-3093 unprotect: the tag is compared, the caller decides)
+template <int NR, bool TAB4, bool AUTH, bool PROTECT, bool UNIFORM, class KEY>
+DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
+{
     const srtp_dev_meta_t m = A.meta[i];
     constexpr uint32_t VID = (NR == 0 ? 0u : 8u + 2u * ((NR - 8) / 2)) +
                              (AUTH ? 1u : 0u);
@@ -478,27 +867,32 @@ __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
         return;
     const uint32_t slot = UNIFORM ? A.uni : m.key;
     const srtp_dev_key_t *key = A.keys + slot;
-
-    typename std::conditional<UNIFORM, UniKey<NR ? NR : 1>,
-                              LaneKey<NR ? NR : 1>>::type rk;
-    if (NR)
+    if constexpr (!UNIFORM && NR > 0)
         rk.load(key);
 
-    const uint8_t *in = A.in + A.in_off[i];
-    uint8_t *out = A.out + A.out_off[i];
+    IcmPkt p;
+    p.in = A.in + A.in_off[i];
+    p.out = A.out + A.out_off[i];
     const uint32_t enc_start = SRTP_META_ENC_START(m.info);
-    const uint32_t L = m.len;                 // end of auth'd region
-    const uint32_t hw = enc_start >> 2, s = hw & 3, qoff = hw >> 2;
-    const bool conf = NR != 0 && key->conf != 0;
+    p.L = m.len;
+    p.hw = enc_start >> 2;
+    p.s = p.hw & 3;
+    p.qoff = p.hw >> 2;
+    p.P = p.L - enc_start;
+    p.roc = m.roc;
+    p.conf = NR != 0 && key->conf != 0;
+    p.nq = (p.L + 15) >> 4;
+    p.nb = AUTH ? ((p.L + 12) >> 6) + 1 : ((p.nq + 3) >> 2);
+    p.bclean = (p.qoff + 4) >> 2;
 
     // counter block (little-endian words), block counter j in bytes 14..15
-    const uint32_t w0 = *(const uint32_t *)in;
+    // (aes_icm.c:236-258 IV formation, srtp.c:2694-2707)
+    const uint32_t w0 = *(const uint32_t *)p.in;
     const uint32_t seq = bswap(w0) & 0xffffu;
-    uint32_t cb[4];
-    cb[0] = key->salt[0];
-    cb[1] = key->salt[1] ^ *(const uint32_t *)(in + 8);   // SSRC bytes
-    cb[2] = key->salt[2] ^ bswap(m.roc);
-    cb[3] = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
+    p.cb[0] = key->salt[0];
+    p.cb[1] = key->salt[1] ^ *(const uint32_t *)(p.in + 8);   // SSRC bytes
+    p.cb[2] = key->salt[2] ^ bswap(m.roc);
+    p.cb[3] = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
 
     uint32_t hst[5];
 #pragma unroll
@@ -506,77 +900,96 @@ __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
         hst[k] = AUTH ? key->ipad[k] : 0;
 
     uint32_t ks_prev[4] = { 0, 0, 0, 0 };
-    const uint32_t nq = (L + 15) >> 4;             // quads holding data
-    const uint32_t nb = AUTH ? ((L + 12) >> 6) + 1 : ((nq + 3) >> 2);
-    const uint32_t bclean = (qoff + 4) >> 2;       // first chunk past header
-
-    // One code path for every 64-byte chunk (header, payload, tail): the
-    // header / tail / padding handling sits in branches that are not taken
-    // in the steady state, so the loop keeps the register footprint of the
-    // plain payload chunk (<= 128 VGPRs -> 4 waves per SIMD).  Keystream
-    // blocks over header quads or past the payload are computed and masked
-    // or never stored.
     uint32_t tailq[4] = { 0, 0, 0, 0 };
-    // header chunks, then the payload chunks (branch-free: no header word,
-    // no tail, full 16-byte loads and stores), then the tail chunks
-    const uint32_t nfull = L >> 6;
+    u32x4 prev[4];   // output quads of the last chunk done
     uint32_t b = 0;
-    for (; b < bclean && b < nb; b++)
-        icm_chunk<NR, AUTH, PROTECT>(b, in, out, L, hw, s, qoff, nq, nb, bclean,
-                                     conf, m.roc, cb, rk, T, ks_prev, hst,
-                                     tailq);
-    for (; b < nfull; b++) {
-        const uint8_t *ip = in + 64 * b;
-        uint8_t *op = out + 64 * b;
-        u32x4 v[4];
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            v[t] = *(const u32x4 *)(ip + 16 * t);
-        uint32_t ks[4][4];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            const uint32_t jj = 4 * b + t - qoff;
-            ks[t][0] = cb[0];
-            ks[t][1] = cb[1];
-            ks[t][2] = cb[2];
-            ks[t][3] = cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+    for (; b < p.bclean && b < p.nb; b++)
+        icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, rk, T, ks_prev, hst, tailq,
+                                           prev);
+
+    // steady chunks: full chunks whose blocks j = 4b+t-qoff stay in counter
+    // epoch 0 (j <= 255, 4 KiB of payload)
+    uint32_t se = p.L >> 6;
+    se = se < ((256 + p.qoff) >> 2) ? se : ((256 + p.qoff) >> 2);
+    if (b < se) {
+        CtrCache C{};
+        if constexpr (NR > 0) {
+            if (p.conf)
+                C = ctr_cache<NR, TAB4>(p.cb, rk, T);
         }
-        if (conf) {
-#pragma unroll
-            for (int g = 0; g < 4; g += ICM_NB)
-                aes_blocks<ICM_NB, NR ? NR : 1>(
-                    *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), rk, T);
+        bool coop = false;
+        if constexpr (UNIFORM && ICM_COOP) {
+            // every lane of the wave active, 16-B aligned and in the same
+            // steady range / keystream shift: the cooperative path
+            const uint32_t al =
+                (uint32_t)(((uintptr_t)p.in | (uintptr_t)p.out) & 15);
+            coop = wave_uniform(b) && wave_uniform(se) && wave_uniform(p.s) &&
+                   wave_uniform(p.conf ? 1u : 0u) &&
+                   __builtin_amdgcn_ballot_w64(al == 0) == ~0ull;
+        }
+        if (coop) {
+            const uint64_t lq = 16 * (threadIdx.x & 3);
+            const uint64_t pin = (uint64_t)(uintptr_t)p.in;
+            const uint64_t seg0 = (uint64_t)(uintptr_t)p.out & ~63ull;
+            const uint32_t r0 = (uint32_t)(((uintptr_t)p.out >> 4) & 3);
+            CoopPtr cp;
+            cp.in[0] = (const uint8_t *)(uintptr_t)(qbcast64<0>(pin) + lq);
+            cp.in[1] = (const uint8_t *)(uintptr_t)(qbcast64<1>(pin) + lq);
+            cp.in[2] = (const uint8_t *)(uintptr_t)(qbcast64<2>(pin) + lq);
+            cp.in[3] = (const uint8_t *)(uintptr_t)(qbcast64<3>(pin) + lq);
+            cp.seg[0] = (uint8_t *)(uintptr_t)(qbcast64<0>(seg0) + lq);
+            cp.seg[1] = (uint8_t *)(uintptr_t)(qbcast64<1>(seg0) + lq);
+            cp.seg[2] = (uint8_t *)(uintptr_t)(qbcast64<2>(seg0) + lq);
+            cp.seg[3] = (uint8_t *)(uintptr_t)(qbcast64<3>(seg0) + lq);
+            switch (p.s) {
+            case 0:
+                icm_coop_run<0, NR, TAB4, AUTH, PROTECT>(
+                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                break;
+            case 1:
+                icm_coop_run<1, NR, TAB4, AUTH, PROTECT>(
+                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                break;
+            case 2:
+                icm_coop_run<2, NR, TAB4, AUTH, PROTECT>(
+                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                break;
+            default:
+                icm_coop_run<3, NR, TAB4, AUTH, PROTECT>(
+                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                break;
+            }
         } else {
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
-        }
-        uint32_t wv[16];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            uint32_t kk[4];
-            ks_shift(ks_prev, ks[t], s, kk);
-            u32x4 o = { v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
-                        v[t].w ^ kk[3] };
-            *(u32x4 *)(op + 16 * t) = o;
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
-                ks_prev[u] = ks[t][u];
+            switch (p.s) {
+            case 0:
+                icm_steady_run<0, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                           ks_prev, hst);
+                break;
+            case 1:
+                icm_steady_run<1, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                           ks_prev, hst);
+                break;
+            case 2:
+                icm_steady_run<2, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                           ks_prev, hst);
+                break;
+            default:
+                icm_steady_run<3, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                           ks_prev, hst);
+                break;
             }
         }
-        if (AUTH)
-            sha1_compress(hst, wv);
     }
-    for (; b < nb; b++)
-        icm_chunk<NR, AUTH, PROTECT>(b, in, out, L, hw, s, qoff, nq, nb, bclean,
-                                     conf, m.roc, cb, rk, T, ks_prev, hst,
-                                     tailq);
-    if (L & 15)
-        store_words_partial(out + (L & ~15u), tailq, (int)(L & 15));
+    for (; b < p.nb; b++)
+        icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, rk, T, ks_prev, hst, tailq,
+                                           prev);
+    if (p.L & 15)
+        store_words_partial(p.out + (p.L & ~15u), tailq, (int)(p.L & 15));
 
     const uint32_t tag_len = key->tag_len;
     const uint32_t mki_size = key->mki_size;
+    const uint32_t L = p.L;
+    uint8_t *out = p.out;
     if (!AUTH) {
         if (PROTECT && mki_size) {
             for (uint32_t u = 0; u < mki_size; u++)
@@ -587,7 +1000,7 @@ __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
         return;
     }
 
-    // outer hash: SHA1(opad || inner)
+    // outer hash: SHA1(opad || inner)  (hmac.c:181-229)
     uint32_t ow[16];
 #pragma unroll
     for (int k = 0; k < 5; k++)
@@ -610,12 +1023,58 @@ __global__ __launch_bounds__(512, ICM_WAVES_PER_SIMD) void k_icm_hmac(IcmArgs A)
         for (uint32_t u = 0; u < tag_len; u++)
             tp[u] = (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3)));
     } else {
-        const uint8_t *tp = in + L + mki_size;
+        const uint8_t *tp = p.in + L + mki_size;
         uint32_t diff = 0;
         for (uint32_t u = 0; u < tag_len; u++)
             diff |= (uint32_t)(tp[u] ^ (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3))));
         A.auth_ok[i] = diff == 0;
     }
+}
+
+// Uniform-key batches: all four T-tables (128 KiB of LDS, one workgroup of
+// 1024 lanes per CU = 4 waves per SIMD, <= 128 VGPRs), the AES schedule in
+// SGPRs.  Per-lane keys: (T0, T1) only, 512 lanes, the schedule in VGPRs.
+// Persistent: the grid is sized to the CUs and each workgroup walks the
+// batch, so the tables are loaded once per CU.
+#ifndef ICM_UNI_THREADS
+#define ICM_UNI_THREADS 512
+#endif
+
+#ifndef ICM_UNI_TAB4
+#define ICM_UNI_TAB4 1
+#endif
+#ifndef ICM_UNI_WGS_PER_CU
+#define ICM_UNI_WGS_PER_CU 1
+#endif
+constexpr int ICM_THREADS_UNI = ICM_UNI_THREADS;
+constexpr int ICM_THREADS_LANE = 512;
+
+template <int NR, bool AUTH, bool PROTECT, bool UNIFORM>
+__global__ __launch_bounds__(UNIFORM ? ICM_THREADS_UNI : ICM_THREADS_LANE)
+void k_icm_hmac(IcmArgs A)
+{
+    constexpr bool TAB4 = UNIFORM && ICM_UNI_TAB4;
+    constexpr int NRK = NR ? NR : 1;
+    constexpr int LDSB = NR ? (TAB4 ? AES_TAB4_BYTES : AES_TAB2_BYTES) : 16;
+    __shared__ u32x4 s_tab[LDSB / 16];
+    if (A.abort && *A.abort)
+        return;
+    if (NR)
+        load_aes_tables<TAB4>(s_tab);
+    __syncthreads();
+    const AesLds T = make_aes_lds(s_tab);
+
+    typename std::conditional<UNIFORM, UniKey<NRK>, LaneKey<NRK>>::type rk;
+    if (UNIFORM && NR)
+        rk.load(A.keys + A.uni);
+    // lane L of a wave takes packet 16 * (L & 3) + (L >> 2) of the wave's 64
+    // (the cooperative path exchanges data inside lane quads)
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t L = threadIdx.x & 63;
+    const uint32_t first = blockIdx.x * blockDim.x + (threadIdx.x & ~63u) +
+                           16 * (L & 3) + (L >> 2);
+    for (uint32_t i = first; i < A.n; i += stride)
+        icm_packet<NR, TAB4, AUTH, PROTECT, UNIFORM>(A, i, T, rk);
 }
 
 // ---------------------------------------------------------------------------
@@ -703,14 +1162,14 @@ DEV u32x4 load_partial(const uint8_t *p, int nbytes)
 template <int NR, bool PROTECT, bool UNIFORM>
 __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
 {
-    __shared__ uint2 s_tab[(AES_LDS_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 8];
+    __shared__ u32x4 s_tab[(AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 16];
     if (A.abort && *A.abort)
         return;
-    load_aes_table(s_tab);
+    load_aes_tables<false>(s_tab);
     if (UNIFORM) {
         const u32x4 *src =
             (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
-        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_LDS_BYTES);
+        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB2_BYTES);
         for (int e = threadIdx.x; e < 256 * 16; e += blockDim.x)
             dst[e] = src[e >> 4];
     }
@@ -731,7 +1190,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
     rk.load(key);
 
     GhTab<UNIFORM> G;
-    G.lds = lds + AES_LDS_BYTES - 0x10000;   // the 0x10000 comes from lane16
+    G.lds = lds + AES_TAB2_BYTES - 0x10000;   // the 0x10000 comes from lane16
     G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
     G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
 
@@ -781,7 +1240,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
         else
             v = load_partial(pin + 16 * j, rem);
         uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = bswap(j + 2);
-        aes_block<NR>(k0, k1, k2, k3, rk, T);
+        aes_block<NR, false>(k0, k1, k2, k3, rk, T);
         u32x4 o = { v.x ^ k0, v.y ^ k1, v.z ^ k2, v.w ^ k3 };
         u32x4 ctv = PROTECT ? o : v;
         if (rem < 16) {   // zero-pad the last ciphertext block for GHASH
@@ -812,7 +1271,7 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
     ghash_mul(x, G);
     // tag = E(J0) ^ S
     uint32_t e0 = c0, e1 = c1, e2 = c2, e3 = bswap(1u);
-    aes_block<NR>(e0, e1, e2, e3, rk, T);
+    aes_block<NR, false>(e0, e1, e2, e3, rk, T);
     uint32_t tagw[4] = { bswap(x[0]) ^ e0, bswap(x[1]) ^ e1, bswap(x[2]) ^ e2,
                          bswap(x[3]) ^ e3 };   // little-endian words of tag
     if (PROTECT) {
@@ -869,7 +1328,7 @@ DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
             x3 = bswap(j + 2);
         else
             x3 = c3base ^ ((j >> 8) << 16) ^ ((j & 0xffu) << 24);
-        aes_block<NR>(x0, x1, x2, x3, rk, T);
+        aes_block<NR, false>(x0, x1, x2, x3, rk, T);
         uint32_t ks[4] = { x0, x1, x2, x3 };
         for (uint32_t b = 0; b < 16 && 16 * j + b < P; b++)
             p[enc_start + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
@@ -882,8 +1341,8 @@ __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
                                               const srtp_dev_key_t *keys,
                                               uint32_t n)
 {
-    __shared__ uint2 s_tab[256 * 32];
-    load_aes_table(s_tab);
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    load_aes_tables<false>(s_tab);
     __syncthreads();
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
@@ -933,7 +1392,7 @@ uint8_t gmul(uint8_t a, uint8_t b)
     return r;
 }
 
-void build_ttab_host(uint2 *t)
+void build_ttab_host(uint32_t *t)
 {
     // S-box from GF(2^8) inverse + affine map (FIPS-197 5.1.1)
     for (int x = 0; x < 256; x++) {
@@ -954,8 +1413,7 @@ void build_ttab_host(uint2 *t)
         uint32_t s = sbox_host[x];
         uint32_t t0 = gmul((uint8_t)s, 2) | (s << 8) | (s << 16) |
                       ((uint32_t)gmul((uint8_t)s, 3) << 24);
-        uint32_t t1 = (t0 << 8) | (t0 >> 24);
-        t[x] = make_uint2(t0, t1);
+        t[x] = t0;
     }
 }
 
@@ -989,6 +1447,7 @@ struct srtp_gpu {
     int timing;
     float last_ms;
     void *pp;   // device pre-pass state (srtp_prepass.hip)
+    int ncu;    // compute units (persistent grids)
 };
 
 // variant mask bits: which kernel instantiations the batch needs
@@ -1010,13 +1469,21 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
-    dim3 grid((unsigned)((b->n + 511) / 512)), block(512);
-    if (b->uniform_key != 0xffffffffu)
-        hipLaunchKernelGGL((k_icm_hmac<NR, AUTH, PROT, true>), grid, block, 0,
-                           st, A);
-    else
-        hipLaunchKernelGGL((k_icm_hmac<NR, AUTH, PROT, false>), grid, block, 0,
-                           st, A);
+    // persistent grid: one 1024-lane workgroup per CU (128 KiB of tables)
+    // for uniform keys, two 512-lane workgroups per CU otherwise
+    if (b->uniform_key != 0xffffffffu) {
+        const size_t wgs = (b->n + ICM_THREADS_UNI - 1) / ICM_THREADS_UNI;
+        const size_t cap = (size_t)g->ncu * ICM_UNI_WGS_PER_CU;
+        hipLaunchKernelGGL((k_icm_hmac<NR, AUTH, PROT, true>),
+                           dim3((unsigned)(wgs < cap ? wgs : cap)),
+                           dim3(ICM_THREADS_UNI), 0, st, A);
+    } else {
+        const size_t wgs = (b->n + ICM_THREADS_LANE - 1) / ICM_THREADS_LANE;
+        const size_t cap = 2 * (size_t)g->ncu;
+        hipLaunchKernelGGL((k_icm_hmac<NR, AUTH, PROT, false>),
+                           dim3((unsigned)(wgs < cap ? wgs : cap)),
+                           dim3(ICM_THREADS_LANE), 0, st, A);
+    }
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -1095,12 +1562,16 @@ int srtp_gpu_open(srtp_gpu_t **gp)
     int dev = -1;
     HIPCHK(hipGetDevice(&dev));
     if (g_table_ready != dev) {
-        uint2 t[256];
+        uint32_t t[256];
         build_ttab_host(t);
-        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_ttab), t, sizeof t));
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_t0), t, sizeof t));
         g_table_ready = dev;
     }
     srtp_gpu_t *g = (srtp_gpu_t *)calloc(1, sizeof(srtp_gpu_t));
+    HIPCHK(hipDeviceGetAttribute(&g->ncu, hipDeviceAttributeMultiprocessorCount,
+                                 dev));
+    if (g->ncu <= 0)
+        g->ncu = 256;
     HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&g->ev0));
     HIPCHK(hipEventCreate(&g->ev1));
