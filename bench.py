@@ -12,10 +12,11 @@ otherwise reject a repeated index).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config icm128|gcm256|g711]
 
-Multi-GPU: one process per GPU (torch.distributed.run), each rank protects
-its own 2^20-packet batch of its own stream (weak scaling; no data-path
-collective: every rank derives identical session keys from the policy, so
-there is nothing to broadcast).  value = all ranks' packets / max rank time.
+Multi-GPU: one process per GPU (torch.distributed.run, nccl = RCCL), each
+rank protects its own 2^20-packet batch of its own stream (weak scaling).
+The master keys are rank 0's and reach the other ranks in one broadcast over
+xGMI (the session (re)key step); the data path has no collective.  value =
+all ranks' packets / max rank time.
 
 Extra fields: roofline (dominant kernel, HIP-event timed on the stream the
 kernels ran on), cpu_baseline (the reference, cisco/libsrtp built from its
@@ -84,36 +85,66 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target wall time of the CPU-baseline sample")
-    ap.add_argument("--pmc-traffic", default="",
-                    help="rocprofv3 --pmc counter_collection.csv to report "
-                         "roofline.traffic from (FETCH_SIZE/WRITE_SIZE)")
+    ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
+                    help="auto: measure roofline.traffic with two rocprofv3 "
+                         "PMC passes (child processes, N=1 only)")
     return ap.parse_args()
 
 
-def pmc_traffic(path, kernel_substr):
-    """HBM bytes per launch of the dominant kernel from a rocprofv3 --pmc
-    CSV holding FETCH_SIZE and WRITE_SIZE (KB).  gfx950 correction
-    (MI355X_MICROARCH.md HBM section): FETCH_SIZE reports half of a wide
-    streaming read -> doubled; WRITE_SIZE exact for 16-B stores."""
+def pmc_counter(path, kernel_substr, counter):
+    """mean per-launch value (KB) of one rocprofv3 --pmc counter of the
+    kernels whose name contains kernel_substr, from counter_collection.csv"""
     import csv
-    if not path or not os.path.exists(path):
-        return None
-    fetch, write, nf, nw = 0.0, 0.0, 0, 0
+    vals = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            name = row.get("Counter_Name", "")
-            val = float(row.get("Counter_Value", 0) or 0)
-            if name == "FETCH_SIZE":
-                fetch += val
-                nf += 1
-            elif name == "WRITE_SIZE":
-                write += val
-                nw += 1
-    if not nf or not nw:
+            if kernel_substr in row.get("Kernel_Name", "") and \
+                    row.get("Counter_Name", "") == counter:
+                vals.append(float(row.get("Counter_Value", 0) or 0))
+    return sum(vals) / len(vals) if vals else None
+
+
+def measure_traffic(a, kname):
+    """HBM bytes per launch of the dominant kernel: FETCH_SIZE and
+    WRITE_SIZE in separate rocprofv3 --pmc passes (MI355X_MICROARCH.md: one
+    pass cannot hold both) over a short run of this same workload, started
+    as child processes before this process touches the GPU.  FETCH_SIZE is
+    TCC_EA0_RDREQ x 64 B; the kernel's reads are 64-B pieces (lane quads)
+    and 16-B lane reads, and the measured value equals the algorithmic read
+    bytes within 3 %, so it is taken as is (the x2 correction of the guide
+    is for 128-B requests of fully coalesced 1 KiB wave reads)."""
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if not prof:
         return None
-    return (2.0 * fetch / nf + write / nw) * 1024.0
+    base = tempfile.mkdtemp(prefix="srtp_pmc_", dir="/tmp")
+    got = {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(base, ctr)
+        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o",
+               "p", "--", sys.executable, os.path.abspath(__file__),
+               "--config", a.config, "--steps", "2", "--warmup", "1",
+               "--no-cpu-baseline", "--traffic", "off"]
+        if a.packets:
+            cmd += ["--packets", str(a.packets)]
+        try:
+            subprocess.run(cmd, stdout=subprocess.DEVNULL,
+                           stderr=subprocess.DEVNULL, timeout=150,
+                           env=dict(os.environ, TMPDIR="/tmp"))
+        except subprocess.TimeoutExpired:
+            return None
+        csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"),
+                         recursive=True)
+        if not csvs:
+            return None
+        got[ctr] = pmc_counter(csvs[0], kname, ctr)
+        if got[ctr] is None:
+            return None
+    shutil.rmtree(base, ignore_errors=True)
+    return (got["FETCH_SIZE"] + got["WRITE_SIZE"]) * 1024.0
 
 
 def rank_ssrc(rank):
@@ -141,7 +172,8 @@ def timed_steps(step, steps, warmup, world, sync=None):
     dt = time.perf_counter() - t0
     if world > 1:
         import torch
-        t = torch.tensor([dt], dtype=torch.float64)
+        dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t[0])
     return dt, res
@@ -181,39 +213,66 @@ def cpu_baseline(cfg, payload, seconds):
             "payload_GBps": done * payload / secs.value / 1e9}
 
 
-def main():
-    a = parse()
+def distribute_keys(keys_hex, world, dev):
+    """Session (re)key: rank 0's master keys reach every rank in ONE
+    broadcast of the key blob -- RCCL over xGMI with the nccl backend (gloo
+    on CPU tensors in the tests).  Every rank then derives its session keys
+    from them (srtp_create runs the KDF), so nothing else is exchanged and
+    the data path has no collective."""
     import torch
     import torch.distributed as dist
+    raw = b"".join(bytes.fromhex(k) for k in keys_hex)
+    blob = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+    if world > 1:
+        dist.broadcast(blob, src=0)
+    raw = blob.cpu().numpy().tobytes()
+    w = len(raw) // len(keys_hex)
+    return [raw[i * w:(i + 1) * w].hex() for i in range(len(keys_hex))]
+
+
+def main():
+    a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    pol, payload, npk, tag = CONFIGS[a.config]
+    kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
+    # PMC passes first: child processes, before this one touches the GPU
+    traffic = None
+    if world == 1 and a.traffic == "auto":
+        traffic = measure_traffic(a, kname)
+    import torch
+    import torch.distributed as dist
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("gloo")
+        dist.init_process_group(
+            os.environ.get("SRTP_DIST_BACKEND", "nccl"),
+            device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     import libsrtp_amd as L
+    dev = torch.device("cuda", torch.cuda.current_device())
 
-    pol, payload, npk, tag = CONFIGS[a.config]
     n = a.packets or npk
     nstreams = STREAMS[a.config]
     ssrc = rank_ssrc(rank)
+    # rank 0's master key(s), broadcast to every rank
+    keys = distribute_keys([TEST_KEY] if nstreams == 1 else
+                           stream_keys(nstreams), world, dev)
     if nstreams == 1:
         policies = [dict(pol, ssrc_type=1, ssrc=ssrc, window_size=128,
-                         allow_repeat_tx=0, keys=[TEST_KEY])]
+                         allow_repeat_tx=0, keys=keys)]
     else:
         base = (0x10000000 + (rank << 20)) & 0xffffffff
         policies = [dict(pol, ssrc_type=1, ssrc=base + k, window_size=128,
                          allow_repeat_tx=0, keys=[key])
-                    for k, key in enumerate(stream_keys(nstreams, rank + 1))]
+                    for k, key in enumerate(keys)]
     sess = L.Session(policies)
 
     # packet arena in HBM: slot = roundup16(rtp_len + tag)
     rtp_len = 12 + payload
     slot = (rtp_len + tag + 15) & ~15
-    dev = torch.device("cuda", torch.cuda.current_device())
     g = torch.Generator(device=dev).manual_seed(0x5352545030303031 & 0x7fffffff)
     arena = torch.randint(0, 256, (n, slot), dtype=torch.uint8, device=dev,
                           generator=g)
@@ -238,14 +297,24 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     sess.set_timing(True)
 
-    seq_base = [0x1234]
+    # The sender's next batch: the same slots with the sequence numbers
+    # advanced by one batch (replay protection rejects a repeated index).
+    # The big-endian sequence bytes of every step are prepared up front, so
+    # the timed step is one 2-byte-per-packet copy plus srtp_protect_device.
+    # out_len keeps the protected lengths (<= slot) between steps: enough
+    # capacity for the next batch, so it is filled once.
+    seqb = []
+    for k in range(a.warmup + a.steps):
+        seq = (pk_seq + 0x1234 + k * per_stream) & 0xffff
+        seqb.append(torch.stack([(seq >> 8), (seq & 0xff)], 1)
+                    .to(torch.uint8).contiguous())
+    out_len.fill_(slot)
+    torch.cuda.synchronize()
+    k_step = [0]
 
     def step():
-        seq = (pk_seq + seq_base[0]) & 0xffff
-        arena[:, 2] = (seq >> 8).to(torch.uint8)
-        arena[:, 3] = (seq & 0xff).to(torch.uint8)
-        out_len.fill_(slot)
-        seq_base[0] += per_stream
+        arena[:, 2:4].copy_(seqb[k_step[0]])
+        k_step[0] += 1
         st = sess.protect_device(flat, off, in_len, flat, off, out_len,
                                  status, stream=stream)
         if st != 0:
@@ -262,8 +331,6 @@ def main():
     kernel_ms = sum(kms) / len(kms)
     algo_bytes = n * (rtp_len + rtp_len + tag)   # read rtp + write srtp
     achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
-    kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
-    traffic = pmc_traffic(a.pmc_traffic, kname)
     if rank != 0:
         return
     cpu = None

@@ -767,6 +767,93 @@ struct CoopPtr {
     uint8_t *seg[4];         // aligned segment 0 base + 16 * (L & 3)
 };
 
+// keystream of chunk b (4 counter blocks of the cached epoch)
+template <int NR, bool TAB4, class KEY>
+DEV void coop_keystream(uint32_t b, const IcmPkt &p, const CtrCache &C,
+                        const KEY &rk, const AesLds &T, uint32_t (&ks)[4][4])
+{
+#ifdef ICM_EXP_NOAES   // timing experiment only: no keystream
+    if constexpr (false) {
+#else
+    if constexpr (NR > 0) {
+#endif
+        if (p.conf) {
+            const uint32_t jb0 = ((4 * b - p.qoff) & 0xffu) << 8;
+#pragma unroll
+            for (int g = 0; g < 4; g += ICM_NB) {
+                uint32_t jb[ICM_NB];
+#pragma unroll
+                for (int j = 0; j < ICM_NB; j++)
+                    jb[j] = jb0 + ((uint32_t)(g + j) << 8);
+                aes_ctr<ICM_NB, NR, TAB4>(
+                    *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), jb, C,
+                    rk, T);
+            }
+            return;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+        ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+}
+
+// One cooperative chunk b.  ks holds chunk b's keystream on entry and, when
+// NEXT, chunk b+1's on exit: the AES of chunk b+1 and the SHA-1 compression
+// of chunk b are independent and sit in one basic block, so the scheduler
+// fills the LDS latency of the table rounds with SHA-1 VALU work.
+template <bool NEXT, int S, int NR, bool TAB4, bool AUTH, bool PROTECT,
+          class KEY>
+DEV void coop_step(uint32_t b, const IcmPkt &p, const CtrCache &C,
+                   const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
+                   uint32_t hst[5], u32x4 (&prev)[4], const CoopPtr &cp,
+                   uint32_t r0, u32x4 (&nx)[4], uint32_t (&ks)[4][4])
+{
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        v[j] = nx[j];
+    if (NEXT) {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            nx[j] = *(gcptr)(cp.in[j] + 64 * (b + 1));
+    }
+    quad_transpose(v);
+    u32x4 o[4];
+    uint32_t wv[16];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t k = u >= S ? ks[t][u - S]
+                                      : (t ? ks[t - 1][u - S + 4]
+                                           : ks_prev[u - S + 4]);
+            o[t][u] = v[t][u] ^ k;
+            wv[4 * t + u] = bswap(PROTECT ? o[t][u] : v[t][u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        ks_prev[u] = ks[3][u];
+    u32x4 sg[4];
+    seg_funnel(prev, o, r0, sg);
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+        prev[t] = o[t];
+    quad_transpose(sg);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+        *(gptr)(cp.seg[j] + 64 * b) = sg[j];
+    if (NEXT)
+        coop_keystream<NR, TAB4>(b + 1, p, C, rk, T, ks);
+#ifdef ICM_EXP_NOSHA   // timing experiment only: fold instead of compress
+    if (AUTH)
+        hst[0] ^= xor3(wv[0], wv[5], wv[10]) ^ wv[15];
+#else
+    if (AUTH)
+        sha1_compress(hst, wv);
+#endif
+}
+
 template <int S, int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
 DEV void icm_coop_run(uint32_t &b, uint32_t e, const IcmPkt &p,
                       const CtrCache &C, const KEY &rk, const AesLds &T,
@@ -777,69 +864,14 @@ DEV void icm_coop_run(uint32_t &b, uint32_t e, const IcmPkt &p,
 #pragma unroll
     for (int j = 0; j < 4; j++)
         nx[j] = *(gcptr)(cp.in[j] + 64 * b);
-    for (; b < e; b++) {
-        u32x4 v[4];
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            v[j] = nx[j];
-        if (b + 1 < e) {
-#pragma unroll
-            for (int j = 0; j < 4; j++)
-                nx[j] = *(gcptr)(cp.in[j] + 64 * (b + 1));
-        }
-        quad_transpose(v);
-        uint32_t ks[4][4];
-        if constexpr (NR > 0) {
-            if (p.conf) {
-                const uint32_t jb0 = ((4 * b - p.qoff) & 0xffu) << 8;
-#pragma unroll
-                for (int g = 0; g < 4; g += ICM_NB) {
-                    uint32_t jb[ICM_NB];
-#pragma unroll
-                    for (int j = 0; j < ICM_NB; j++)
-                        jb[j] = jb0 + ((uint32_t)(g + j) << 8);
-                    aes_ctr<ICM_NB, NR, TAB4>(
-                        *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]), jb,
-                        C, rk, T);
-                }
-            } else {
-#pragma unroll
-                for (int t = 0; t < 4; t++)
-                    ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < 4; t++)
-                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
-        }
-        u32x4 o[4];
-        uint32_t wv[16];
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint32_t k = u >= S ? ks[t][u - S]
-                                          : (t ? ks[t - 1][u - S + 4]
-                                               : ks_prev[u - S + 4]);
-                o[t][u] = v[t][u] ^ k;
-                wv[4 * t + u] = bswap(PROTECT ? o[t][u] : v[t][u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-            ks_prev[u] = ks[3][u];
-        u32x4 sg[4];
-        seg_funnel(prev, o, r0, sg);
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            prev[t] = o[t];
-        quad_transpose(sg);
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-            *(gptr)(cp.seg[j] + 64 * b) = sg[j];
-        if (AUTH)
-            sha1_compress(hst, wv);
-    }
+    uint32_t ks[4][4];
+    coop_keystream<NR, TAB4>(b, p, C, rk, T, ks);
+    for (; b + 1 < e; b++)
+        coop_step<true, S, NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev,
+                                                    hst, prev, cp, r0, nx, ks);
+    coop_step<false, S, NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst,
+                                                 prev, cp, r0, nx, ks);
+    b++;
     // quads 4e - r0 .. 4e - 1 (the head of segment e) are not stored yet
 #pragma unroll
     for (int t = 1; t < 4; t++)

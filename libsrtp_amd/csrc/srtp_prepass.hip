@@ -142,6 +142,30 @@ __global__ void k_pp_classify(ClassifyArgs A)
     A.skey[i] = key;
 }
 
+// One stream (the common case of a single-session sender): the stable sort
+// by stream id is a stable partition into the chain packets (key 0) and the
+// rest (NOCHAIN), placed by an exclusive scan of the chain flags -- a scan
+// and a scatter instead of a full radix sort.
+struct IsChain {
+    __host__ __device__ __forceinline__ uint32_t operator()(const uint32_t &k) const
+    {
+        return k == 0u ? 1u : 0u;
+    }
+};
+
+__global__ void k_pp_partition1(const uint32_t *skey, const uint32_t *excl,
+                                uint32_t n, uint32_t *skey2, uint32_t *perm2)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t total = excl[n - 1] + (skey[n - 1] == 0u ? 1u : 0u);
+    const uint32_t k = skey[i];
+    const uint32_t pos = k == 0u ? excl[i] : total + (i - excl[i]);
+    skey2[pos] = k;
+    perm2[pos] = i;
+}
+
 // sorted position k: the advance over the previous packet of the stream,
 // or for a stream's first packet the exact estimate from its stored index
 // (srtp_host.c estimate / index_guess = rdbx.c:112-145, 280-299)
@@ -408,7 +432,14 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
         nullptr, b, P->skey2, P->val, P->est, hipcub::Sum(), (int)c,
         hipcub::Equality(), stream));
+    size_t c1 = 0;
+    hipcub::TransformInputIterator<uint32_t, IsChain, const uint32_t *> it(
+        P->skey, IsChain());
+    PPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, c1, it, P->perm, (int)c,
+                                           stream));
     P->cub_bytes = a > b ? a : b;
+    if (c1 > P->cub_bytes)
+        P->cub_bytes = c1;
     PPCHK(hipMalloc(&P->cub, P->cub_bytes));
     P->n_cap = c;
     return 0;
@@ -541,9 +572,20 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     while ((1u << end_bit) <= ns && end_bit < 32)
         end_bit++;
     size_t tb = P->cub_bytes;
-    PPCHK(hipcub::DeviceRadixSort::SortPairs(P->cub, tb, P->skey, P->skey2,
-                                             P->perm, P->perm2, (int)N, 0,
-                                             end_bit, stream));
+    if (ns == 1) {
+        // perm (the sort's identity values) is free: it takes the scan
+        hipcub::TransformInputIterator<uint32_t, IsChain, const uint32_t *> it(
+            P->skey, IsChain());
+        PPCHK(hipcub::DeviceScan::ExclusiveSum(P->cub, tb, it, P->perm, (int)N,
+                                               stream));
+        hipLaunchKernelGGL(k_pp_partition1, gp, blk, 0, stream, P->skey,
+                           P->perm, N, P->skey2, P->perm2);
+        PPCHK(hipGetLastError());
+    } else {
+        PPCHK(hipcub::DeviceRadixSort::SortPairs(P->cub, tb, P->skey, P->skey2,
+                                                 P->perm, P->perm2, (int)N, 0,
+                                                 end_bit, stream));
+    }
     if (pp_step(stream, "sort"))
         return -1;
     hipLaunchKernelGGL(k_pp_delta, gp, blk, 0, stream, P->skey2, P->perm2,

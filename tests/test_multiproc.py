@@ -51,3 +51,32 @@ def test_timed_steps_world2_takes_max_over_ranks():
     assert dt0 == pytest.approx(dt1)      # both report the max ...
     assert dt1 >= 3 * 0.04                # ... which is the slow rank's time
     assert s0 != s1                       # one stream per rank
+
+
+def _key_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # every rank starts from different key material; rank 0's must win
+    mine = bench.stream_keys(3, seed=100 + rank)
+    got = bench.distribute_keys(mine, world, "cpu")
+    q.put((rank, got))
+    dist.destroy_process_group()
+
+
+def test_key_broadcast_world2():
+    """the session (re)key step: rank 0's master keys reach every rank in
+    one broadcast (RCCL in bench.py on GPUs, gloo here)"""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_key_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = bench.stream_keys(3, seed=100)
+    assert out[0] == out[1] == want
+    assert all(len(bytes.fromhex(k)) == 46 for k in want)
