@@ -1191,40 +1191,37 @@ DEV u32x4 load_partial(const uint8_t *p, int nbytes)
     return v;
 }
 
-template <int NR, bool PROTECT, bool UNIFORM>
-__global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
-{
-    __shared__ u32x4 s_tab[(AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 16];
-    if (A.abort && *A.abort)
-        return;
-    load_aes_tables<false>(s_tab);
-    if (UNIFORM) {
-        const u32x4 *src =
-            (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
-        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB2_BYTES);
-        for (int e = threadIdx.x; e < 256 * 16; e += blockDim.x)
-            dst[e] = src[e >> 4];
-    }
-    __syncthreads();
-    const char *lds = (const char *)s_tab;
-    const AesLds T = make_aes_lds(s_tab);
+#ifndef GCM_PF
+#define GCM_PF 2   // 64-byte payload chunks loaded ahead of their use
+#endif
 
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n)
-        return;
+DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
+{
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+        v[t] = *(const u32x4a4 *)(ip + 16 * t);
+}
+
+// One GCM packet (srtp.c:2088-2267 protect / 2276-2491 unprotect through
+// aes_gcm_ossl.c: IV = (00 00 || SSRC || ROC || SEQ) ^ salt, AAD = header,
+// CTR from inc32(J0), tag = E(J0) ^ GHASH).  The payload runs in 64-byte
+// chunks of four CTR blocks whose counters stay in the cached epoch
+// (j + 2 <= 255: the first 4 KiB), data loaded GCM_PF chunks ahead; the
+// rest block by block with full AES.
+template <int NR, bool PROTECT, bool UNIFORM, class KEY>
+DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
+                    GhTab<UNIFORM> G, KEY &rk)
+{
     const srtp_dev_meta_t m = A.meta[i];
     constexpr uint32_t VID = 16u + 2u * ((NR - 8) / 2);
     if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
         return;
     const uint32_t slot = UNIFORM ? A.uni : m.key;
     const srtp_dev_key_t *key = A.keys + slot;
-    typename std::conditional<UNIFORM, UniKey<NR>, LaneKey<NR>>::type rk;
-    rk.load(key);
-
-    GhTab<UNIFORM> G;
-    G.lds = lds + AES_TAB2_BYTES - 0x10000;   // the 0x10000 comes from lane16
-    G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
-    G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
+    if constexpr (!UNIFORM) {
+        rk.load(key);
+        G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
+    }
 
     const uint8_t *in = A.in + A.in_off[i];
     uint8_t *out = A.out + A.out_off[i];
@@ -1264,7 +1261,54 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
     const uint32_t nblk = (P + 15) >> 4;
     const uint8_t *pin = in + enc_start;
     uint8_t *pout = out + enc_start;
-    for (uint32_t j = 0; j < nblk; j++) {
+    uint32_t j = 0;
+    // full chunks in the cached counter epoch: block 4c+3 has j + 2 <= 255
+    uint32_t nfc = P >> 6;
+    nfc = nfc < 63 ? nfc : 63;
+    if (nfc) {
+        const uint32_t cc[4] = { c0, c1, c2, 0u };   // BE32(j+2) < 256
+        const CtrCache C = ctr_cache<NR, false>(cc, rk, T);
+        u32x4 ring[GCM_PF][4];
+#pragma unroll
+        for (int k = 0; k < GCM_PF; k++)
+            if ((uint32_t)k < nfc)
+                load_chunk4(ring[k], pin + 64 * k);
+        for (uint32_t c = 0; c < nfc; c++) {
+            u32x4 cur[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                cur[t] = ring[0][t];
+#pragma unroll
+            for (int k = 0; k + 1 < GCM_PF; k++)
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    ring[k][t] = ring[k + 1][t];
+            if (c + GCM_PF < nfc)
+                load_chunk4(ring[GCM_PF - 1], pin + 64 * (c + GCM_PF));
+            uint32_t ks[4][4];
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                const uint32_t jb[2] = { (4 * c + g + 2) << 8,
+                                         (4 * c + g + 3) << 8 };
+                aes_ctr<2, NR, false>(
+                    *reinterpret_cast<uint32_t(*)[2][4]>(&ks[g]), jb, C, rk, T);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const u32x4 o = { cur[t].x ^ ks[t][0], cur[t].y ^ ks[t][1],
+                                  cur[t].z ^ ks[t][2], cur[t].w ^ ks[t][3] };
+                *(u32x4a4 *)(pout + 64 * c + 16 * t) = o;
+                const u32x4 ctv = PROTECT ? o : cur[t];
+                x[0] ^= bswap(ctv.x);
+                x[1] ^= bswap(ctv.y);
+                x[2] ^= bswap(ctv.z);
+                x[3] ^= bswap(ctv.w);
+                ghash_mul(x, G);
+            }
+        }
+        j = 4 * nfc;
+    }
+    for (; j < nblk; j++) {
         const int rem = (int)P - (int)(16 * j);
         u32x4 v;
         if (rem >= 16)
@@ -1319,6 +1363,44 @@ __global__ __launch_bounds__(512) void k_gcm(GcmArgs A)
             diff |= (uint32_t)(tp[u] ^ (uint8_t)(tagw[u >> 2] >> (8 * (u & 3))));
         A.auth_ok[i] = diff == 0;
     }
+}
+
+// (T0, T1) in LDS plus, for uniform keys, the GHASH table replicated 16x
+// (128 KiB: one 512-lane workgroup per CU); persistent grid.
+#ifndef GCM_THREADS_N
+#define GCM_THREADS_N 512
+#endif
+constexpr int GCM_THREADS = GCM_THREADS_N;
+
+template <int NR, bool PROTECT, bool UNIFORM>
+__global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
+{
+    __shared__ u32x4 s_tab[(AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 16];
+    if (A.abort && *A.abort)
+        return;
+    load_aes_tables<false>(s_tab);
+    if (UNIFORM) {
+        const u32x4 *src =
+            (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
+        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB2_BYTES);
+        for (int e = threadIdx.x; e < 256 * 16; e += blockDim.x)
+            dst[e] = src[e >> 4];
+    }
+    __syncthreads();
+    const char *lds = (const char *)s_tab;
+    const AesLds T = make_aes_lds(s_tab);
+
+    typename std::conditional<UNIFORM, UniKey<NR>, LaneKey<NR>>::type rk;
+    if (UNIFORM)
+        rk.load(A.keys + A.uni);
+    GhTab<UNIFORM> G;
+    G.lds = lds + AES_TAB2_BYTES - 0x10000;   // the 0x10000 comes from lane16
+    G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
+    G.g = nullptr;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+         i += stride)
+        gcm_packet<NR, PROTECT, UNIFORM>(A, i, T, G, rk);
 }
 
 // ---------------------------------------------------------------------------
@@ -1535,8 +1617,13 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
-    dim3 grid((unsigned)((b->n + 511) / 512)), block(512);
-    if (b->uniform_key != 0xffffffffu)
+    // persistent grid: one workgroup per CU (128 KiB of tables) for uniform
+    // keys, two otherwise (64 KiB)
+    const bool uni = b->uniform_key != 0xffffffffu;
+    const size_t wgs = (b->n + GCM_THREADS - 1) / GCM_THREADS;
+    const size_t cap = (size_t)g->ncu * (uni ? 1 : 2);
+    const dim3 grid((unsigned)(wgs < cap ? wgs : cap)), block(GCM_THREADS);
+    if (uni)
         hipLaunchKernelGGL((k_gcm<NR, PROT, true>), grid, block, 0, st, A);
     else
         hipLaunchKernelGGL((k_gcm<NR, PROT, false>), grid, block, 0, st, A);
