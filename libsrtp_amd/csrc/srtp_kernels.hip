@@ -815,7 +815,11 @@ DEV void coop_step(uint32_t b, const IcmPkt &p, const CtrCache &C,
     if (NEXT) {
 #pragma unroll
         for (int j = 0; j < 4; j++)
+#ifdef ICM_EXP_L2   // timing experiment only: re-read 2 chunks (cache hits)
+            nx[j] = *(gcptr)(cp.in[j] + 64 * (1 + ((b + 1) & 1)));
+#else
             nx[j] = *(gcptr)(cp.in[j] + 64 * (b + 1));
+#endif
     }
     quad_transpose(v);
     u32x4 o[4];
@@ -842,7 +846,11 @@ DEV void coop_step(uint32_t b, const IcmPkt &p, const CtrCache &C,
     quad_transpose(sg);
 #pragma unroll
     for (int j = 0; j < 4; j++)
+#ifdef ICM_EXP_L2
+        *(gptr)(cp.seg[j] + 64 * (1 + (b & 1))) = sg[j];
+#else
         *(gptr)(cp.seg[j] + 64 * b) = sg[j];
+#endif
     if (NEXT)
         coop_keystream<NR, TAB4>(b + 1, p, C, rk, T, ks);
 #ifdef ICM_EXP_NOSHA   // timing experiment only: fold instead of compress
