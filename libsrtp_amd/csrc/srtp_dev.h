@@ -109,6 +109,15 @@ int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
                   const uint64_t *off, const srtp_dev_meta_t *meta,
                   void *stream);
 
+/* SRTCP (k_rtcp), packets in place at arena+off.  meta: key = RTCP key
+ * slot, roc = 31-bit SRTCP index, info bit 0 = E bit (confidentiality),
+ * [23:16] status, len = protect: RTCP length / unprotect: authenticated
+ * length (RTCP + trailer).  op 0: write trailer, encrypt, MKI, tag;
+ * op 1: verify the tag (auth_ok[i]), then decrypt a verified packet. */
+int srtp_gpu_rtcp(srtp_gpu_t *g, int op, size_t n, uint8_t *arena,
+                  const uint64_t *off, const srtp_dev_meta_t *meta,
+                  uint8_t *auth_ok, void *stream);
+
 /* device header parse for the device-resident API */
 int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
                    const uint64_t *in_off, const uint32_t *in_len,

@@ -82,6 +82,10 @@ typedef struct {
     uint8_t mki[SRTP_MAX_MKI_LEN];
     uint64_t num_left;      /* key.c: srtp_key_limit_ctx_t                   */
     int limit_state;        /* 0 normal, 1 past soft limit, 2 expired        */
+    /* SRTCP session key (srtp.c:1527-1600, KDF labels 3/4/5): own device
+     * slot, ~0 when the RTCP policy is not on the GPU path (AEAD) */
+    uint32_t rslot;
+    size_t rtag_len;
 } hkey_t;
 
 typedef struct {
@@ -113,6 +117,9 @@ struct srtp_stream_ctx_t_ {
     uint64_t spec_epoch;
     rdbx_t spec;
     uint32_t dev_sid;   /* id in the device stream table (dev_build) */
+    /* SRTCP replay database (crypto/replay/rdb.c): 31-bit index window */
+    uint32_t rtcp_start;
+    uint32_t rtcp_bm[4];
 };
 
 typedef struct {
@@ -656,6 +663,67 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
                                      auth_on);
     hk->slot = alloc_slot(ctx);
     dk.ghash_slot = hk->slot;
+
+    /* SRTCP key: srtp.c:1527-1600 (labels 3 encryption, 5 salt, 4 auth).
+     * AEAD RTCP stays off the GPU path (srtp_protect_rtcp reports
+     * no_such_op for it). */
+    hk->rslot = 0xffffffffu;
+    hk->rtag_len = rtcp->auth_tag_len;
+    int rtcp_gpu = (rtcp->cipher_type == SRTP_NULL_CIPHER ||
+                    rtcp->cipher_type == SRTP_AES_ICM_128 ||
+                    rtcp->cipher_type == SRTP_AES_ICM_192 ||
+                    rtcp->cipher_type == SRTP_AES_ICM_256) &&
+                   cipher_supported(rtcp) &&
+                   (rtcp->auth_type == SRTP_NULL_AUTH ||
+                    rtcp->auth_type == SRTP_HMAC_SHA1) &&
+                   auth_supported(rtcp) && hk->family != SRTP_DEV_GCM;
+    if (rtcp_gpu) {
+        srtp_dev_key_t rk;
+        memset(&rk, 0, sizeof rk);
+        size_t rbase = base_key_length(rtcp->cipher_type, rtcp_keylen);
+        size_t rsalt_len = rtcp->cipher_type == SRTP_NULL_CIPHER
+                               ? 0 : rtcp_keylen - rbase;
+        uint8_t rek[32], rsalt[16], rak[20];
+        memset(rsalt, 0, sizeof rsalt);
+        memcpy(rk.mki, hk->mki, sizeof rk.mki);
+        rk.mki_size = (uint32_t)mki_size;
+        rk.tag_len = (uint32_t)rtcp->auth_tag_len;
+        if (rtcp->cipher_type == SRTP_NULL_CIPHER) {
+            rk.family = SRTP_DEV_NULL;
+        } else {
+            kdf_gen(&kdf, kdf_salt, 0x03, rek, rbase);
+            if (rsalt_len > 0)
+                kdf_gen(&kdf, kdf_salt, 0x05, rsalt, rsalt_len);
+            hc_aes_t ca;
+            hc_aes_init(&ca, rek, rbase);
+            memcpy(rk.rk, ca.rk, sizeof rk.rk);
+            rk.rounds = (uint32_t)ca.rounds;
+            rk.family = SRTP_DEV_ICM;
+            rk.conf = 1;
+        }
+        for (int i = 0; i < 4; i++)
+            rk.salt[i] = (uint32_t)rsalt[4 * i] | (uint32_t)rsalt[4 * i + 1] << 8 |
+                         (uint32_t)rsalt[4 * i + 2] << 16 |
+                         (uint32_t)rsalt[4 * i + 3] << 24;
+        if (rtcp->auth_type == SRTP_HMAC_SHA1) {
+            size_t rakl = rtcp->auth_key_len;
+            kdf_gen(&kdf, kdf_salt, 0x04, rak, rakl);
+            uint8_t pad[64];
+            for (int i = 0; i < 64; i++)
+                pad[i] = (uint8_t)((i < (int)rakl ? rak[i] : 0) ^ 0x36);
+            hc_sha1_midstate(pad, rk.ipad);
+            for (int i = 0; i < 64; i++)
+                pad[i] = (uint8_t)((i < (int)rakl ? rak[i] : 0) ^ 0x5c);
+            hc_sha1_midstate(pad, rk.opad);
+            rk.auth = 1;
+        }
+        hk->rslot = alloc_slot(ctx);
+        rk.ghash_slot = hk->rslot;
+        memset(rek, 0, sizeof rek);
+        memset(rak, 0, sizeof rak);
+        if (srtp_gpu_set_key(ctx->gpu, hk->rslot, &rk, NULL))
+            return srtp_err_status_init_fail;
+    }
     memset(tmp, 0, sizeof tmp);
     memset(ek, 0, sizeof ek);
     memset(ak, 0, sizeof ak);
@@ -669,8 +737,11 @@ static void keyset_release(srtp_t ctx, keyset_t *ks)
 {
     if (!ks || --ks->refs > 0)
         return;
-    for (size_t i = 0; i < ks->n; i++)
+    for (size_t i = 0; i < ks->n; i++) {
         release_slot(ctx, ks->k[i].slot);
+        if (ks->k[i].rslot != 0xffffffffu)
+            release_slot(ctx, ks->k[i].rslot);
+    }
     memset(ks, 0, sizeof *ks);
     free(ks);
 }
@@ -746,6 +817,8 @@ static srtp_err_status_t stream_new(srtp_t ctx, const srtp_policy_t *p,
         return srtp_err_status_alloc_fail;
     }
     ks->refs = 1;
+    for (size_t i = 0; i < SRTP_MAX_NUM_MASTER_KEYS; i++)
+        ks->k[i].rslot = 0xffffffffu;
     s->keys = ks;
     if (p->key) {
         s->use_mki = false;
@@ -2123,31 +2196,242 @@ out:
 }
 
 /* ------------------------------------------------------------------------
- * RTCP (not on the GPU path yet)
+ * SRTCP (RFC 3711 3.4) for AES-ICM / null cipher with HMAC-SHA1 / null auth.
+ * Host: stream lookup, E-bit / 31-bit index trailer, replay database
+ * (crypto/replay/rdb.c).  GPU: keystream, trailer + MKI placement, HMAC and
+ * tag verification (k_rtcp).  AEAD SRTCP (srtp.c:3894-4300) is not on the
+ * GPU path: srtp_err_status_no_such_op.
  * ---------------------------------------------------------------------- */
+#define SRTCP_HDR_LEN 8u          /* octets_in_rtcp_header             */
+#define SRTCP_TRAILER_LEN 4u      /* sizeof(srtcp_trailer_t)           */
+#define SRTCP_RDB_BITS 128u       /* rdb_bits_in_bitmask               */
+
+static uint32_t be32_at(const uint8_t *p)
+{
+    return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 |
+           p[3];
+}
+
+/* v128_left_shift, crypto/math/datatypes.c:231-262: bit (i + shift) -> i */
+static void rdb_shift(uint32_t bm[4], uint32_t shift)
+{
+    uint32_t o[4] = { 0, 0, 0, 0 };
+    if (shift < 128) {
+        uint32_t base = shift >> 5, bit = shift & 31;
+        for (uint32_t i = 0; i + base < 4; i++) {
+            uint32_t lo = bm[i + base];
+            uint32_t hi = i + base + 1 < 4 ? bm[i + base + 1] : 0;
+            o[i] = bit ? (lo >> bit) | (hi << (32 - bit)) : lo;
+        }
+    }
+    memcpy(bm, o, sizeof o);
+}
+
+/* srtp_rdb_check, rdb.c:74-96 */
+static srtp_err_status_t rdb_check(const srtp_stream_ctx_t *s, uint32_t idx)
+{
+    if ((uint64_t)idx >= (uint64_t)s->rtcp_start + SRTCP_RDB_BITS)
+        return srtp_err_status_ok;
+    if (idx < s->rtcp_start)
+        return srtp_err_status_replay_old;
+    uint32_t d = idx - s->rtcp_start;
+    if ((s->rtcp_bm[d >> 5] >> (d & 31)) & 1)
+        return srtp_err_status_replay_fail;
+    return srtp_err_status_ok;
+}
+
+/* srtp_rdb_add_index, rdb.c:103-127 */
+static void rdb_add(srtp_stream_ctx_t *s, uint32_t idx)
+{
+    if (idx < s->rtcp_start)
+        return;
+    uint32_t d = idx - s->rtcp_start;
+    if (d < SRTCP_RDB_BITS) {
+        s->rtcp_bm[d >> 5] |= 1u << (d & 31);
+    } else {
+        d -= SRTCP_RDB_BITS - 1;
+        rdb_shift(s->rtcp_bm, d);
+        s->rtcp_bm[3] |= 1u << 31;
+        s->rtcp_start += d;
+    }
+}
+
+/* one SRTCP packet through k_rtcp on the session stream (staged in place) */
+static srtp_err_status_t rtcp_gpu(srtp_t ctx, int op, const uint8_t *in,
+                                  size_t in_len, const srtp_dev_meta_t *m,
+                                  size_t out_len, uint8_t *out, int *auth_ok)
+{
+    size_t arena = r16(in_len + SRTCP_TRAILER_LEN + SRTP_MAX_TRAILER_LEN);
+    if (stage_reserve(ctx, 1, arena))
+        return srtp_err_status_alloc_fail;
+    stage_t *sg = &ctx->st;
+    memcpy(sg->h_arena, in, in_len);
+    sg->h_off[0] = 0;
+    sg->h_meta[0] = *m;
+    sg->h_auth[0] = 0;
+    void *hs = HS(ctx);
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, arena, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, 8, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_meta, sg->h_meta, sizeof *m, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_auth, sg->h_auth, 1, hs) ||
+        srtp_gpu_rtcp(ctx->gpu, op, 1, sg->d_arena, sg->d_off, sg->d_meta,
+                      sg->d_auth, hs) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, arena, hs) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, 1, hs) ||
+        srtp_gpu_sync(ctx->gpu, hs)) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        return srtp_err_status_cipher_fail;
+    }
+    if (auth_ok)
+        *auth_ok = sg->h_auth[0];
+    if (!auth_ok || *auth_ok)
+        memcpy(out, sg->h_arena, out_len);
+    return srtp_err_status_ok;
+}
+
+/* srtp_protect_rtcp, srtp.c:4304-4544 */
 srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
                                     size_t rtcp_len, uint8_t *srtcp,
                                     size_t *srtcp_len, size_t mki_index)
 {
-    (void)ctx;
-    (void)rtcp;
-    (void)rtcp_len;
-    (void)srtcp;
-    (void)srtcp_len;
-    (void)mki_index;
-    return srtp_err_status_no_such_op;
+    if (!ctx || !rtcp || !srtcp || !srtcp_len)
+        return srtp_err_status_bad_param;
+    if (rtcp_len < SRTCP_HDR_LEN)
+        return srtp_err_status_bad_param;
+    dev_pull(ctx);
+    uint32_t ssrc = be32_at(rtcp + 4);
+    srtp_stream_ctx_t *st = map_get(ctx, ssrc);
+    if (!st) {
+        if (!ctx->templ)
+            return srtp_err_status_no_ctx;
+        st = stream_clone(ctx->templ, ssrc);
+        if (!st)
+            return srtp_err_status_alloc_fail;
+        if (list_insert(ctx, st)) {
+            stream_free(ctx, st);
+            return srtp_err_status_alloc_fail;
+        }
+    }
+    if (st->direction != DIR_SENDER) {
+        if (st->direction == DIR_UNKNOWN)
+            st->direction = DIR_SENDER;
+        else
+            fire(ctx, st, event_ssrc_collision);
+    }
+    hkey_t *k = &st->keys->k[0];
+    if (st->use_mki) {
+        if (mki_index >= st->keys->n)
+            return srtp_err_status_bad_mki;
+        k = &st->keys->k[mki_index];
+    }
+    if (k->family == SRTP_DEV_GCM || k->rslot == 0xffffffffu)
+        return srtp_err_status_no_such_op;
+    size_t tag_len = k->rtag_len;
+    size_t out_len = rtcp_len + SRTCP_TRAILER_LEN + st->mki_size + tag_len;
+    if (*srtcp_len < out_len)
+        return srtp_err_status_buffer_small;
+    /* srtp_rdb_increment, rdb.c:133-140; the index is the new window start */
+    if (st->rtcp_start >= 0x7fffffffu)
+        return srtp_err_status_key_expired;
+    uint32_t idx = ++st->rtcp_start;
+    srtp_dev_meta_t m;
+    m.key = k->rslot;
+    m.roc = idx;
+    m.info = (st->rtcp_services & sec_serv_conf) ? 1u : 0u;
+    m.len = (uint32_t)rtcp_len;
+    srtp_err_status_t rc = rtcp_gpu(ctx, 0, rtcp, rtcp_len, &m, out_len,
+                                    srtcp, NULL);
+    if (rc)
+        return rc;
+    *srtcp_len = out_len;
+    return srtp_err_status_ok;
 }
 
+/* srtp_unprotect_rtcp, srtp.c:4546-4837 */
 srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
                                       size_t srtcp_len, uint8_t *rtcp,
                                       size_t *rtcp_len)
 {
-    (void)ctx;
-    (void)srtcp;
-    (void)srtcp_len;
-    (void)rtcp;
-    (void)rtcp_len;
-    return srtp_err_status_no_such_op;
+    if (!ctx || !srtcp || !rtcp || !rtcp_len)
+        return srtp_err_status_bad_param;
+    if (srtcp_len < SRTCP_HDR_LEN + SRTCP_TRAILER_LEN)
+        return srtp_err_status_bad_param;
+    dev_pull(ctx);
+    uint32_t ssrc = be32_at(srtcp + 4);
+    srtp_stream_ctx_t *st = map_get(ctx, ssrc);
+    if (!st) {
+        if (!ctx->templ)
+            return srtp_err_status_no_ctx;
+        st = ctx->templ; /* provisional */
+    }
+    /* srtp_get_session_keys_for_rtcp_packet, srtp.c:2018-2035 */
+    hkey_t *k = &st->keys->k[0];
+    if (st->use_mki) {
+        size_t tl = k->family == SRTP_DEV_GCM ? 0 : k->rtag_len;
+        if (tl > srtcp_len || st->mki_size > srtcp_len - tl)
+            return srtp_err_status_bad_mki;
+        k = mki_lookup(st, srtcp + srtcp_len - tl - st->mki_size);
+        if (!k)
+            return srtp_err_status_bad_mki;
+    }
+    if (k->family == SRTP_DEV_GCM || k->rslot == 0xffffffffu)
+        return srtp_err_status_no_such_op;
+    size_t tag_len = k->rtag_len;
+    if (srtcp_len < SRTCP_HDR_LEN + SRTCP_TRAILER_LEN + st->mki_size + tag_len)
+        return srtp_err_status_bad_param;
+    int conf = st->rtcp_services == sec_serv_conf ||
+               st->rtcp_services == sec_serv_conf_and_auth;
+    const uint8_t *trailer = srtcp + srtcp_len -
+                             (tag_len + st->mki_size + SRTCP_TRAILER_LEN);
+    if (((trailer[0] & 0x80) != 0) != (conf != 0))
+        return srtp_err_status_cant_check;
+    size_t auth_len = srtcp_len - tag_len - st->mki_size;
+    uint32_t idx = be32_at(trailer) & 0x7fffffffu;
+    srtp_err_status_t rc = rdb_check(st, idx);
+    if (rc)
+        return rc;
+    size_t out_len = auth_len - SRTCP_TRAILER_LEN;
+    srtp_dev_meta_t m;
+    m.key = k->rslot;
+    m.roc = idx;
+    m.info = conf ? 1u : 0u;
+    m.len = (uint32_t)auth_len;
+    /* the kernel verifies first and decrypts only a verified packet; the
+     * plaintext is copied out after the buffer check below */
+    uint8_t *tmp = (uint8_t *)malloc(out_len ? out_len : 1);
+    if (!tmp)
+        return srtp_err_status_alloc_fail;
+    int ok = 0;
+    rc = rtcp_gpu(ctx, 1, srtcp, srtcp_len, &m, out_len, tmp, &ok);
+    if (!rc && !ok)
+        rc = srtp_err_status_auth_fail;
+    if (!rc && *rtcp_len < out_len)
+        rc = srtp_err_status_buffer_small;
+    if (rc) {
+        free(tmp);
+        return rc;
+    }
+    memcpy(rtcp, tmp, out_len);
+    free(tmp);
+    *rtcp_len = out_len;
+    if (st->direction != DIR_RECEIVER) {
+        if (st->direction == DIR_UNKNOWN)
+            st->direction = DIR_RECEIVER;
+        else
+            fire(ctx, st, event_ssrc_collision);
+    }
+    if (st == ctx->templ) {
+        srtp_stream_ctx_t *ns = stream_clone(ctx->templ, ssrc);
+        if (!ns)
+            return srtp_err_status_alloc_fail;
+        if (list_insert(ctx, ns)) {
+            stream_free(ctx, ns);
+            return srtp_err_status_alloc_fail;
+        }
+        st = ns;
+    }
+    rdb_add(st, idx);
+    return srtp_err_status_ok;
 }
 
 /* ------------------------------------------------------------------------
@@ -2354,7 +2638,7 @@ static srtp_err_status_t trailer_of(const srtp_stream_ctx_t *s, int is_rtp,
     } else {
         k = &s->keys->k[0];
     }
-    *len += k->tag_len;
+    *len += is_rtp ? k->tag_len : k->rtag_len; /* rtp_auth / rtcp_auth */
     if (!is_rtp)
         *len += 4; /* srtcp_trailer_t */
     return srtp_err_status_ok;

@@ -1486,6 +1486,140 @@ __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
 }
 
 // ---------------------------------------------------------------------------
+// SRTCP (srtp.c:4304-4544 protect, 4546-4837 unprotect): one lane per packet.
+// RTCP is a low-rate control channel, so this is the plain byte-wise form of
+// the RTP kernel's pieces: AES-ICM keystream over [8, P), the E|index trailer
+// at P, MKI, HMAC-SHA1 over [0, P + 4).
+
+// HMAC-SHA1 over msg[0, L) (hmac.c:157-229; no ROC suffix for SRTCP)
+DEV void hmac_sha1_bytes(const srtp_dev_key_t *key, const uint8_t *msg,
+                         uint32_t L, uint32_t oh[5])
+{
+    uint32_t h[5];
+    for (int k = 0; k < 5; k++)
+        h[k] = key->ipad[k];
+    const uint32_t nb = (L + 1 + 8 + 63) / 64;   // data, 0x80, 64-bit length
+    const uint32_t bits = (64 + L) * 8;          // the ipad block counts
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t w[16];
+        for (int t = 0; t < 16; t++) {
+            uint32_t v = 0;
+            for (int u = 0; u < 4; u++) {
+                const uint32_t o = 64 * b + 4 * t + u;
+                const uint32_t c = o < L ? msg[o] : (o == L ? 0x80u : 0u);
+                v = (v << 8) | c;
+            }
+            w[t] = v;
+        }
+        if (b == nb - 1)
+            w[15] = bits;
+        sha1_compress(h, w);
+    }
+    uint32_t ow[16];
+    for (int k = 0; k < 5; k++)
+        ow[k] = h[k];
+    ow[5] = 0x80000000u;
+    for (int k = 6; k < 15; k++)
+        ow[k] = 0;
+    ow[15] = (64 + 20) * 8;
+    for (int k = 0; k < 5; k++)
+        oh[k] = key->opad[k];
+    sha1_compress(oh, ow);
+}
+
+// AES-ICM over p[8, P): counter = salt ^ (0^4 || SSRC || be48(idx)) with the
+// 16-bit block counter in bytes 14..15 (srtp.c:4470-4478, aes_icm.c:236-414)
+template <int NR>
+DEV void rtcp_icm(const srtp_dev_key_t *key, uint32_t idx, uint8_t *p,
+                  uint32_t P, const AesLds &T)
+{
+    GlobalKey rk{ key };
+    const uint32_t ssrc_le = (uint32_t)p[4] | (uint32_t)p[5] << 8 |
+                             (uint32_t)p[6] << 16 | (uint32_t)p[7] << 24;
+    const uint32_t c0 = key->salt[0];
+    const uint32_t c1 = key->salt[1] ^ ssrc_le;
+    const uint32_t c2 = key->salt[2] ^ bswap(idx >> 16);
+    const uint32_t c3base = key->salt[3] ^ bswap(idx << 16);
+    for (uint32_t j = 0; 8 + 16 * j < P; j++) {
+        uint32_t x0 = c0, x1 = c1, x2 = c2;
+        uint32_t x3 = c3base ^ ((j >> 8) << 16) ^ ((j & 0xffu) << 24);
+        aes_block<NR, false>(x0, x1, x2, x3, rk, T);
+        const uint32_t ks[4] = { x0, x1, x2, x3 };
+        for (uint32_t b = 0; b < 16 && 8 + 16 * j + b < P; b++)
+            p[8 + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+DEV void rtcp_crypt(const srtp_dev_key_t *key, uint32_t idx, uint8_t *p,
+                    uint32_t P, const AesLds &T)
+{
+    if (key->rounds == 10)
+        rtcp_icm<10>(key, idx, p, P, T);
+    else if (key->rounds == 12)
+        rtcp_icm<12>(key, idx, p, P, T);
+    else
+        rtcp_icm<14>(key, idx, p, P, T);
+}
+
+__global__ __launch_bounds__(256) void k_rtcp(uint8_t *arena,
+                                              const uint64_t *off,
+                                              const srtp_dev_meta_t *meta,
+                                              const srtp_dev_key_t *keys,
+                                              uint8_t *auth_ok, uint32_t n,
+                                              int protect)
+{
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    load_aes_tables<false>(s_tab);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const srtp_dev_meta_t m = meta[i];
+    if (SRTP_META_STATUS(m.info))
+        return;
+    const srtp_dev_key_t *key = keys + m.key;
+    const AesLds T = make_aes_lds(s_tab);
+    uint8_t *p = arena + off[i];
+    const uint32_t E = m.info & 1u;
+    const bool enc = E && key->family == SRTP_DEV_ICM;
+    const uint32_t tag_len = key->tag_len, mki_size = key->mki_size;
+    if (protect) {
+        const uint32_t P = m.len;
+        const uint32_t tr = (E << 31) | m.roc;
+        p[P] = (uint8_t)(tr >> 24);
+        p[P + 1] = (uint8_t)(tr >> 16);
+        p[P + 2] = (uint8_t)(tr >> 8);
+        p[P + 3] = (uint8_t)tr;
+        if (enc)
+            rtcp_crypt(key, m.roc, p, P, T);
+        for (uint32_t u = 0; u < mki_size; u++)
+            p[P + 4 + u] = key->mki[u];
+        if (key->auth) {
+            uint32_t oh[5];
+            hmac_sha1_bytes(key, p, P + 4, oh);
+            uint8_t *tp = p + P + 4 + mki_size;
+            for (uint32_t u = 0; u < tag_len; u++)
+                tp[u] = (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3)));
+        }
+    } else {
+        const uint32_t A = m.len;   // authenticated bytes, trailer included
+        uint32_t ok = 1;
+        if (key->auth) {
+            uint32_t oh[5];
+            hmac_sha1_bytes(key, p, A, oh);
+            const uint8_t *tp = p + A + mki_size;
+            uint32_t diff = 0;   // constant time (datatypes.c:407-420)
+            for (uint32_t u = 0; u < tag_len; u++)
+                diff |= tp[u] ^ ((oh[u >> 2] >> (24 - 8 * (u & 3))) & 0xffu);
+            ok = diff == 0;
+        }
+        auth_ok[i] = (uint8_t)ok;
+        if (ok && enc)
+            rtcp_crypt(key, m.roc, p, A - 4, T);
+    }
+}
+
+// ---------------------------------------------------------------------------
 // header parse for the device-resident API (srtp_validate_rtp_header,
 // srtp.c:307-336; header length 96-125)
 __global__ void k_parse(const uint8_t *in, const uint64_t *in_off,
@@ -1782,6 +1916,20 @@ int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
     hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     hipLaunchKernelGGL(k_undo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        st, arena, off, meta, g->d_keys, (uint32_t)n);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int srtp_gpu_rtcp(srtp_gpu_t *g, int op, size_t n, uint8_t *arena,
+                  const uint64_t *off, const srtp_dev_meta_t *meta,
+                  uint8_t *auth_ok, void *stream)
+{
+    if (!n)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    hipLaunchKernelGGL(k_rtcp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, arena, off, meta, g->d_keys, auth_ok, (uint32_t)n,
+                       op == 0 ? 1 : 0);
     HIPCHK(hipGetLastError());
     return 0;
 }

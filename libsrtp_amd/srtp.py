@@ -128,6 +128,8 @@ def lib():
         "srtp_dealloc": ([P], C.c_int),
         "srtp_protect": ([P, C.c_char_p, S, P, SP, S], C.c_int),
         "srtp_unprotect": ([P, C.c_char_p, S, P, SP], C.c_int),
+        "srtp_protect_rtcp": ([P, C.c_char_p, S, P, SP, S], C.c_int),
+        "srtp_unprotect_rtcp": ([P, C.c_char_p, S, P, SP], C.c_int),
         "srtp_protect_batch": ([P, S, P, P, P, P, P, P], C.c_int),
         "srtp_unprotect_batch": ([P, S, P, P, P, P, P], C.c_int),
         "srtp_protect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
@@ -261,6 +263,23 @@ class Session:
         out = C.create_string_buffer(max(cap, len(srtp), 1))
         n = C.c_size_t(cap)
         st = self.L.srtp_unprotect(self.h, srtp, len(srtp), out, C.byref(n))
+        return Status(st), (out.raw[:n.value] if st == 0 else None)
+
+    # -- SRTCP (srtp_protect_rtcp / srtp_unprotect_rtcp) -------------------
+    def protect_rtcp(self, rtcp, cap=None, mki_index=0):
+        cap = len(rtcp) + 148 if cap is None else cap
+        out = C.create_string_buffer(max(cap, len(rtcp), 1))
+        n = C.c_size_t(cap)
+        st = self.L.srtp_protect_rtcp(self.h, rtcp, len(rtcp), out,
+                                      C.byref(n), mki_index)
+        return Status(st), (out.raw[:n.value] if st == 0 else None)
+
+    def unprotect_rtcp(self, srtcp, cap=None):
+        cap = len(srtcp) if cap is None else cap
+        out = C.create_string_buffer(max(cap, len(srtcp), 1))
+        n = C.c_size_t(cap)
+        st = self.L.srtp_unprotect_rtcp(self.h, srtcp, len(srtcp), out,
+                                        C.byref(n))
         return Status(st), (out.raw[:n.value] if st == 0 else None)
 
     # -- batch over host buffers -------------------------------------------
