@@ -249,9 +249,9 @@ void srtp_append_salt_to_key(uint8_t *key,
                              uint8_t *salt,
                              size_t bytes_in_salt);
 
-/* ---- RTCP: include/srtp.h:1162-1216 (srtp/srtp.c:4304-4837).  AES-ICM
- *      128/192/256 or null cipher with HMAC-SHA1 or null auth run on the GPU
- *      (k_rtcp); AEAD SRTCP returns srtp_err_status_no_such_op. ------------ */
+/* ---- RTCP: include/srtp.h:1162-1216 (srtp/srtp.c:3894-4837).  AES-ICM
+ *      128/192/256 or null cipher with HMAC-SHA1 or null auth, and AES-GCM
+ *      128/256 (AEAD SRTCP), crypto on the GPU (k_rtcp). ------------------ */
 srtp_err_status_t srtp_protect_rtcp(srtp_t ctx,
                                     const uint8_t *rtcp,
                                     size_t rtcp_len,

@@ -669,20 +669,21 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
      * no_such_op for it). */
     hk->rslot = 0xffffffffu;
     hk->rtag_len = rtcp->auth_tag_len;
-    int rtcp_gpu = (rtcp->cipher_type == SRTP_NULL_CIPHER ||
-                    rtcp->cipher_type == SRTP_AES_ICM_128 ||
-                    rtcp->cipher_type == SRTP_AES_ICM_192 ||
-                    rtcp->cipher_type == SRTP_AES_ICM_256) &&
+    int rtcp_gcm = rtcp->cipher_type == SRTP_AES_GCM_128 ||
+                   rtcp->cipher_type == SRTP_AES_GCM_256;
+    /* srtp.c:4380-4384 picks the AEAD path from the RTP cipher: the two
+     * must agree here */
+    int rtcp_gpu = rtcp_gcm == (hk->family == SRTP_DEV_GCM) &&
                    cipher_supported(rtcp) &&
                    (rtcp->auth_type == SRTP_NULL_AUTH ||
                     rtcp->auth_type == SRTP_HMAC_SHA1) &&
-                   auth_supported(rtcp) && hk->family != SRTP_DEV_GCM;
+                   auth_supported(rtcp);
     if (rtcp_gpu) {
         srtp_dev_key_t rk;
         memset(&rk, 0, sizeof rk);
         size_t rbase = base_key_length(rtcp->cipher_type, rtcp_keylen);
         size_t rsalt_len = rtcp->cipher_type == SRTP_NULL_CIPHER
-                               ? 0 : rtcp_keylen - rbase;
+                               ? 0 : rtcp_keylen - rbase; /* 14 ICM, 12 GCM */
         uint8_t rek[32], rsalt[16], rak[20];
         memset(rsalt, 0, sizeof rsalt);
         memcpy(rk.mki, hk->mki, sizeof rk.mki);
@@ -698,14 +699,22 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
             hc_aes_init(&ca, rek, rbase);
             memcpy(rk.rk, ca.rk, sizeof rk.rk);
             rk.rounds = (uint32_t)ca.rounds;
-            rk.family = SRTP_DEV_ICM;
+            rk.family = rtcp_gcm ? SRTP_DEV_GCM : SRTP_DEV_ICM;
             rk.conf = 1;
+            if (rtcp_gcm) {
+                uint8_t z[16] = { 0 }, h[16];
+                hc_aes_block(&ca, z, h);
+                for (int i = 0; i < 4; i++)
+                    rk.h[i] = (uint32_t)h[4 * i] << 24 |
+                              (uint32_t)h[4 * i + 1] << 16 |
+                              (uint32_t)h[4 * i + 2] << 8 | h[4 * i + 3];
+            }
         }
         for (int i = 0; i < 4; i++)
             rk.salt[i] = (uint32_t)rsalt[4 * i] | (uint32_t)rsalt[4 * i + 1] << 8 |
                          (uint32_t)rsalt[4 * i + 2] << 16 |
                          (uint32_t)rsalt[4 * i + 3] << 24;
-        if (rtcp->auth_type == SRTP_HMAC_SHA1) {
+        if (rtcp->auth_type == SRTP_HMAC_SHA1 && !rtcp_gcm) {
             size_t rakl = rtcp->auth_key_len;
             kdf_gen(&kdf, kdf_salt, 0x04, rak, rakl);
             uint8_t pad[64];
@@ -2324,8 +2333,10 @@ srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
             return srtp_err_status_bad_mki;
         k = &st->keys->k[mki_index];
     }
-    if (k->family == SRTP_DEV_GCM || k->rslot == 0xffffffffu)
+    if (k->rslot == 0xffffffffu)
         return srtp_err_status_no_such_op;
+    /* same layout arithmetic for srtp_protect_rtcp_aead (srtp.c:3939-4100):
+     * there the tag precedes the trailer */
     size_t tag_len = k->rtag_len;
     size_t out_len = rtcp_len + SRTCP_TRAILER_LEN + st->mki_size + tag_len;
     if (*srtcp_len < out_len)
@@ -2346,6 +2357,12 @@ srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
     *srtcp_len = out_len;
     return srtp_err_status_ok;
 }
+
+static srtp_err_status_t rtcp_finish(srtp_t ctx, srtp_stream_ctx_t *st,
+                                     uint32_t ssrc, uint32_t idx,
+                                     const uint8_t *srtcp, size_t srtcp_len,
+                                     const srtp_dev_meta_t *mp, size_t out_len,
+                                     uint8_t *rtcp, size_t *rtcp_len);
 
 /* srtp_unprotect_rtcp, srtp.c:4546-4837 */
 srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
@@ -2374,11 +2391,32 @@ srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
         if (!k)
             return srtp_err_status_bad_mki;
     }
-    if (k->family == SRTP_DEV_GCM || k->rslot == 0xffffffffu)
+    if (k->rslot == 0xffffffffu)
         return srtp_err_status_no_such_op;
     size_t tag_len = k->rtag_len;
     if (srtcp_len < SRTCP_HDR_LEN + SRTCP_TRAILER_LEN + st->mki_size + tag_len)
         return srtp_err_status_bad_param;
+    srtp_err_status_t rc;
+    size_t out_len;
+    srtp_dev_meta_t m;
+    if (k->family == SRTP_DEV_GCM) {
+        /* srtp_unprotect_rtcp_aead, srtp.c:4102-4300: trailer after the
+         * tag, E bit taken from the packet, buffer checked before the tag */
+        const uint8_t *tp = srtcp + srtcp_len - SRTCP_TRAILER_LEN - st->mki_size;
+        uint32_t gidx = be32_at(tp) & 0x7fffffffu;
+        rc = rdb_check(st, gidx);
+        if (rc)
+            return rc;
+        out_len = srtcp_len - tag_len - SRTCP_TRAILER_LEN - st->mki_size;
+        if (*rtcp_len < out_len)
+            return srtp_err_status_buffer_small;
+        m.key = k->rslot;
+        m.roc = gidx;
+        m.info = (tp[0] & 0x80) ? 1u : 0u;
+        m.len = (uint32_t)out_len;
+        return rtcp_finish(ctx, st, ssrc, gidx, srtcp, srtcp_len, &m, out_len,
+                           rtcp, rtcp_len);
+    }
     int conf = st->rtcp_services == sec_serv_conf ||
                st->rtcp_services == sec_serv_conf_and_auth;
     const uint8_t *trailer = srtcp + srtcp_len -
@@ -2387,15 +2425,29 @@ srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
         return srtp_err_status_cant_check;
     size_t auth_len = srtcp_len - tag_len - st->mki_size;
     uint32_t idx = be32_at(trailer) & 0x7fffffffu;
-    srtp_err_status_t rc = rdb_check(st, idx);
+    rc = rdb_check(st, idx);
     if (rc)
         return rc;
-    size_t out_len = auth_len - SRTCP_TRAILER_LEN;
-    srtp_dev_meta_t m;
+    out_len = auth_len - SRTCP_TRAILER_LEN;
     m.key = k->rslot;
     m.roc = idx;
     m.info = conf ? 1u : 0u;
     m.len = (uint32_t)auth_len;
+    return rtcp_finish(ctx, st, ssrc, idx, srtcp, srtcp_len, &m, out_len,
+                       rtcp, rtcp_len);
+}
+
+/* GPU verify(+decrypt), then the reference's post-auth bookkeeping
+ * (srtp.c:4747-4837): buffer check, direction, template promotion, replay
+ * add */
+static srtp_err_status_t rtcp_finish(srtp_t ctx, srtp_stream_ctx_t *st,
+                                     uint32_t ssrc, uint32_t idx,
+                                     const uint8_t *srtcp, size_t srtcp_len,
+                                     const srtp_dev_meta_t *mp, size_t out_len,
+                                     uint8_t *rtcp, size_t *rtcp_len)
+{
+    srtp_dev_meta_t m = *mp;
+    srtp_err_status_t rc;
     /* the kernel verifies first and decrypts only a verified packet; the
      * plaintext is copied out after the buffer check below */
     uint8_t *tmp = (uint8_t *)malloc(out_len ? out_len : 1);

@@ -1561,6 +1561,149 @@ DEV void rtcp_crypt(const srtp_dev_key_t *key, uint32_t idx, uint8_t *p,
         rtcp_icm<14>(key, idx, p, P, T);
 }
 
+// ---- AEAD SRTCP (srtp.c:3894-4300): AES-GCM with a bit-serial GHASH --------
+// X <- X * H in GF(2^128), GCM bit order (SP 800-38D 6.3); 64-bit BE halves
+DEV void gf128_mul(uint64_t &xh, uint64_t &xl, uint64_t hh, uint64_t hl)
+{
+    uint64_t zh = 0, zl = 0, vh = hh, vl = hl;
+    for (int i = 0; i < 128; i++) {
+        const uint64_t bit = i < 64 ? (xh >> (63 - i)) & 1u : (xl >> (127 - i)) & 1u;
+        const uint64_t m = 0 - bit;
+        zh ^= vh & m;
+        zl ^= vl & m;
+        const uint64_t lsb = vl & 1u;
+        vl = (vl >> 1) | (vh << 63);
+        vh = (vh >> 1) ^ ((0 - lsb) & 0xe100000000000000ull);
+    }
+    xh = zh;
+    xl = zl;
+}
+
+struct Ghash {
+    uint64_t xh, xl, hh, hl;
+    uint8_t buf[16];
+    uint32_t fill;
+    DEV void put(uint8_t b)
+    {
+        buf[fill++] = b;
+        if (fill == 16)
+            flush();
+    }
+    DEV void flush()   // absorb the (zero-padded) pending block
+    {
+        if (!fill)
+            return;
+        for (uint32_t u = fill; u < 16; u++)
+            buf[u] = 0;
+        uint64_t a = 0, b = 0;
+        for (int u = 0; u < 8; u++) {
+            a = (a << 8) | buf[u];
+            b = (b << 8) | buf[8 + u];
+        }
+        xh ^= a;
+        xl ^= b;
+        gf128_mul(xh, xl, hh, hl);
+        fill = 0;
+    }
+};
+
+// the GCM counter block IV12 || be32(ctr) through AES
+template <int NR>
+DEV void gcm_block(const srtp_dev_key_t *key, const uint8_t iv[12],
+                   uint32_t ctr, uint32_t ks[4], const AesLds &T)
+{
+    GlobalKey rk{ key };
+    uint32_t x[4];
+    for (int w = 0; w < 3; w++)
+        x[w] = (uint32_t)iv[4 * w] | (uint32_t)iv[4 * w + 1] << 8 |
+               (uint32_t)iv[4 * w + 2] << 16 | (uint32_t)iv[4 * w + 3] << 24;
+    x[3] = bswap(ctr);
+    aes_block<NR, false>(x[0], x[1], x[2], x[3], rk, T);
+    for (int w = 0; w < 4; w++)
+        ks[w] = x[w];
+}
+
+template <int NR>
+DEV void rtcp_gcm(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
+                  uint8_t *p, uint8_t *auth_ok, uint32_t i, bool protect,
+                  const AesLds &T)
+{
+    const uint32_t P = m.len, TL = key->tag_len, E = m.info & 1u;
+    uint8_t *tr = p + P + TL;
+    if (protect) {
+        const uint32_t v = (E << 31) | m.roc;
+        tr[0] = (uint8_t)(v >> 24);
+        tr[1] = (uint8_t)(v >> 16);
+        tr[2] = (uint8_t)(v >> 8);
+        tr[3] = (uint8_t)v;
+    }
+    // IV = salt ^ (00 00 || SSRC || 00 00 || be32(index))  (srtp.c:3894-3930)
+    const uint8_t *salt = (const uint8_t *)key->salt;
+    uint8_t iv[12];
+    for (int u = 0; u < 12; u++)
+        iv[u] = salt[u];
+    for (int u = 0; u < 4; u++) {
+        iv[2 + u] ^= p[4 + u];
+        iv[8 + u] ^= (uint8_t)(m.roc >> (24 - 8 * u));
+    }
+    Ghash G;
+    G.xh = G.xl = 0;
+    G.hh = (uint64_t)key->h[0] << 32 | key->h[1];
+    G.hl = (uint64_t)key->h[2] << 32 | key->h[3];
+    G.fill = 0;
+    // AAD: header (E set) or the whole RTCP packet, then the trailer
+    const uint32_t A1 = E ? 8u : P;
+    for (uint32_t u = 0; u < A1; u++)
+        G.put(p[u]);
+    for (uint32_t u = 0; u < 4; u++)
+        G.put(tr[u]);
+    G.flush();
+    const uint32_t C = E ? P - 8 : 0;
+    uint32_t ks[4];
+    for (uint32_t j = 0; 16 * j < C; j++) {
+        gcm_block<NR>(key, iv, j + 2, ks, T);
+        for (uint32_t b = 0; b < 16 && 16 * j + b < C; b++) {
+            uint8_t *q = p + 8 + 16 * j + b;
+            const uint8_t k8 = (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+            if (protect) {
+                *q ^= k8;
+                G.put(*q);
+            } else {
+                G.put(*q);   // GHASH runs over the ciphertext
+            }
+        }
+    }
+    G.flush();
+    G.xh ^= (uint64_t)(A1 + 4) * 8;   // len(A) || len(C) in bits
+    G.xl ^= (uint64_t)C * 8;
+    gf128_mul(G.xh, G.xl, G.hh, G.hl);
+    gcm_block<NR>(key, iv, 1, ks, T);   // E_K(J0)
+    uint8_t tag[16];
+    for (int u = 0; u < 16; u++) {
+        const uint64_t half = u < 8 ? G.xh : G.xl;
+        tag[u] = (uint8_t)(half >> (56 - 8 * (u & 7))) ^
+                 (uint8_t)(ks[u >> 2] >> (8 * (u & 3)));
+    }
+    if (protect) {
+        for (uint32_t u = 0; u < TL; u++)
+            p[P + u] = tag[u];
+        for (uint32_t u = 0; u < key->mki_size; u++)
+            tr[4 + u] = key->mki[u];
+        return;
+    }
+    uint32_t diff = 0;
+    for (uint32_t u = 0; u < TL; u++)
+        diff |= p[P + u] ^ tag[u];
+    auth_ok[i] = (uint8_t)(diff == 0);
+    if (diff)
+        return;
+    for (uint32_t j = 0; 16 * j < C; j++) {
+        gcm_block<NR>(key, iv, j + 2, ks, T);
+        for (uint32_t b = 0; b < 16 && 16 * j + b < C; b++)
+            p[8 + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
 __global__ __launch_bounds__(256) void k_rtcp(uint8_t *arena,
                                               const uint64_t *off,
                                               const srtp_dev_meta_t *meta,
@@ -1580,6 +1723,13 @@ __global__ __launch_bounds__(256) void k_rtcp(uint8_t *arena,
     const srtp_dev_key_t *key = keys + m.key;
     const AesLds T = make_aes_lds(s_tab);
     uint8_t *p = arena + off[i];
+    if (key->family == SRTP_DEV_GCM) {
+        if (key->rounds == 10)
+            rtcp_gcm<10>(key, m, p, auth_ok, i, protect != 0, T);
+        else
+            rtcp_gcm<14>(key, m, p, auth_ok, i, protect != 0, T);
+        return;
+    }
     const uint32_t E = m.info & 1u;
     const bool enc = E && key->family == SRTP_DEV_ICM;
     const uint32_t tag_len = key->tag_len, mki_size = key->mki_size;

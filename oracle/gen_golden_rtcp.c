@@ -269,6 +269,28 @@ int main(int argc, char **argv)
     g_out = fopen(argv[1], "w");
     if (!g_out)
         return 1;
+#ifdef REF_OSSL
+    static const desc_t d[] = {
+        { "rtcp_gcm128_16", srtp_crypto_policy_set_aes_gcm_128_16_auth,
+          srtp_crypto_policy_set_aes_gcm_128_16_auth, -1, 1, 0, ssrc_specific,
+          ssrc_specific },
+        { "rtcp_gcm256_16", srtp_crypto_policy_set_aes_gcm_256_16_auth,
+          srtp_crypto_policy_set_aes_gcm_256_16_auth, -1, 1, 0, ssrc_specific,
+          ssrc_specific },
+        { "rtcp_gcm256_auth_only", srtp_crypto_policy_set_aes_gcm_256_16_auth,
+          srtp_crypto_policy_set_aes_gcm_256_16_auth, sec_serv_auth, 1, 0,
+          ssrc_specific, ssrc_specific },
+        { "rtcp_gcm128_mki2", srtp_crypto_policy_set_aes_gcm_128_16_auth,
+          srtp_crypto_policy_set_aes_gcm_128_16_auth, -1, 2, 3, ssrc_specific,
+          ssrc_specific },
+        { "rtcp_gcm256_template", srtp_crypto_policy_set_aes_gcm_256_16_auth,
+          srtp_crypto_policy_set_aes_gcm_256_16_auth, -1, 1, 0,
+          ssrc_any_outbound, ssrc_any_inbound },
+        { "rtcp_icm192_sha1_80", srtp_crypto_policy_set_aes_cm_192_hmac_sha1_80,
+          srtp_crypto_policy_set_aes_cm_192_hmac_sha1_80, -1, 1, 0,
+          ssrc_specific, ssrc_specific },
+    };
+#else
     static const desc_t d[] = {
         { "rtcp_default", srtp_crypto_policy_set_rtp_default,
           srtp_crypto_policy_set_rtcp_default, -1, 1, 0, ssrc_specific,
@@ -298,9 +320,16 @@ int main(int argc, char **argv)
           srtp_crypto_policy_set_aes_cm_256_hmac_sha1_80, -1, 1, 0,
           ssrc_any_outbound, ssrc_any_inbound },
     };
+#endif
+#ifdef REF_OSSL
+    fputs("{\n  \"generator\": \"oracle/gen_golden_rtcp.c against "
+          "oracle/_ref/libsrtp_ref_ossl.so (cisco/libsrtp 3.0.0, OpenSSL)\",\n"
+          "  \"cases\": [\n", g_out);
+#else
     fputs("{\n  \"generator\": \"oracle/gen_golden_rtcp.c against "
           "oracle/_ref/libsrtp_ref_int.so (cisco/libsrtp 3.0.0)\",\n"
           "  \"cases\": [\n", g_out);
+#endif
     for (size_t i = 0; i < sizeof d / sizeof d[0]; i++)
         gen(&d[i], i == 0);
     fputs("\n  ]\n}\n", g_out);

@@ -1,9 +1,11 @@
 """CPU restatement of libsrtp's SRTCP path (AES-ICM / null cipher with
-HMAC-SHA1 / null auth), built on the oracle primitives of pyoracle.
+HMAC-SHA1 / null auth, and AES-GCM), built on the oracle primitives of
+pyoracle.
 
 TEST INFRASTRUCTURE ONLY: imported by tests/ -- never by libsrtp_amd.
-Pinned against tests/golden/ref_rtcp.json (the reference's own outputs,
-oracle/gen_golden_rtcp.c) by tests/test_oracle_golden.py.
+Pinned against tests/golden/ref_rtcp.json and ref_rtcp_gcm.json (the
+reference's own outputs, oracle/gen_golden_rtcp.c) by
+tests/test_oracle_golden.py.
 
 Follows cisco/libsrtp 3.0.0:
   srtp_protect_rtcp      srtp/srtp.c:4304-4544
@@ -12,6 +14,7 @@ Follows cisco/libsrtp 3.0.0:
                          srtp.c:1070-1142
   replay database        crypto/replay/rdb.c:63-140
   MKI lookup             srtp/srtp.c:1961-2035
+  AEAD SRTCP             srtp/srtp.c:3894-4300 (IV 3894-3930)
 """
 from oracle import pyoracle as O
 
@@ -20,6 +23,7 @@ NO_CTX, CANT_CHECK, KEY_EXPIRED, BAD_MKI, BUFFER_SMALL = 13, 14, 15, 25, 28
 NO_SUCH_OP = 12
 
 NULL_CIPHER, ICM_128, ICM_192, ICM_256 = 0, 1, 4, 5
+GCM_128, GCM_256 = 6, 7
 HMAC_SHA1 = 3
 SEC_CONF, SEC_AUTH = 1, 2
 SSRC_SPECIFIC, SSRC_ANY_INBOUND, SSRC_ANY_OUTBOUND = 1, 2, 3
@@ -39,13 +43,31 @@ def _kdf(key, salt14, label, n):
 
 class _Key:
     def __init__(self, pol, master, mki):
-        icm = (ICM_128, ICM_192, ICM_256)
-        if pol["rtcp_cipher_type"] not in (NULL_CIPHER,) + icm:
-            raise NotImplementedError("AEAD SRTCP")
-        kdf_len = max(30, pol["cipher_key_len"], pol["rtcp_cipher_key_len"])
+        self.gcm = pol["rtcp_cipher_type"] in (GCM_128, GCM_256)
+        # srtp_stream_init_keys, srtp.c:1262-1320: the master key is used up
+        # to input_keylen and zero-padded to the KDF key length
+        full = {ICM_128: 30, ICM_192: 38, ICM_256: 46, GCM_128: 28,
+                GCM_256: 44}
+        inp = max(full.get(pol["cipher_type"], 0),
+                  full.get(pol["rtcp_cipher_type"], 0),
+                  30 if HMAC_SHA1 in (pol["auth_type"], pol["rtcp_auth_type"])
+                  else 0)
+        master = master[:inp] + bytes(64)
+        kdf_len = max(30, pol["cipher_key_len"], pol["rtcp_cipher_key_len"],
+                      inp)
+        if kdf_len in (28, 44):
+            kdf_len += 2                 # srtp.c:1309-1312
         kdf_key = master[:kdf_len - 14]
         kdf_salt = master[kdf_len - 14:kdf_len]
         self.null = pol["rtcp_cipher_type"] == NULL_CIPHER
+        if self.gcm:
+            base = pol["rtcp_cipher_key_len"] - 12
+            self.ek = _kdf(kdf_key, kdf_salt, 3, base)
+            self.salt = _kdf(kdf_key, kdf_salt, 5, 12)
+            self.hmac, self.ak = False, b""
+            self.tag_len = pol["rtcp_auth_tag_len"]
+            self.mki = mki
+            return
         if not self.null:
             base = pol["rtcp_cipher_key_len"] - 14
             self.ek = _kdf(kdf_key, kdf_salt, 3, base)
@@ -64,6 +86,10 @@ class _Key:
         rc, out = O.icm_xor(self.ek, self.salt, iv, data)
         assert rc == 0
         return out
+
+    def aead_iv(self, ssrc4, idx):
+        x = bytes(2) + ssrc4 + bytes(2) + idx.to_bytes(4, "big")
+        return bytes(a ^ b for a, b in zip(x, self.salt))
 
     def tag(self, msg):
         if not self.hmac:
@@ -141,6 +167,14 @@ class SrtcpSession:
         st.start += 1
         idx = st.start
         conf = bool(st.services & SEC_CONF)
+        if k.gcm:   # srtp_protect_rtcp_aead, srtp.c:3939-4100
+            tr = (((1 << 31) if conf else 0) | idx).to_bytes(4, "big")
+            iv = k.aead_iv(rtcp[4:8], idx)
+            if conf:
+                ct = O.gcm_seal(k.ek, iv, rtcp[:8] + tr, rtcp[8:], k.tag_len)
+                return OK, rtcp[:8] + ct + tr + k.mki
+            t = O.gcm_seal(k.ek, iv, rtcp + tr, b"", k.tag_len)
+            return OK, rtcp + t + tr + k.mki
         body = k.crypt(rtcp[4:8], idx, rtcp[8:]) if conf else rtcp[8:]
         msg = rtcp[:8] + body + (((1 << 31) if conf else 0) | idx).to_bytes(
             4, "big")
@@ -159,7 +193,7 @@ class SrtcpSession:
             st, provisional = self.templ, True
         k = st.keys[0]
         if st.mki_size:
-            tl = k.tag_len
+            tl = 0 if k.gcm else k.tag_len
             if tl > n or st.mki_size > n - tl:
                 return BAD_MKI, None
             m = srtcp[n - tl - st.mki_size:n - tl]
@@ -169,6 +203,28 @@ class SrtcpSession:
         tl = k.tag_len
         if n < 8 + 4 + st.mki_size + tl:
             return BAD_PARAM, None
+        if k.gcm:   # srtp_unprotect_rtcp_aead, srtp.c:4102-4300
+            tp = n - 4 - st.mki_size
+            idx = int.from_bytes(srtcp[tp:tp + 4], "big") & 0x7fffffff
+            rc = st.check(idx)
+            if rc:
+                return rc, None
+            out_len = n - tl - 4 - st.mki_size
+            if cap < out_len:
+                return BUFFER_SMALL, None
+            iv = k.aead_iv(srtcp[4:8], idx)
+            tr = srtcp[tp:tp + 4]
+            tag = srtcp[out_len:out_len + tl]
+            if srtcp[tp] & 0x80:
+                rc, pt = O.gcm_open(k.ek, iv, srtcp[:8] + tr, srtcp[8:out_len],
+                                    tag)
+                out = srtcp[:8] + pt
+            else:
+                rc, _ = O.gcm_open(k.ek, iv, srtcp[:out_len] + tr, b"", tag)
+                out = srtcp[:out_len]
+            if rc:
+                return rc, None
+            return self._accept(st, provisional, ssrc, idx, out)
         conf = st.services in (SEC_CONF, SEC_CONF | SEC_AUTH)
         tp = n - (tl + st.mki_size + 4)
         if bool(srtcp[tp] & 0x80) != conf:
@@ -185,6 +241,9 @@ class SrtcpSession:
             return BUFFER_SMALL, None
         body = srtcp[8:out_len]
         out = srtcp[:8] + (k.crypt(srtcp[4:8], idx, body) if conf else body)
+        return self._accept(st, provisional, ssrc, idx, out)
+
+    def _accept(self, st, provisional, ssrc, idx, out):
         if st.direction == DIR_UNKNOWN:
             st.direction = DIR_RECEIVER
         if provisional:

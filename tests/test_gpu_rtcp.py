@@ -1,6 +1,6 @@
 """GPU parity for SRTCP (srtp_protect_rtcp / srtp_unprotect_rtcp through the
-C ABI, crypto in k_rtcp): the reference's own outputs
-(tests/golden/ref_rtcp.json, oracle/gen_golden_rtcp.c) and the CPU
+C ABI, crypto in k_rtcp; AES-ICM/null and AES-GCM): the reference's own
+outputs (tests/golden/ref_rtcp*.json, oracle/gen_golden_rtcp.c) and the CPU
 restatement (oracle/srtcp_oracle.py) on seeded random traffic.  Bit-exact.
 """
 import random
@@ -13,7 +13,7 @@ from tests.golden_util import load
 from tests.test_oracle_golden import replay_rtcp
 
 pytestmark = pytest.mark.gpu
-CASES = load("ref_rtcp.json")["cases"]
+CASES = load("ref_rtcp.json")["cases"] + load("ref_rtcp_gcm.json")["cases"]
 
 
 def _gpu():
