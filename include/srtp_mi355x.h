@@ -264,6 +264,25 @@ srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx,
                                       uint8_t *rtcp,
                                       size_t *rtcp_len);
 
+/* Batch extension for SRTCP, same contract as srtp_protect_batch /
+ * srtp_unprotect_batch: per-packet status, results identical to n sequential
+ * srtp_protect_rtcp / srtp_unprotect_rtcp calls, one GPU launch per batch. */
+srtp_err_status_t srtp_protect_rtcp_batch(srtp_t ctx,
+                                          size_t n,
+                                          const uint8_t *const *rtcp,
+                                          const size_t *rtcp_len,
+                                          uint8_t *const *srtcp,
+                                          size_t *srtcp_len,
+                                          const size_t *mki_index,
+                                          srtp_err_status_t *status);
+srtp_err_status_t srtp_unprotect_rtcp_batch(srtp_t ctx,
+                                            size_t n,
+                                            const uint8_t *const *srtcp,
+                                            const size_t *srtcp_len,
+                                            uint8_t *const *rtcp,
+                                            size_t *rtcp_len,
+                                            srtp_err_status_t *status);
+
 /* ---- misc: include/srtp.h:1240-1480 ------------------------------------- */
 void srtp_set_user_data(srtp_t ctx, void *data);
 void *srtp_get_user_data(srtp_t ctx);

@@ -83,7 +83,8 @@ typedef struct {
     uint64_t num_left;      /* key.c: srtp_key_limit_ctx_t                   */
     int limit_state;        /* 0 normal, 1 past soft limit, 2 expired        */
     /* SRTCP session key (srtp.c:1527-1600, KDF labels 3/4/5): own device
-     * slot, ~0 when the RTCP policy is not on the GPU path (AEAD) */
+     * slot, ~0 when the RTCP policy is not supported (srtp_protect_rtcp then
+     * reports no_such_op) */
     uint32_t rslot;
     size_t rtag_len;
 } hkey_t;
@@ -2265,49 +2266,38 @@ static void rdb_add(srtp_stream_ctx_t *s, uint32_t idx)
     }
 }
 
-/* one SRTCP packet through k_rtcp on the session stream (staged in place) */
-static srtp_err_status_t rtcp_gpu(srtp_t ctx, int op, const uint8_t *in,
-                                  size_t in_len, const srtp_dev_meta_t *m,
-                                  size_t out_len, uint8_t *out, int *auth_ok)
+/* k_rtcp over a staged batch: packet i at h_arena + h_off[i] (in place);
+ * meta with a non-zero status byte is skipped by the kernel */
+static srtp_err_status_t rtcp_run(srtp_t ctx, int op, size_t n, size_t arena)
 {
-    size_t arena = r16(in_len + SRTCP_TRAILER_LEN + SRTP_MAX_TRAILER_LEN);
-    if (stage_reserve(ctx, 1, arena))
-        return srtp_err_status_alloc_fail;
     stage_t *sg = &ctx->st;
-    memcpy(sg->h_arena, in, in_len);
-    sg->h_off[0] = 0;
-    sg->h_meta[0] = *m;
-    sg->h_auth[0] = 0;
     void *hs = HS(ctx);
+    memset(sg->h_auth, 0, n);
     if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, arena, hs) ||
-        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, 8, hs) ||
-        srtp_gpu_h2d(ctx->gpu, sg->d_meta, sg->h_meta, sizeof *m, hs) ||
-        srtp_gpu_h2d(ctx->gpu, sg->d_auth, sg->h_auth, 1, hs) ||
-        srtp_gpu_rtcp(ctx->gpu, op, 1, sg->d_arena, sg->d_off, sg->d_meta,
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_meta, sg->h_meta, n * sizeof *sg->h_meta,
+                     hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_auth, sg->h_auth, n, hs) ||
+        srtp_gpu_rtcp(ctx->gpu, op, n, sg->d_arena, sg->d_off, sg->d_meta,
                       sg->d_auth, hs) ||
         srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, arena, hs) ||
-        srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, 1, hs) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, n, hs) ||
         srtp_gpu_sync(ctx->gpu, hs)) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
-        return srtp_err_status_cipher_fail;
+        return srtp_err_status_fail;
     }
-    if (auth_ok)
-        *auth_ok = sg->h_auth[0];
-    if (!auth_ok || *auth_ok)
-        memcpy(out, sg->h_arena, out_len);
     return srtp_err_status_ok;
 }
 
-/* srtp_protect_rtcp, srtp.c:4304-4544 */
-srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
-                                    size_t rtcp_len, uint8_t *srtcp,
-                                    size_t *srtcp_len, size_t mki_index)
+/* protect bookkeeping of one packet, in call order (srtp.c:4304-4420,
+ * 3939-3990): stream / template clone, direction, key, buffer, index */
+static srtp_err_status_t rtcp_pre_protect(srtp_t ctx, const uint8_t *rtcp,
+                                          size_t rtcp_len, size_t cap,
+                                          size_t mki_index,
+                                          srtp_dev_meta_t *m, size_t *out_len)
 {
-    if (!ctx || !rtcp || !srtcp || !srtcp_len)
+    if (!rtcp || rtcp_len < SRTCP_HDR_LEN)
         return srtp_err_status_bad_param;
-    if (rtcp_len < SRTCP_HDR_LEN)
-        return srtp_err_status_bad_param;
-    dev_pull(ctx);
     uint32_t ssrc = be32_at(rtcp + 4);
     srtp_stream_ctx_t *st = map_get(ctx, ssrc);
     if (!st) {
@@ -2335,51 +2325,94 @@ srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
     }
     if (k->rslot == 0xffffffffu)
         return srtp_err_status_no_such_op;
-    /* same layout arithmetic for srtp_protect_rtcp_aead (srtp.c:3939-4100):
-     * there the tag precedes the trailer */
-    size_t tag_len = k->rtag_len;
-    size_t out_len = rtcp_len + SRTCP_TRAILER_LEN + st->mki_size + tag_len;
-    if (*srtcp_len < out_len)
+    /* same length arithmetic for srtp_protect_rtcp_aead (srtp.c:3939-4100),
+     * where the tag precedes the trailer */
+    *out_len = rtcp_len + SRTCP_TRAILER_LEN + st->mki_size + k->rtag_len;
+    if (cap < *out_len)
         return srtp_err_status_buffer_small;
     /* srtp_rdb_increment, rdb.c:133-140; the index is the new window start */
     if (st->rtcp_start >= 0x7fffffffu)
         return srtp_err_status_key_expired;
-    uint32_t idx = ++st->rtcp_start;
-    srtp_dev_meta_t m;
-    m.key = k->rslot;
-    m.roc = idx;
-    m.info = (st->rtcp_services & sec_serv_conf) ? 1u : 0u;
-    m.len = (uint32_t)rtcp_len;
-    srtp_err_status_t rc = rtcp_gpu(ctx, 0, rtcp, rtcp_len, &m, out_len,
-                                    srtcp, NULL);
-    if (rc)
-        return rc;
-    *srtcp_len = out_len;
+    m->key = k->rslot;
+    m->roc = ++st->rtcp_start;
+    m->info = (st->rtcp_services & sec_serv_conf) ? 1u : 0u;
+    m->len = (uint32_t)rtcp_len;
     return srtp_err_status_ok;
 }
 
-static srtp_err_status_t rtcp_finish(srtp_t ctx, srtp_stream_ctx_t *st,
-                                     uint32_t ssrc, uint32_t idx,
-                                     const uint8_t *srtcp, size_t srtcp_len,
-                                     const srtp_dev_meta_t *mp, size_t out_len,
-                                     uint8_t *rtcp, size_t *rtcp_len);
-
-/* srtp_unprotect_rtcp, srtp.c:4546-4837 */
-srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
-                                      size_t srtcp_len, uint8_t *rtcp,
-                                      size_t *rtcp_len)
+/* Batched srtp_protect_rtcp: results identical to n sequential calls */
+srtp_err_status_t srtp_protect_rtcp_batch(srtp_t ctx, size_t n,
+                                          const uint8_t *const *rtcp,
+                                          const size_t *rtcp_len,
+                                          uint8_t *const *srtcp,
+                                          size_t *srtcp_len,
+                                          const size_t *mki_index,
+                                          srtp_err_status_t *status)
 {
-    if (!ctx || !srtcp || !rtcp || !rtcp_len)
-        return srtp_err_status_bad_param;
-    if (srtcp_len < SRTCP_HDR_LEN + SRTCP_TRAILER_LEN)
+    if (!ctx)
         return srtp_err_status_bad_param;
     dev_pull(ctx);
-    uint32_t ssrc = be32_at(srtcp + 4);
-    srtp_stream_ctx_t *st = map_get(ctx, ssrc);
+    if (!n)
+        return srtp_err_status_ok;
+    size_t arena = 0;
+    for (size_t i = 0; i < n; i++)
+        arena += r16(rtcp_len[i] + SRTCP_TRAILER_LEN + SRTP_MAX_TRAILER_LEN);
+    if (stage_reserve(ctx, n, arena))
+        return srtp_err_status_alloc_fail;
+    stage_t *sg = &ctx->st;
+    size_t *olen = (size_t *)calloc(n, sizeof(size_t));
+    if (!olen)
+        return srtp_err_status_alloc_fail;
+    size_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        srtp_dev_meta_t *m = &sg->h_meta[i];
+        memset(m, 0, sizeof *m);
+        sg->h_off[i] = off;
+        status[i] = rtcp_pre_protect(ctx, rtcp[i], rtcp_len[i], srtcp_len[i],
+                                     mki_index ? mki_index[i] : 0, m,
+                                     &olen[i]);
+        if (status[i])
+            m->info = (uint32_t)(status[i] & 0xff) << 16;
+        else
+            memcpy(sg->h_arena + off, rtcp[i], rtcp_len[i]);
+        off += r16(rtcp_len[i] + SRTCP_TRAILER_LEN + SRTP_MAX_TRAILER_LEN);
+    }
+    srtp_err_status_t ret = rtcp_run(ctx, 0, n, off);
+    for (size_t i = 0; i < n; i++) {
+        if (ret) {
+            status[i] = srtp_err_status_cipher_fail;
+            continue;
+        }
+        if (status[i])
+            continue;
+        memcpy(srtcp[i], sg->h_arena + sg->h_off[i], olen[i]);
+        srtcp_len[i] = olen[i];
+    }
+    free(olen);
+    return ret;
+}
+
+/* state-independent unprotect checks (srtp.c:4546-4700, 4102-4170): stream
+ * or template, MKI, lengths, E bit; fills the kernel descriptor.  Replay
+ * state is consulted later, in order (rtcp_post_unprotect). */
+typedef struct {
+    uint32_t ssrc, idx;
+    int gcm;
+    size_t out_len;
+} rtcp_u_t;
+
+static srtp_err_status_t rtcp_pre_unprotect(srtp_t ctx, const uint8_t *srtcp,
+                                            size_t srtcp_len,
+                                            srtp_dev_meta_t *m, rtcp_u_t *u)
+{
+    if (!srtcp || srtcp_len < SRTCP_HDR_LEN + SRTCP_TRAILER_LEN)
+        return srtp_err_status_bad_param;
+    u->ssrc = be32_at(srtcp + 4);
+    srtp_stream_ctx_t *st = map_get(ctx, u->ssrc);
     if (!st) {
         if (!ctx->templ)
             return srtp_err_status_no_ctx;
-        st = ctx->templ; /* provisional */
+        st = ctx->templ; /* provisional; clones share its keys/services */
     }
     /* srtp_get_session_keys_for_rtcp_packet, srtp.c:2018-2035 */
     hkey_t *k = &st->keys->k[0];
@@ -2396,76 +2429,49 @@ srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
     size_t tag_len = k->rtag_len;
     if (srtcp_len < SRTCP_HDR_LEN + SRTCP_TRAILER_LEN + st->mki_size + tag_len)
         return srtp_err_status_bad_param;
-    srtp_err_status_t rc;
-    size_t out_len;
-    srtp_dev_meta_t m;
-    if (k->family == SRTP_DEV_GCM) {
-        /* srtp_unprotect_rtcp_aead, srtp.c:4102-4300: trailer after the
-         * tag, E bit taken from the packet, buffer checked before the tag */
+    m->key = k->rslot;
+    u->gcm = k->family == SRTP_DEV_GCM;
+    if (u->gcm) {
+        /* srtp_unprotect_rtcp_aead: trailer after the tag, E bit from the
+         * packet */
         const uint8_t *tp = srtcp + srtcp_len - SRTCP_TRAILER_LEN - st->mki_size;
-        uint32_t gidx = be32_at(tp) & 0x7fffffffu;
-        rc = rdb_check(st, gidx);
-        if (rc)
-            return rc;
-        out_len = srtcp_len - tag_len - SRTCP_TRAILER_LEN - st->mki_size;
-        if (*rtcp_len < out_len)
-            return srtp_err_status_buffer_small;
-        m.key = k->rslot;
-        m.roc = gidx;
-        m.info = (tp[0] & 0x80) ? 1u : 0u;
-        m.len = (uint32_t)out_len;
-        return rtcp_finish(ctx, st, ssrc, gidx, srtcp, srtcp_len, &m, out_len,
-                           rtcp, rtcp_len);
+        u->idx = be32_at(tp) & 0x7fffffffu;
+        u->out_len = srtcp_len - tag_len - SRTCP_TRAILER_LEN - st->mki_size;
+        m->info = (tp[0] & 0x80) ? 1u : 0u;
+        m->len = (uint32_t)u->out_len;
+    } else {
+        int conf = st->rtcp_services == sec_serv_conf ||
+                   st->rtcp_services == sec_serv_conf_and_auth;
+        const uint8_t *tp = srtcp + srtcp_len -
+                            (tag_len + st->mki_size + SRTCP_TRAILER_LEN);
+        if (((tp[0] & 0x80) != 0) != (conf != 0))
+            return srtp_err_status_cant_check;
+        u->idx = be32_at(tp) & 0x7fffffffu;
+        u->out_len = srtcp_len - tag_len - st->mki_size - SRTCP_TRAILER_LEN;
+        m->info = conf ? 1u : 0u;
+        m->len = (uint32_t)(u->out_len + SRTCP_TRAILER_LEN);
     }
-    int conf = st->rtcp_services == sec_serv_conf ||
-               st->rtcp_services == sec_serv_conf_and_auth;
-    const uint8_t *trailer = srtcp + srtcp_len -
-                             (tag_len + st->mki_size + SRTCP_TRAILER_LEN);
-    if (((trailer[0] & 0x80) != 0) != (conf != 0))
-        return srtp_err_status_cant_check;
-    size_t auth_len = srtcp_len - tag_len - st->mki_size;
-    uint32_t idx = be32_at(trailer) & 0x7fffffffu;
-    rc = rdb_check(st, idx);
-    if (rc)
-        return rc;
-    out_len = auth_len - SRTCP_TRAILER_LEN;
-    m.key = k->rslot;
-    m.roc = idx;
-    m.info = conf ? 1u : 0u;
-    m.len = (uint32_t)auth_len;
-    return rtcp_finish(ctx, st, ssrc, idx, srtcp, srtcp_len, &m, out_len,
-                       rtcp, rtcp_len);
+    m->roc = u->idx;
+    return srtp_err_status_ok;
 }
 
-/* GPU verify(+decrypt), then the reference's post-auth bookkeeping
- * (srtp.c:4747-4837): buffer check, direction, template promotion, replay
- * add */
-static srtp_err_status_t rtcp_finish(srtp_t ctx, srtp_stream_ctx_t *st,
-                                     uint32_t ssrc, uint32_t idx,
-                                     const uint8_t *srtcp, size_t srtcp_len,
-                                     const srtp_dev_meta_t *mp, size_t out_len,
-                                     uint8_t *rtcp, size_t *rtcp_len)
+/* in-order part of unprotect: replay check, tag verdict, buffer, then the
+ * reference's post-auth bookkeeping (srtp.c:4747-4837) */
+static srtp_err_status_t rtcp_post_unprotect(srtp_t ctx, const rtcp_u_t *u,
+                                             int auth_ok, size_t cap)
 {
-    srtp_dev_meta_t m = *mp;
-    srtp_err_status_t rc;
-    /* the kernel verifies first and decrypts only a verified packet; the
-     * plaintext is copied out after the buffer check below */
-    uint8_t *tmp = (uint8_t *)malloc(out_len ? out_len : 1);
-    if (!tmp)
-        return srtp_err_status_alloc_fail;
-    int ok = 0;
-    rc = rtcp_gpu(ctx, 1, srtcp, srtcp_len, &m, out_len, tmp, &ok);
-    if (!rc && !ok)
-        rc = srtp_err_status_auth_fail;
-    if (!rc && *rtcp_len < out_len)
-        rc = srtp_err_status_buffer_small;
-    if (rc) {
-        free(tmp);
+    srtp_stream_ctx_t *st = map_get(ctx, u->ssrc);
+    if (!st)
+        st = ctx->templ;
+    srtp_err_status_t rc = rdb_check(st, u->idx);
+    if (rc)
         return rc;
-    }
-    memcpy(rtcp, tmp, out_len);
-    free(tmp);
-    *rtcp_len = out_len;
+    if (u->gcm && cap < u->out_len)     /* AEAD checks the buffer first */
+        return srtp_err_status_buffer_small;
+    if (!auth_ok)
+        return srtp_err_status_auth_fail;
+    if (cap < u->out_len)
+        return srtp_err_status_buffer_small;
     if (st->direction != DIR_RECEIVER) {
         if (st->direction == DIR_UNKNOWN)
             st->direction = DIR_RECEIVER;
@@ -2473,7 +2479,7 @@ static srtp_err_status_t rtcp_finish(srtp_t ctx, srtp_stream_ctx_t *st,
             fire(ctx, st, event_ssrc_collision);
     }
     if (st == ctx->templ) {
-        srtp_stream_ctx_t *ns = stream_clone(ctx->templ, ssrc);
+        srtp_stream_ctx_t *ns = stream_clone(ctx->templ, u->ssrc);
         if (!ns)
             return srtp_err_status_alloc_fail;
         if (list_insert(ctx, ns)) {
@@ -2482,8 +2488,89 @@ static srtp_err_status_t rtcp_finish(srtp_t ctx, srtp_stream_ctx_t *st,
         }
         st = ns;
     }
-    rdb_add(st, idx);
+    rdb_add(st, u->idx);
     return srtp_err_status_ok;
+}
+
+/* Batched srtp_unprotect_rtcp: the tag checks of the whole batch run in one
+ * launch (they do not depend on replay state); the replay database is then
+ * walked in packet order, so results equal n sequential calls */
+srtp_err_status_t srtp_unprotect_rtcp_batch(srtp_t ctx, size_t n,
+                                            const uint8_t *const *srtcp,
+                                            const size_t *srtcp_len,
+                                            uint8_t *const *rtcp,
+                                            size_t *rtcp_len,
+                                            srtp_err_status_t *status)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    dev_pull(ctx);
+    if (!n)
+        return srtp_err_status_ok;
+    size_t arena = 0;
+    for (size_t i = 0; i < n; i++)
+        arena += r16(srtcp_len[i] + 16);
+    if (stage_reserve(ctx, n, arena))
+        return srtp_err_status_alloc_fail;
+    stage_t *sg = &ctx->st;
+    rtcp_u_t *u = (rtcp_u_t *)calloc(n, sizeof *u);
+    if (!u)
+        return srtp_err_status_alloc_fail;
+    size_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        srtp_dev_meta_t *m = &sg->h_meta[i];
+        memset(m, 0, sizeof *m);
+        sg->h_off[i] = off;
+        status[i] = rtcp_pre_unprotect(ctx, srtcp[i], srtcp_len[i], m, &u[i]);
+        if (status[i])
+            m->info = (uint32_t)(status[i] & 0xff) << 16;
+        else
+            memcpy(sg->h_arena + off, srtcp[i], srtcp_len[i]);
+        off += r16(srtcp_len[i] + 16);
+    }
+    srtp_err_status_t ret = rtcp_run(ctx, 1, n, off);
+    for (size_t i = 0; i < n; i++) {
+        if (ret) {
+            status[i] = srtp_err_status_cipher_fail;
+            continue;
+        }
+        if (status[i])
+            continue;
+        status[i] = rtcp_post_unprotect(ctx, &u[i], sg->h_auth[i],
+                                        rtcp_len[i]);
+        if (status[i])
+            continue;
+        memcpy(rtcp[i], sg->h_arena + sg->h_off[i], u[i].out_len);
+        rtcp_len[i] = u[i].out_len;
+    }
+    free(u);
+    return ret;
+}
+
+/* srtp_protect_rtcp, srtp.c:4304-4544: a batch of one */
+srtp_err_status_t srtp_protect_rtcp(srtp_t ctx, const uint8_t *rtcp,
+                                    size_t rtcp_len, uint8_t *srtcp,
+                                    size_t *srtcp_len, size_t mki_index)
+{
+    if (!ctx || !srtcp || !srtcp_len)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st;
+    srtp_err_status_t rc = srtp_protect_rtcp_batch(
+        ctx, 1, &rtcp, &rtcp_len, &srtcp, srtcp_len, &mki_index, &st);
+    return rc ? rc : st;
+}
+
+/* srtp_unprotect_rtcp, srtp.c:4546-4837: a batch of one */
+srtp_err_status_t srtp_unprotect_rtcp(srtp_t ctx, const uint8_t *srtcp,
+                                      size_t srtcp_len, uint8_t *rtcp,
+                                      size_t *rtcp_len)
+{
+    if (!ctx || !rtcp || !rtcp_len)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st;
+    srtp_err_status_t rc = srtp_unprotect_rtcp_batch(
+        ctx, 1, &srtcp, &srtcp_len, &rtcp, rtcp_len, &st);
+    return rc ? rc : st;
 }
 
 /* ------------------------------------------------------------------------

@@ -132,6 +132,8 @@ def lib():
         "srtp_unprotect_rtcp": ([P, C.c_char_p, S, P, SP], C.c_int),
         "srtp_protect_batch": ([P, S, P, P, P, P, P, P], C.c_int),
         "srtp_unprotect_batch": ([P, S, P, P, P, P, P], C.c_int),
+        "srtp_protect_rtcp_batch": ([P, S, P, P, P, P, P, P], C.c_int),
+        "srtp_unprotect_rtcp_batch": ([P, S, P, P, P, P, P], C.c_int),
         "srtp_protect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
         "srtp_unprotect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
         "srtp_get_protect_trailer_length": ([P, S, SP], C.c_int),
@@ -283,9 +285,10 @@ class Session:
         return Status(st), (out.raw[:n.value] if st == 0 else None)
 
     # -- batch over host buffers -------------------------------------------
-    def protect_batch(self, pkts, caps=None, mki=None):
+    def protect_batch(self, pkts, caps=None, mki=None,
+                      fn="srtp_protect_batch"):
         n = len(pkts)
-        caps = [len(p) + 144 for p in pkts] if caps is None else caps
+        caps = [len(p) + 148 for p in pkts] if caps is None else caps
         ins = [C.create_string_buffer(p, max(1, len(p))) for p in pkts]
         outs = [C.create_string_buffer(max(1, c, len(p)))
                 for c, p in zip(caps, pkts)]
@@ -295,15 +298,14 @@ class Session:
         olen = (C.c_size_t * n)(*caps)
         mk = (C.c_size_t * n)(*(mki or [0] * n))
         st = (C.c_int * n)()
-        rc = self.L.srtp_protect_batch(self.h, n, inp, ilen, outp, olen, mk,
-                                       st)
+        rc = getattr(self.L, fn)(self.h, n, inp, ilen, outp, olen, mk, st)
         if rc:
-            raise RuntimeError("srtp_protect_batch: %s" % Status(rc).name)
+            raise RuntimeError("%s: %s" % (fn, Status(rc).name))
         return ([Status(s) for s in st],
                 [outs[i].raw[:olen[i]] if st[i] == 0 else None
                  for i in range(n)])
 
-    def unprotect_batch(self, pkts, caps=None):
+    def unprotect_batch(self, pkts, caps=None, fn="srtp_unprotect_batch"):
         n = len(pkts)
         caps = [len(p) for p in pkts] if caps is None else caps
         ins = [C.create_string_buffer(p, max(1, len(p))) for p in pkts]
@@ -314,12 +316,18 @@ class Session:
         ilen = (C.c_size_t * n)(*[len(p) for p in pkts])
         olen = (C.c_size_t * n)(*caps)
         st = (C.c_int * n)()
-        rc = self.L.srtp_unprotect_batch(self.h, n, inp, ilen, outp, olen, st)
+        rc = getattr(self.L, fn)(self.h, n, inp, ilen, outp, olen, st)
         if rc:
-            raise RuntimeError("srtp_unprotect_batch: %s" % Status(rc).name)
+            raise RuntimeError("%s: %s" % (fn, Status(rc).name))
         return ([Status(s) for s in st],
                 [outs[i].raw[:olen[i]] if st[i] == 0 else None
                  for i in range(n)])
+
+    def protect_rtcp_batch(self, pkts, caps=None, mki=None):
+        return self.protect_batch(pkts, caps, mki, "srtp_protect_rtcp_batch")
+
+    def unprotect_rtcp_batch(self, pkts, caps=None):
+        return self.unprotect_batch(pkts, caps, "srtp_unprotect_rtcp_batch")
 
     # -- batch over device (HBM) arenas: torch tensors on cuda --------------
     def _device(self, fn, arena_in, in_off, in_len, arena_out, out_off,
