@@ -137,6 +137,7 @@ def lib():
         "srtp_protect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
         "srtp_unprotect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
         "srtp_get_protect_trailer_length": ([P, S, SP], C.c_int),
+        "srtp_get_protect_rtcp_trailer_length": ([P, S, SP], C.c_int),
         "srtp_stream_get_roc": ([P, C.c_uint32, C.POINTER(C.c_uint32)],
                                 C.c_int),
         "srtp_stream_set_roc": ([P, C.c_uint32, C.c_uint32], C.c_int),
@@ -367,6 +368,12 @@ class Session:
         n = C.c_size_t()
         st = self.L.srtp_get_protect_trailer_length(self.h, mki_index,
                                                     C.byref(n))
+        return Status(st), n.value
+
+    def rtcp_trailer_length(self, mki_index=0):
+        n = C.c_size_t()
+        st = self.L.srtp_get_protect_rtcp_trailer_length(self.h, mki_index,
+                                                         C.byref(n))
         return Status(st), n.value
 
     def set_timing(self, on=True):

@@ -124,3 +124,17 @@ def test_srtcp_batch_vs_oracle_large():
     st, back = g_rcv.unprotect_rtcp_batch(rx)
     for k, p in enumerate(rx):
         assert (st[k], back[k]) == o_rcv.unprotect_rtcp(p, len(p)), k
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_rtcp_trailer_length_matches_reference_output(case):
+    """srtp_get_protect_rtcp_trailer_length (srtp.c:4972-5000 with the
+    rtcp_auth tag) equals the growth the reference's own srtp_protect_rtcp
+    produced for the same session and MKI index."""
+    _gpu()
+    s = L.Session([case["snd"]])
+    for op in case["ops"]:
+        if op["op"] == "protect_rtcp" and op["status"] == 0:
+            st, n = s.rtcp_trailer_length(op["mki_index"])
+            assert st == 0
+            assert n == (len(op["out"]) - len(op["in"])) // 2, op["mki_index"]
