@@ -31,3 +31,19 @@ def test_udp_relay_roundtrip(packets, payload, batch, chunk):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(res)
     assert res["verified"] == packets and res["failed"] == 0
+
+
+def test_rtcp_bench_roundtrip():
+    """tools/rtcp_bench.c: 65536 SRTCP packets per batch through the C batch
+    API, ICM-128 + HMAC-80 and GCM-256; the tool exits non-zero unless every
+    packet unprotects back to its original bytes."""
+    if not L.lib().srtp_mi355x_gpu_available():
+        pytest.skip("no GPU")
+    exe = os.path.join(ROOT, "tools", "rtcp_bench")
+    assert os.path.exists(exe), "tools/rtcp_bench not built (build())"
+    r = subprocess.run([exe, "65536", "100", "1"], capture_output=True,
+                       text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    lines = [json.loads(x) for x in r.stdout.strip().splitlines()]
+    assert [x["policy"] for x in lines] == ["icm128_sha1_80", "gcm256_16"]
+    assert all(x["verified"] for x in lines)
