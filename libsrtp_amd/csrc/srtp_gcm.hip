@@ -1,0 +1,252 @@
+// srtp_gcm.hip -- k_gcm: AES-GCM seal / open for SRTP AEAD protect and
+// unprotect (srtp/srtp.c:2088-2267, 2276-2491) with the semantics of
+// libsrtp's OpenSSL EVP backend (crypto/cipher/aes_gcm_ossl.c:214-389):
+// IV = (00 00 || SSRC || ROC || SEQ) ^ salt12, AAD = the RTP header, CTR from
+// inc32(J0), tag = E(J0) ^ GHASH, 8 or 16 bytes.  One lane per packet.
+//
+// Compiled once per AES round count: -DGCM_NR=10 or 14.
+#include "srtp_dev_common.h"
+#include "srtp_gpu_int.h"
+
+#ifndef GCM_NR
+#error "GCM_NR (10 or 14) must be defined"
+#endif
+
+namespace {
+
+#ifndef GCM_PF
+#define GCM_PF 2   // 64-byte payload chunks loaded ahead of their use
+#endif
+
+DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
+{
+#pragma unroll
+    for (int t = 0; t < 4; t++)
+        v[t] = *(const u32x4a4 *)(ip + 16 * t);
+}
+
+// One GCM packet (srtp.c:2088-2267 protect / 2276-2491 unprotect through
+// aes_gcm_ossl.c: IV = (00 00 || SSRC || ROC || SEQ) ^ salt, AAD = header,
+// CTR from inc32(J0), tag = E(J0) ^ GHASH).  The payload runs in 64-byte
+// chunks of four CTR blocks whose counters stay in the cached epoch
+// (j + 2 <= 255: the first 4 KiB), data loaded GCM_PF chunks ahead; the
+// rest block by block with full AES.
+template <int NR, bool PROTECT, bool UNIFORM, class KEY>
+DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
+                    GhTab<UNIFORM> G, KEY &rk)
+{
+    const srtp_dev_meta_t m = A.meta[i];
+    constexpr uint32_t VID = 16u + 2u * ((NR - 8) / 2);
+    if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
+        return;
+    const uint32_t slot = UNIFORM ? A.uni : m.key;
+    const srtp_dev_key_t *key = A.keys + slot;
+    if constexpr (!UNIFORM) {
+        rk.load(key);
+        G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
+    }
+
+    const uint8_t *in = A.in + A.in_off[i];
+    uint8_t *out = A.out + A.out_off[i];
+    const uint32_t enc_start = SRTP_META_ENC_START(m.info);
+    const uint32_t tag_len = key->tag_len;
+    const uint32_t mki_size = key->mki_size;
+    const uint32_t P = m.len - enc_start;       // plaintext / ciphertext bytes
+
+    // IV = (00 00 || SSRC || ROC || SEQ) ^ salt12   (srtp.c:1925-1959)
+    const uint32_t w0 = bswap(*(const uint32_t *)in);
+    const uint32_t ssrc = bswap(*(const uint32_t *)(in + 8));
+    const uint32_t seq = w0 & 0xffffu;
+    const uint32_t iv0 = (ssrc >> 16) ^ bswap(key->salt[0]);
+    const uint32_t iv1 = ((ssrc << 16) | (m.roc >> 16)) ^ bswap(key->salt[1]);
+    const uint32_t iv2 = ((m.roc << 16) | seq) ^ bswap(key->salt[2]);
+    const uint32_t c0 = bswap(iv0), c1 = bswap(iv1), c2 = bswap(iv2);
+
+    uint32_t x[4] = { 0, 0, 0, 0 };   // GHASH accumulator (BE words)
+
+    // AAD = the RTP header (enc_start bytes), copied as-is when out != in
+    const bool copy_hdr = in != out;
+    for (uint32_t q = 0; 16 * q < enc_start; q++) {
+        u32x4 v = *(const u32x4 *)(in + 16 * q);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            uint32_t wi = 4 * q + u;
+            uint32_t vu = v[u];
+            if (4 * wi >= enc_start)
+                vu = 0;
+            else if (copy_hdr)
+                *(uint32_t *)(out + 4 * wi) = vu;
+            x[u] ^= bswap(vu);
+        }
+        ghash_mul(x, G);
+    }
+
+    const uint32_t nblk = (P + 15) >> 4;
+    const uint8_t *pin = in + enc_start;
+    uint8_t *pout = out + enc_start;
+    uint32_t j = 0;
+    // full chunks in the cached counter epoch: block 4c+3 has j + 2 <= 255
+    uint32_t nfc = P >> 6;
+    nfc = nfc < 63 ? nfc : 63;
+    if (nfc) {
+        const uint32_t cc[4] = { c0, c1, c2, 0u };   // BE32(j+2) < 256
+        const CtrCache C = ctr_cache<NR, false>(cc, rk, T);
+        u32x4 ring[GCM_PF][4];
+#pragma unroll
+        for (int k = 0; k < GCM_PF; k++)
+            if ((uint32_t)k < nfc)
+                load_chunk4(ring[k], pin + 64 * k);
+        for (uint32_t c = 0; c < nfc; c++) {
+            u32x4 cur[4];
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+                cur[t] = ring[0][t];
+#pragma unroll
+            for (int k = 0; k + 1 < GCM_PF; k++)
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+                    ring[k][t] = ring[k + 1][t];
+            if (c + GCM_PF < nfc)
+                load_chunk4(ring[GCM_PF - 1], pin + 64 * (c + GCM_PF));
+            uint32_t ks[4][4];
+#pragma unroll
+            for (int g = 0; g < 4; g += 2) {
+                const uint32_t jb[2] = { (4 * c + g + 2) << 8,
+                                         (4 * c + g + 3) << 8 };
+                aes_ctr<2, NR, false>(
+                    *reinterpret_cast<uint32_t(*)[2][4]>(&ks[g]), jb, C, rk, T);
+            }
+#pragma unroll
+            for (int t = 0; t < 4; t++) {
+                const u32x4 o = { cur[t].x ^ ks[t][0], cur[t].y ^ ks[t][1],
+                                  cur[t].z ^ ks[t][2], cur[t].w ^ ks[t][3] };
+                *(u32x4a4 *)(pout + 64 * c + 16 * t) = o;
+                const u32x4 ctv = PROTECT ? o : cur[t];
+                x[0] ^= bswap(ctv.x);
+                x[1] ^= bswap(ctv.y);
+                x[2] ^= bswap(ctv.z);
+                x[3] ^= bswap(ctv.w);
+                ghash_mul(x, G);
+            }
+        }
+        j = 4 * nfc;
+    }
+    for (; j < nblk; j++) {
+        const int rem = (int)P - (int)(16 * j);
+        u32x4 v;
+        if (rem >= 16)
+            v = *(const u32x4a4 *)(pin + 16 * j);
+        else
+            v = load_partial(pin + 16 * j, rem);
+        uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = bswap(j + 2);
+        aes_block<NR, false>(k0, k1, k2, k3, rk, T);
+        u32x4 o = { v.x ^ k0, v.y ^ k1, v.z ^ k2, v.w ^ k3 };
+        u32x4 ctv = PROTECT ? o : v;
+        if (rem < 16) {   // zero-pad the last ciphertext block for GHASH
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                int nb = rem - 4 * u;
+                if (nb <= 0)
+                    ctv[u] = 0;
+                else if (nb < 4)
+                    ctv[u] &= 0xffffffffu >> (8 * (4 - nb));
+            }
+        }
+        x[0] ^= bswap(ctv.x);
+        x[1] ^= bswap(ctv.y);
+        x[2] ^= bswap(ctv.z);
+        x[3] ^= bswap(ctv.w);
+        ghash_mul(x, G);
+        if (rem >= 16) {
+            *(u32x4a4 *)(pout + 16 * j) = o;
+        } else {
+            uint32_t oa[4] = { o.x, o.y, o.z, o.w };
+            store_words_partial(pout + 16 * j, oa, rem);
+        }
+    }
+    // length block: [len(A)]64 || [len(C)]64 in bits
+    x[1] ^= enc_start * 8;
+    x[3] ^= P * 8;
+    ghash_mul(x, G);
+    // tag = E(J0) ^ S
+    uint32_t e0 = c0, e1 = c1, e2 = c2, e3 = bswap(1u);
+    aes_block<NR, false>(e0, e1, e2, e3, rk, T);
+    uint32_t tagw[4] = { bswap(x[0]) ^ e0, bswap(x[1]) ^ e1, bswap(x[2]) ^ e2,
+                         bswap(x[3]) ^ e3 };   // little-endian words of tag
+    if (PROTECT) {
+        uint8_t *tp = pout + P;
+        for (uint32_t u = 0; u < tag_len; u++)
+            tp[u] = (uint8_t)(tagw[u >> 2] >> (8 * (u & 3)));
+        for (uint32_t u = 0; u < mki_size; u++)
+            tp[tag_len + u] = key->mki[u];
+    } else {
+        const uint8_t *tp = pin + P;
+        uint32_t diff = 0;
+        for (uint32_t u = 0; u < tag_len; u++)
+            diff |= (uint32_t)(tp[u] ^ (uint8_t)(tagw[u >> 2] >> (8 * (u & 3))));
+        A.auth_ok[i] = diff == 0;
+    }
+}
+
+// (T0, T1) in LDS plus, for uniform keys, the GHASH table replicated 16x
+// (128 KiB: one 512-lane workgroup per CU); persistent grid.
+#ifndef GCM_THREADS_N
+#define GCM_THREADS_N 512
+#endif
+constexpr int GCM_THREADS = GCM_THREADS_N;
+
+template <int NR, bool PROTECT, bool UNIFORM>
+__global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
+{
+    __shared__ u32x4 s_tab[(AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 16];
+    if (A.abort && *A.abort)
+        return;
+    load_aes_tables<false>(s_tab);
+    if (UNIFORM) {
+        const u32x4 *src =
+            (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
+        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB2_BYTES);
+        for (int e = threadIdx.x; e < 256 * 16; e += blockDim.x)
+            dst[e] = src[e >> 4];
+    }
+    __syncthreads();
+    const char *lds = (const char *)s_tab;
+    const AesLds T = make_aes_lds(s_tab);
+
+    typename std::conditional<UNIFORM, UniKey<NR>, LaneKey<NR>>::type rk;
+    if (UNIFORM)
+        rk.load(A.keys + A.uni);
+    GhTab<UNIFORM> G;
+    G.lds = lds + AES_TAB2_BYTES - 0x10000;   // the 0x10000 comes from lane16
+    G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
+    G.g = nullptr;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+         i += stride)
+        gcm_packet<NR, PROTECT, UNIFORM>(A, i, T, G, rk);
+}
+
+}   // namespace
+
+template <int NR>
+int launch_gcm_nr(const GcmArgs &A, bool prot, int ncu, hipStream_t st)
+{
+    // persistent grid: one workgroup per CU (128 KiB of tables) for uniform
+    // keys, two otherwise (64 KiB)
+    const bool uni = A.uni != 0xffffffffu;
+    const size_t wgs = (A.n + GCM_THREADS - 1) / GCM_THREADS;
+    const size_t cap = (size_t)ncu * (uni ? 1 : 2);
+    const dim3 grid((unsigned)(wgs < cap ? wgs : cap)), block(GCM_THREADS);
+    if (uni && prot)
+        hipLaunchKernelGGL((k_gcm<NR, true, true>), grid, block, 0, st, A);
+    else if (uni)
+        hipLaunchKernelGGL((k_gcm<NR, false, true>), grid, block, 0, st, A);
+    else if (prot)
+        hipLaunchKernelGGL((k_gcm<NR, true, false>), grid, block, 0, st, A);
+    else
+        hipLaunchKernelGGL((k_gcm<NR, false, false>), grid, block, 0, st, A);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+template int launch_gcm_nr<GCM_NR>(const GcmArgs &, bool, int, hipStream_t);

@@ -1,0 +1,685 @@
+// srtp_gpu.hip -- the thin extern "C" FFI (srtp_dev.h) between the C host
+// engine and the HIP kernels: device context, key table, kernel dispatch,
+// plus the small kernels (speculative-unprotect undo, SRTCP, header parse).
+// The RTP crypto kernels live in srtp_icm.hip, srtp_icm_wave.hip and
+// srtp_gcm.hip (srtp_gpu_int.h).
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "srtp_dev_common.h"
+#include "srtp_gpu_int.h"
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Restore kernel for speculative unprotect: XORs the keystream the
+// speculative pass used back over [enc_start, len) so the ciphertext of a
+// packet that must be re-run is intact again (CTR decryption is an XOR).
+// Rare path: byte-granular, runtime round count.
+template <int NR>
+DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
+                  uint8_t *p, const AesLds &T)
+{
+    GlobalKey rk{ key };
+    const uint32_t enc_start = SRTP_META_ENC_START(m.info);
+    const uint32_t P = m.len - enc_start;
+    const uint32_t w0 = bswap(*(const uint32_t *)p);
+    const uint32_t seq = w0 & 0xffffu;
+    uint32_t c0, c1, c2, c3base;
+    const bool gcm = key->family == SRTP_DEV_GCM;
+    if (gcm) {
+        const uint32_t ssrc = bswap(*(const uint32_t *)(p + 8));
+        c0 = bswap((ssrc >> 16) ^ bswap(key->salt[0]));
+        c1 = bswap(((ssrc << 16) | (m.roc >> 16)) ^ bswap(key->salt[1]));
+        c2 = bswap(((m.roc << 16) | seq) ^ bswap(key->salt[2]));
+        c3base = 0;
+    } else {
+        c0 = key->salt[0];
+        c1 = key->salt[1] ^ *(const uint32_t *)(p + 8);
+        c2 = key->salt[2] ^ bswap(m.roc);
+        c3base = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
+    }
+    for (uint32_t j = 0; 16 * j < P; j++) {
+        uint32_t x0 = c0, x1 = c1, x2 = c2, x3;
+        if (gcm)
+            x3 = bswap(j + 2);
+        else
+            x3 = c3base ^ ((j >> 8) << 16) ^ ((j & 0xffu) << 24);
+        aes_block<NR, false>(x0, x1, x2, x3, rk, T);
+        uint32_t ks[4] = { x0, x1, x2, x3 };
+        for (uint32_t b = 0; b < 16 && 16 * j + b < P; b++)
+            p[enc_start + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
+                                              const uint64_t *off,
+                                              const srtp_dev_meta_t *meta,
+                                              const srtp_dev_key_t *keys,
+                                              uint32_t n)
+{
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    load_aes_tables<false>(s_tab);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const srtp_dev_meta_t m = meta[i];
+    if (SRTP_META_STATUS(m.info))
+        return;
+    const srtp_dev_key_t *key = keys + m.key;
+    if (!key->conf || key->family == SRTP_DEV_NULL)
+        return;
+    const AesLds T = make_aes_lds(s_tab);
+    uint8_t *p = arena + off[i];
+    if (key->rounds == 10)
+        undo_one<10>(key, m, p, T);
+    else if (key->rounds == 12)
+        undo_one<12>(key, m, p, T);
+    else
+        undo_one<14>(key, m, p, T);
+}
+
+// ---------------------------------------------------------------------------
+// SRTCP (srtp.c:4304-4544 protect, 4546-4837 unprotect): one lane per packet.
+// RTCP is a low-rate control channel, so this is the plain byte-wise form of
+// the RTP kernel's pieces: AES-ICM keystream over [8, P), the E|index trailer
+// at P, MKI, HMAC-SHA1 over [0, P + 4).
+
+// HMAC-SHA1 over msg[0, L) (hmac.c:157-229; no ROC suffix for SRTCP)
+DEV void hmac_sha1_bytes(const srtp_dev_key_t *key, const uint8_t *msg,
+                         uint32_t L, uint32_t oh[5])
+{
+    uint32_t h[5];
+    for (int k = 0; k < 5; k++)
+        h[k] = key->ipad[k];
+    const uint32_t nb = (L + 1 + 8 + 63) / 64;   // data, 0x80, 64-bit length
+    const uint32_t bits = (64 + L) * 8;          // the ipad block counts
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t w[16];
+        for (int t = 0; t < 16; t++) {
+            uint32_t v = 0;
+            for (int u = 0; u < 4; u++) {
+                const uint32_t o = 64 * b + 4 * t + u;
+                const uint32_t c = o < L ? msg[o] : (o == L ? 0x80u : 0u);
+                v = (v << 8) | c;
+            }
+            w[t] = v;
+        }
+        if (b == nb - 1)
+            w[15] = bits;
+        sha1_compress(h, w);
+    }
+    uint32_t ow[16];
+    for (int k = 0; k < 5; k++)
+        ow[k] = h[k];
+    ow[5] = 0x80000000u;
+    for (int k = 6; k < 15; k++)
+        ow[k] = 0;
+    ow[15] = (64 + 20) * 8;
+    for (int k = 0; k < 5; k++)
+        oh[k] = key->opad[k];
+    sha1_compress(oh, ow);
+}
+
+// AES-ICM over p[8, P): counter = salt ^ (0^4 || SSRC || be48(idx)) with the
+// 16-bit block counter in bytes 14..15 (srtp.c:4470-4478, aes_icm.c:236-414)
+template <int NR>
+DEV void rtcp_icm(const srtp_dev_key_t *key, uint32_t idx, uint8_t *p,
+                  uint32_t P, const AesLds &T)
+{
+    GlobalKey rk{ key };
+    const uint32_t ssrc_le = (uint32_t)p[4] | (uint32_t)p[5] << 8 |
+                             (uint32_t)p[6] << 16 | (uint32_t)p[7] << 24;
+    const uint32_t c0 = key->salt[0];
+    const uint32_t c1 = key->salt[1] ^ ssrc_le;
+    const uint32_t c2 = key->salt[2] ^ bswap(idx >> 16);
+    const uint32_t c3base = key->salt[3] ^ bswap(idx << 16);
+    for (uint32_t j = 0; 8 + 16 * j < P; j++) {
+        uint32_t x0 = c0, x1 = c1, x2 = c2;
+        uint32_t x3 = c3base ^ ((j >> 8) << 16) ^ ((j & 0xffu) << 24);
+        aes_block<NR, false>(x0, x1, x2, x3, rk, T);
+        const uint32_t ks[4] = { x0, x1, x2, x3 };
+        for (uint32_t b = 0; b < 16 && 8 + 16 * j + b < P; b++)
+            p[8 + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+DEV void rtcp_crypt(const srtp_dev_key_t *key, uint32_t idx, uint8_t *p,
+                    uint32_t P, const AesLds &T)
+{
+    if (key->rounds == 10)
+        rtcp_icm<10>(key, idx, p, P, T);
+    else if (key->rounds == 12)
+        rtcp_icm<12>(key, idx, p, P, T);
+    else
+        rtcp_icm<14>(key, idx, p, P, T);
+}
+
+// ---- AEAD SRTCP (srtp.c:3894-4300): AES-GCM with a bit-serial GHASH --------
+// X <- X * H in GF(2^128), GCM bit order (SP 800-38D 6.3); 64-bit BE halves
+DEV void gf128_mul(uint64_t &xh, uint64_t &xl, uint64_t hh, uint64_t hl)
+{
+    uint64_t zh = 0, zl = 0, vh = hh, vl = hl;
+    for (int i = 0; i < 128; i++) {
+        const uint64_t bit = i < 64 ? (xh >> (63 - i)) & 1u : (xl >> (127 - i)) & 1u;
+        const uint64_t m = 0 - bit;
+        zh ^= vh & m;
+        zl ^= vl & m;
+        const uint64_t lsb = vl & 1u;
+        vl = (vl >> 1) | (vh << 63);
+        vh = (vh >> 1) ^ ((0 - lsb) & 0xe100000000000000ull);
+    }
+    xh = zh;
+    xl = zl;
+}
+
+struct Ghash {
+    uint64_t xh, xl, hh, hl;
+    uint8_t buf[16];
+    uint32_t fill;
+    DEV void put(uint8_t b)
+    {
+        buf[fill++] = b;
+        if (fill == 16)
+            flush();
+    }
+    DEV void flush()   // absorb the (zero-padded) pending block
+    {
+        if (!fill)
+            return;
+        for (uint32_t u = fill; u < 16; u++)
+            buf[u] = 0;
+        uint64_t a = 0, b = 0;
+        for (int u = 0; u < 8; u++) {
+            a = (a << 8) | buf[u];
+            b = (b << 8) | buf[8 + u];
+        }
+        xh ^= a;
+        xl ^= b;
+        gf128_mul(xh, xl, hh, hl);
+        fill = 0;
+    }
+};
+
+// the GCM counter block IV12 || be32(ctr) through AES
+template <int NR>
+DEV void gcm_block(const srtp_dev_key_t *key, const uint8_t iv[12],
+                   uint32_t ctr, uint32_t ks[4], const AesLds &T)
+{
+    GlobalKey rk{ key };
+    uint32_t x[4];
+    for (int w = 0; w < 3; w++)
+        x[w] = (uint32_t)iv[4 * w] | (uint32_t)iv[4 * w + 1] << 8 |
+               (uint32_t)iv[4 * w + 2] << 16 | (uint32_t)iv[4 * w + 3] << 24;
+    x[3] = bswap(ctr);
+    aes_block<NR, false>(x[0], x[1], x[2], x[3], rk, T);
+    for (int w = 0; w < 4; w++)
+        ks[w] = x[w];
+}
+
+template <int NR>
+DEV void rtcp_gcm(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
+                  uint8_t *p, uint8_t *auth_ok, uint32_t i, bool protect,
+                  const AesLds &T)
+{
+    const uint32_t P = m.len, TL = key->tag_len, E = m.info & 1u;
+    uint8_t *tr = p + P + TL;
+    if (protect) {
+        const uint32_t v = (E << 31) | m.roc;
+        tr[0] = (uint8_t)(v >> 24);
+        tr[1] = (uint8_t)(v >> 16);
+        tr[2] = (uint8_t)(v >> 8);
+        tr[3] = (uint8_t)v;
+    }
+    // IV = salt ^ (00 00 || SSRC || 00 00 || be32(index))  (srtp.c:3894-3930)
+    const uint8_t *salt = (const uint8_t *)key->salt;
+    uint8_t iv[12];
+    for (int u = 0; u < 12; u++)
+        iv[u] = salt[u];
+    for (int u = 0; u < 4; u++) {
+        iv[2 + u] ^= p[4 + u];
+        iv[8 + u] ^= (uint8_t)(m.roc >> (24 - 8 * u));
+    }
+    Ghash G;
+    G.xh = G.xl = 0;
+    G.hh = (uint64_t)key->h[0] << 32 | key->h[1];
+    G.hl = (uint64_t)key->h[2] << 32 | key->h[3];
+    G.fill = 0;
+    // AAD: header (E set) or the whole RTCP packet, then the trailer
+    const uint32_t A1 = E ? 8u : P;
+    for (uint32_t u = 0; u < A1; u++)
+        G.put(p[u]);
+    for (uint32_t u = 0; u < 4; u++)
+        G.put(tr[u]);
+    G.flush();
+    const uint32_t C = E ? P - 8 : 0;
+    uint32_t ks[4];
+    for (uint32_t j = 0; 16 * j < C; j++) {
+        gcm_block<NR>(key, iv, j + 2, ks, T);
+        for (uint32_t b = 0; b < 16 && 16 * j + b < C; b++) {
+            uint8_t *q = p + 8 + 16 * j + b;
+            const uint8_t k8 = (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+            if (protect) {
+                *q ^= k8;
+                G.put(*q);
+            } else {
+                G.put(*q);   // GHASH runs over the ciphertext
+            }
+        }
+    }
+    G.flush();
+    G.xh ^= (uint64_t)(A1 + 4) * 8;   // len(A) || len(C) in bits
+    G.xl ^= (uint64_t)C * 8;
+    gf128_mul(G.xh, G.xl, G.hh, G.hl);
+    gcm_block<NR>(key, iv, 1, ks, T);   // E_K(J0)
+    uint8_t tag[16];
+    for (int u = 0; u < 16; u++) {
+        const uint64_t half = u < 8 ? G.xh : G.xl;
+        tag[u] = (uint8_t)(half >> (56 - 8 * (u & 7))) ^
+                 (uint8_t)(ks[u >> 2] >> (8 * (u & 3)));
+    }
+    if (protect) {
+        for (uint32_t u = 0; u < TL; u++)
+            p[P + u] = tag[u];
+        for (uint32_t u = 0; u < key->mki_size; u++)
+            tr[4 + u] = key->mki[u];
+        return;
+    }
+    uint32_t diff = 0;
+    for (uint32_t u = 0; u < TL; u++)
+        diff |= p[P + u] ^ tag[u];
+    auth_ok[i] = (uint8_t)(diff == 0);
+    if (diff)
+        return;
+    for (uint32_t j = 0; 16 * j < C; j++) {
+        gcm_block<NR>(key, iv, j + 2, ks, T);
+        for (uint32_t b = 0; b < 16 && 16 * j + b < C; b++)
+            p[8 + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rtcp(uint8_t *arena,
+                                              const uint64_t *off,
+                                              const srtp_dev_meta_t *meta,
+                                              const srtp_dev_key_t *keys,
+                                              uint8_t *auth_ok, uint32_t n,
+                                              int protect)
+{
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    load_aes_tables<false>(s_tab);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const srtp_dev_meta_t m = meta[i];
+    if (SRTP_META_STATUS(m.info))
+        return;
+    const srtp_dev_key_t *key = keys + m.key;
+    const AesLds T = make_aes_lds(s_tab);
+    uint8_t *p = arena + off[i];
+    if (key->family == SRTP_DEV_GCM) {
+        if (key->rounds == 10)
+            rtcp_gcm<10>(key, m, p, auth_ok, i, protect != 0, T);
+        else
+            rtcp_gcm<14>(key, m, p, auth_ok, i, protect != 0, T);
+        return;
+    }
+    const uint32_t E = m.info & 1u;
+    const bool enc = E && key->family == SRTP_DEV_ICM;
+    const uint32_t tag_len = key->tag_len, mki_size = key->mki_size;
+    if (protect) {
+        const uint32_t P = m.len;
+        const uint32_t tr = (E << 31) | m.roc;
+        p[P] = (uint8_t)(tr >> 24);
+        p[P + 1] = (uint8_t)(tr >> 16);
+        p[P + 2] = (uint8_t)(tr >> 8);
+        p[P + 3] = (uint8_t)tr;
+        if (enc)
+            rtcp_crypt(key, m.roc, p, P, T);
+        for (uint32_t u = 0; u < mki_size; u++)
+            p[P + 4 + u] = key->mki[u];
+        if (key->auth) {
+            uint32_t oh[5];
+            hmac_sha1_bytes(key, p, P + 4, oh);
+            uint8_t *tp = p + P + 4 + mki_size;
+            for (uint32_t u = 0; u < tag_len; u++)
+                tp[u] = (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3)));
+        }
+    } else {
+        const uint32_t A = m.len;   // authenticated bytes, trailer included
+        uint32_t ok = 1;
+        if (key->auth) {
+            uint32_t oh[5];
+            hmac_sha1_bytes(key, p, A, oh);
+            const uint8_t *tp = p + A + mki_size;
+            uint32_t diff = 0;   // constant time (datatypes.c:407-420)
+            for (uint32_t u = 0; u < tag_len; u++)
+                diff |= tp[u] ^ ((oh[u >> 2] >> (24 - 8 * (u & 3))) & 0xffu);
+            ok = diff == 0;
+        }
+        auth_ok[i] = (uint8_t)ok;
+        if (ok && enc)
+            rtcp_crypt(key, m.roc, p, A - 4, T);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// header parse for the device-resident API (srtp_validate_rtp_header,
+// srtp.c:307-336; header length 96-125)
+__global__ void k_parse(const uint8_t *in, const uint64_t *in_off,
+                        const uint32_t *in_len, srtp_dev_hdr_t *hdr, uint32_t n)
+{
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t off = in_off[i];
+    hdr[i] = srtp_parse_rtp(in + off, off, in_len[i]);
+}
+
+}   // namespace
+
+// ===========================================================================
+// thin C-ABI FFI (srtp_dev.h)
+
+static thread_local char g_err[256];
+
+int srtp_gpu_fail(hipError_t e, const char *what)
+{
+    snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+    return -1;
+}
+
+// variant mask bits: which kernel instantiations the batch needs
+//   bit (family*8 + rounds_code*2 + auth) with rounds_code 0:null 1:10 2:12 3:14
+#define VBIT(fam, rc, au) (1u << ((fam) * 8 + (rc) * 2 + (au)))
+
+template <int NR, bool AUTH, bool PROT>
+static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
+                      hipStream_t st)
+{
+    IcmArgs A;
+    A.in = b->in;
+    A.in_off = b->in_off;
+    A.out = b->out;
+    A.out_off = b->out_off;
+    A.meta = b->meta;
+    A.keys = g->d_keys;
+    A.auth_ok = b->auth_ok;
+    A.abort = b->abort;
+    A.n = (uint32_t)b->n;
+    A.uni = b->uniform_key;
+    A.rest = nullptr;
+    A.any = nullptr;
+    A.any_seq = 0;
+    // uniform-key batches: the wave-uniform streaming kernel first; it
+    // leaves the groups it cannot take to k_icm_hmac (A.rest / A.any)
+    if (A.uni != 0xffffffffu && NR != 0) {
+        const int w = launch_icm_wave(g, A, NR, AUTH, PROT, st);
+        if (w < 0)
+            return w;
+    }
+    return launch_icm_nr<NR>(A, AUTH, PROT, g->ncu, st);
+}
+
+template <int NR, bool PROT>
+static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
+{
+    GcmArgs A;
+    A.in = b->in;
+    A.in_off = b->in_off;
+    A.out = b->out;
+    A.out_off = b->out_off;
+    A.meta = b->meta;
+    A.keys = g->d_keys;
+    A.ghash = g->d_ghash;
+    A.auth_ok = b->auth_ok;
+    A.abort = b->abort;
+    A.n = (uint32_t)b->n;
+    A.uni = b->uniform_key;
+    return launch_gcm_nr<NR>(A, PROT, g->ncu, st);
+}
+
+template <bool PROT>
+static int run_dir(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
+{
+    uint32_t m = b->mask;
+    int rc = 0;
+    // ICM / null family
+    if (m & VBIT(SRTP_DEV_NULL, 0, 0)) rc |= launch_icm<0, false, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_NULL, 0, 1)) rc |= launch_icm<0, true, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_ICM, 1, 0)) rc |= launch_icm<10, false, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_ICM, 1, 1)) rc |= launch_icm<10, true, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_ICM, 2, 0)) rc |= launch_icm<12, false, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_ICM, 2, 1)) rc |= launch_icm<12, true, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_ICM, 3, 0)) rc |= launch_icm<14, false, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_ICM, 3, 1)) rc |= launch_icm<14, true, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_GCM, 1, 0)) rc |= launch_gcm<10, PROT>(g, b, st);
+    if (m & VBIT(SRTP_DEV_GCM, 3, 0)) rc |= launch_gcm<14, PROT>(g, b, st);
+    return rc;
+}
+
+
+extern "C" {
+
+const char *srtp_gpu_last_error(void) { return g_err; }
+
+void **srtp_gpu_pp_slot(srtp_gpu_t *g) { return &g->pp; }
+void *srtp_gpu_stream_of(srtp_gpu_t *g) { return (void *)g->stream; }
+
+int srtp_gpu_available(void)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess)
+        return 0;
+    return n > 0;
+}
+
+int srtp_gpu_open(srtp_gpu_t **gp)
+{
+    *gp = NULL;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n == 0) {
+        snprintf(g_err, sizeof g_err, "no HIP device (%s)",
+                 hipGetErrorString(e));
+        return -1;
+    }
+    int dev = -1;
+    HIPCHK(hipGetDevice(&dev));
+    srtp_gpu_t *g = (srtp_gpu_t *)calloc(1, sizeof(srtp_gpu_t));
+    HIPCHK(hipDeviceGetAttribute(&g->ncu, hipDeviceAttributeMultiprocessorCount,
+                                 dev));
+    if (g->ncu <= 0)
+        g->ncu = 256;
+    const char *wv = getenv("SRTP_MI355X_WAVE");
+    g->wave_off = wv && wv[0] == '0';
+    HIPCHK(hipMalloc((void **)&g->d_wave_cnt, 2 * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(g->d_wave_cnt, 0, 2 * sizeof(unsigned long long)));
+    HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&g->ev0));
+    HIPCHK(hipEventCreate(&g->ev1));
+    *gp = g;
+    return 0;
+}
+
+void srtp_gpu_close(srtp_gpu_t *g)
+{
+    if (!g)
+        return;
+    (void)hipStreamSynchronize(g->stream);
+    srtp_gpu_pp_free(g->pp);
+    (void)hipFree(g->d_keys);
+    (void)hipFree(g->d_ghash);
+    (void)hipFree(g->d_rest);
+    (void)hipFree(g->d_any);
+    (void)hipFree(g->d_wave_cnt);
+    (void)hipEventDestroy(g->ev0);
+    (void)hipEventDestroy(g->ev1);
+    (void)hipStreamDestroy(g->stream);
+    free(g);
+}
+
+static int grow(void **p, uint32_t *cap, uint32_t need, size_t elem)
+{
+    if (need <= *cap)
+        return 0;
+    uint32_t nc = *cap ? *cap : 16;
+    while (nc < need)
+        nc *= 2;
+    void *np = NULL;
+    HIPCHK(hipMalloc(&np, (size_t)nc * elem));
+    if (*p) {
+        HIPCHK(hipMemcpy(np, *p, (size_t)(*cap) * elem, hipMemcpyDeviceToDevice));
+        HIPCHK(hipFree(*p));
+    }
+    *p = np;
+    *cap = nc;
+    return 0;
+}
+
+int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
+                     const uint32_t *ghash_tab)
+{
+    if (grow((void **)&g->d_keys, &g->key_cap, slot + 1, sizeof(srtp_dev_key_t)))
+        return -1;
+    HIPCHK(hipMemcpyAsync(g->d_keys + slot, k, sizeof *k,
+                          hipMemcpyHostToDevice, g->stream));
+    if (ghash_tab) {
+        if (grow((void **)&g->d_ghash, &g->ghash_cap, k->ghash_slot + 1,
+                 1024 * sizeof(uint32_t)))
+            return -1;
+        HIPCHK(hipMemcpyAsync(g->d_ghash + 1024 * (size_t)k->ghash_slot,
+                              ghash_tab, 4096, hipMemcpyHostToDevice,
+                              g->stream));
+    }
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return 0;
+}
+
+int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b)
+{
+    if (b->n == 0)
+        return 0;
+    hipStream_t st = (hipStream_t)b->stream;   // NULL = the null stream
+    if (g->timing)
+        HIPCHK(hipEventRecord(g->ev0, st));
+    int rc = op == 0 ? run_dir<true>(g, b, st) : run_dir<false>(g, b, st);
+    if (g->timing) {
+        HIPCHK(hipEventRecord(g->ev1, st));
+        HIPCHK(hipEventSynchronize(g->ev1));
+        HIPCHK(hipEventElapsedTime(&g->last_ms, g->ev0, g->ev1));
+    }
+    return rc;
+}
+
+int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
+                  const uint64_t *off, const srtp_dev_meta_t *meta,
+                  void *stream)
+{
+    if (!n)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    hipLaunchKernelGGL(k_undo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, arena, off, meta, g->d_keys, (uint32_t)n);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int srtp_gpu_rtcp(srtp_gpu_t *g, int op, size_t n, uint8_t *arena,
+                  const uint64_t *off, const srtp_dev_meta_t *meta,
+                  uint8_t *auth_ok, void *stream)
+{
+    if (!n)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    hipLaunchKernelGGL(k_rtcp, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       st, arena, off, meta, g->d_keys, auth_ok, (uint32_t)n,
+                       op == 0 ? 1 : 0);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
+                   const uint64_t *in_off, const uint32_t *in_len,
+                   srtp_dev_hdr_t *hdr_out, void *stream)
+{
+    if (!n)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    hipLaunchKernelGGL(k_parse, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                       0, st, in, in_off, in_len, hdr_out, (uint32_t)n);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+void *srtp_gpu_malloc(size_t bytes)
+{
+    void *p = NULL;
+    if (hipMalloc(&p, bytes ? bytes : 16) != hipSuccess)
+        return NULL;
+    return p;
+}
+
+void srtp_gpu_free(void *p)
+{
+    if (p)
+        (void)hipFree(p);
+}
+
+void *srtp_gpu_host_alloc(size_t bytes)
+{
+    void *p = NULL;
+    if (hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault) !=
+        hipSuccess)
+        return NULL;
+    return p;
+}
+
+void srtp_gpu_host_free(void *p)
+{
+    if (p)
+        (void)hipHostFree(p);
+}
+
+int srtp_gpu_h2d(srtp_gpu_t *g, void *dst, const void *src, size_t n,
+                 void *stream)
+{
+    if (!n)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st));
+    return 0;
+}
+
+int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
+                 void *stream)
+{
+    if (!n)
+        return 0;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    HIPCHK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, st));
+    return 0;
+}
+
+int srtp_gpu_sync(srtp_gpu_t *g, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
+    HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+double srtp_gpu_last_kernel_ms(srtp_gpu_t *g) { return g->last_ms; }
+
+int srtp_gpu_wave_stats(srtp_gpu_t *g, uint64_t out[2])
+{
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long c[2];
+    HIPCHK(hipMemcpy(c, g->d_wave_cnt, sizeof c, hipMemcpyDeviceToHost));
+    out[0] = c[0];
+    out[1] = c[1];
+    return 0;
+}
+void srtp_gpu_set_timing(srtp_gpu_t *g, int on) { g->timing = on; }
+
+}   // extern "C"

@@ -87,6 +87,7 @@ typedef struct {
      * reports no_such_op) */
     uint32_t rslot;
     size_t rtag_len;
+    int rgcm;               /* the RTCP cipher is AES-GCM (MKI offset)      */
 } hkey_t;
 
 typedef struct {
@@ -672,6 +673,7 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
     hk->rtag_len = rtcp->auth_tag_len;
     int rtcp_gcm = rtcp->cipher_type == SRTP_AES_GCM_128 ||
                    rtcp->cipher_type == SRTP_AES_GCM_256;
+    hk->rgcm = rtcp_gcm;
     /* srtp.c:4380-4384 picks the AEAD path from the RTP cipher: the two
      * must agree here */
     int rtcp_gpu = rtcp_gcm == (hk->family == SRTP_DEV_GCM) &&
@@ -927,9 +929,9 @@ static srtp_err_status_t add_stream(srtp_t ctx, const srtp_policy_t *p)
 
 srtp_err_status_t srtp_stream_add(srtp_t ctx, const srtp_policy_t *p)
 {
-    dev_pull(ctx);
     if (!ctx)
         return srtp_err_status_bad_param;
+    dev_pull(ctx);
     srtp_err_status_t st = valid_policy(p);
     if (st)
         return st;
@@ -1031,7 +1033,11 @@ static srtp_err_status_t update_specific(srtp_t ctx, const srtp_policy_t *p)
         return srtp_err_status_bad_param;
     if (s->use_mki != p->use_mki || (s->use_mki && s->mki_size != p->mki_size))
         return srtp_err_status_bad_param;
+    /* the extended sequence number and the SRTCP replay database survive
+     * the update (srtp.c:3594-3614: old_index, old_rtcp_rdb) */
     uint64_t old_index = s->rdbx.index;
+    uint32_t old_rtcp_start = s->rtcp_start, old_rtcp_bm[4];
+    memcpy(old_rtcp_bm, s->rtcp_bm, sizeof old_rtcp_bm);
     srtp_err_status_t st = srtp_stream_remove(ctx, p->ssrc.value);
     if (st)
         return st;
@@ -1042,6 +1048,8 @@ static srtp_err_status_t update_specific(srtp_t ctx, const srtp_policy_t *p)
     if (!s)
         return srtp_err_status_fail;
     s->rdbx.index = old_index;
+    s->rtcp_start = old_rtcp_start;
+    memcpy(s->rtcp_bm, old_rtcp_bm, sizeof old_rtcp_bm);
     return srtp_err_status_ok;
 }
 
@@ -1069,7 +1077,11 @@ static srtp_err_status_t update_template(srtp_t ctx, const srtp_policy_t *p)
             stream_free(ctx, nt);
             return srtp_err_status_alloc_fail;
         }
+        /* srtp.c:3459-3483: extended sequence number and SRTCP replay
+         * database carried over */
         c->rdbx.index = s->rdbx.index;
+        c->rtcp_start = s->rtcp_start;
+        memcpy(c->rtcp_bm, s->rtcp_bm, sizeof c->rtcp_bm);
         ctx->list[i] = c;
         stream_free(ctx, s);
     }
@@ -2414,10 +2426,11 @@ static srtp_err_status_t rtcp_pre_unprotect(srtp_t ctx, const uint8_t *srtcp,
             return srtp_err_status_no_ctx;
         st = ctx->templ; /* provisional; clones share its keys/services */
     }
-    /* srtp_get_session_keys_for_rtcp_packet, srtp.c:2018-2035 */
+    /* srtp_get_session_keys_for_rtcp_packet, srtp.c:2018-2035: the MKI
+     * sits before a tag whose length follows key 0's RTCP cipher */
     hkey_t *k = &st->keys->k[0];
     if (st->use_mki) {
-        size_t tl = k->family == SRTP_DEV_GCM ? 0 : k->rtag_len;
+        size_t tl = k->rgcm ? 0 : k->rtag_len;
         if (tl > srtcp_len || st->mki_size > srtcp_len - tl)
             return srtp_err_status_bad_mki;
         k = mki_lookup(st, srtcp + srtcp_len - tl - st->mki_size);
@@ -2867,6 +2880,18 @@ void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
         *device_batches = ctx ? ctx->dt.fast_batches : 0;
     if (host_batches)
         *host_batches = ctx ? ctx->dt.host_batches : 0;
+}
+
+void srtp_mi355x_wave_stats(srtp_t ctx, uint64_t *wave_groups,
+                            uint64_t *rest_groups)
+{
+    uint64_t c[2] = { 0, 0 };
+    if (ctx && ctx->gpu)
+        (void)srtp_gpu_wave_stats(ctx->gpu, c);
+    if (wave_groups)
+        *wave_groups = c[0];
+    if (rest_groups)
+        *rest_groups = c[1];
 }
 
 /* Test hook (no GPU): drives the protect pre-pass index / replay logic of a
