@@ -375,13 +375,6 @@ void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
  * / receiver direction, 4 sequence number not advancing by 1..2^15-1,
  * 64 empty session, 128 a key near its usage limit */
 int srtp_mi355x_prepass_last_abort(srtp_t ctx);
-/* 64-packet groups protected by the streaming wave kernel (k_icm_wave) and
- * groups it left to the general kernel, summed over the session's batches
- * (synchronises the session's device).  Uniform-key AES-ICM + HMAC-SHA1
- * protect batches only; SRTP_MI355X_WAVE=0 in the environment disables the
- * wave kernel (k_icm_hmac then takes every packet, and nothing is counted). */
-void srtp_mi355x_wave_stats(srtp_t ctx, uint64_t *wave_groups,
-                            uint64_t *rest_groups);
 /* 1 when a HIP device is usable from this process */
 int srtp_mi355x_gpu_available(void);
 

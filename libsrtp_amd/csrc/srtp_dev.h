@@ -192,9 +192,6 @@ int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
                  void *stream);
 int srtp_gpu_sync(srtp_gpu_t *g, void *stream);
 
-/* groups taken by / left by k_icm_wave so far: out[0], out[1] */
-int srtp_gpu_wave_stats(srtp_gpu_t *g, uint64_t out[2]);
-
 /* timing of the last srtp_gpu_run kernels (ms, from HIP events) */
 double srtp_gpu_last_kernel_ms(srtp_gpu_t *g);
 void srtp_gpu_set_timing(srtp_gpu_t *g, int on);

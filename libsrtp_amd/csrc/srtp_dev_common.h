@@ -1,5 +1,5 @@
 // srtp_dev_common.h -- CDNA4 (gfx950) device building blocks shared by the
-// SRTP kernels (srtp_icm.hip, srtp_icm_wave.hip, srtp_gcm.hip, srtp_gpu.hip).
+// SRTP kernels (srtp_icm.hip, srtp_gcm.hip, srtp_gpu.hip).
 //
 //   AES (T-table) crypto/cipher/aes.c:2102-2130 semantics, AES-ICM counter
 //   caching (aes_icm.c:236-414), SHA-1 compression (crypto/hash/sha1.c:91-212),
@@ -126,9 +126,18 @@ DEV AesLds make_aes_lds(const void *lds)
 
 // address of T_TAB[byte K of w] for an even TAB; odd tables sit +128 bytes
 // further (the ds_read immediate offset)
+// Byte 1 is already at bits 15:8: (w & 0xff00) | template is one
+// v_bitop3_b32, a full-rate VALU op on gfx950, where v_perm_b32 is
+// half-rate (tools/valu_rate.hip: 1.15 vs 1.9 ns per wave-instruction per
+// SIMD); the other bytes need the permute.
+#ifndef AES_BITOP3_B1
+#define AES_BITOP3_B1 1
+#endif
 template <int TAB, int K>
 DEV uint32_t ta(const AesLds &T, uint32_t w)
 {
+    if constexpr (K == 1 && AES_BITOP3_B1)
+        return __builtin_amdgcn_bitop3_b32(w, 0x0000ff00u, T.L[TAB >> 1], 0xEA);
     return __builtin_amdgcn_perm(w, T.L[TAB >> 1], 0x0c020000u | ((4u + K) << 8));
 }
 

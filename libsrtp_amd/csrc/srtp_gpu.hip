@@ -1,8 +1,8 @@
 // srtp_gpu.hip -- the thin extern "C" FFI (srtp_dev.h) between the C host
 // engine and the HIP kernels: device context, key table, kernel dispatch,
 // plus the small kernels (speculative-unprotect undo, SRTCP, header parse).
-// The RTP crypto kernels live in srtp_icm.hip, srtp_icm_wave.hip and
-// srtp_gcm.hip (srtp_gpu_int.h).
+// The RTP crypto kernels live in srtp_icm.hip and srtp_gcm.hip
+// (srtp_gpu_int.h).
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -409,16 +409,6 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
-    A.rest = nullptr;
-    A.any = nullptr;
-    A.any_seq = 0;
-    // uniform-key batches: the wave-uniform streaming kernel first; it
-    // leaves the groups it cannot take to k_icm_hmac (A.rest / A.any)
-    if (A.uni != 0xffffffffu && NR != 0) {
-        const int w = launch_icm_wave(g, A, NR, AUTH, PROT, st);
-        if (w < 0)
-            return w;
-    }
     return launch_icm_nr<NR>(A, AUTH, PROT, g->ncu, st);
 }
 
@@ -492,10 +482,6 @@ int srtp_gpu_open(srtp_gpu_t **gp)
                                  dev));
     if (g->ncu <= 0)
         g->ncu = 256;
-    const char *wv = getenv("SRTP_MI355X_WAVE");
-    g->wave_off = wv && wv[0] == '0';
-    HIPCHK(hipMalloc((void **)&g->d_wave_cnt, 2 * sizeof(unsigned long long)));
-    HIPCHK(hipMemset(g->d_wave_cnt, 0, 2 * sizeof(unsigned long long)));
     HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&g->ev0));
     HIPCHK(hipEventCreate(&g->ev1));
@@ -511,9 +497,6 @@ void srtp_gpu_close(srtp_gpu_t *g)
     srtp_gpu_pp_free(g->pp);
     (void)hipFree(g->d_keys);
     (void)hipFree(g->d_ghash);
-    (void)hipFree(g->d_rest);
-    (void)hipFree(g->d_any);
-    (void)hipFree(g->d_wave_cnt);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);
     (void)hipStreamDestroy(g->stream);
@@ -670,16 +653,6 @@ int srtp_gpu_sync(srtp_gpu_t *g, void *stream)
 }
 
 double srtp_gpu_last_kernel_ms(srtp_gpu_t *g) { return g->last_ms; }
-
-int srtp_gpu_wave_stats(srtp_gpu_t *g, uint64_t out[2])
-{
-    HIPCHK(hipDeviceSynchronize());
-    unsigned long long c[2];
-    HIPCHK(hipMemcpy(c, g->d_wave_cnt, sizeof c, hipMemcpyDeviceToHost));
-    out[0] = c[0];
-    out[1] = c[1];
-    return 0;
-}
 void srtp_gpu_set_timing(srtp_gpu_t *g, int on) { g->timing = on; }
 
 }   // extern "C"

@@ -5,8 +5,6 @@
 //                       (undo, SRTCP, header parse), kernel dispatch
 //   srtp_icm.hip        k_icm_hmac, the general one-lane-per-packet AES-ICM +
 //                       HMAC-SHA1 kernel; compiled once per AES round count
-//   srtp_icm_wave.hip   k_icm_wave, the wave-uniform streaming kernel for
-//                       uniform-key batches (the headline path)
 //   srtp_gcm.hip        k_gcm (AES-GCM); compiled once per round count
 //   srtp_prepass.hip    the device pre-pass of srtp_protect_device
 #pragma once
@@ -27,13 +25,6 @@ struct srtp_gpu {
     float last_ms;
     void *pp;         // device pre-pass state (srtp_prepass.hip)
     int ncu;          // compute units (persistent grids)
-    uint8_t *d_rest;  // per-64-packet-group "left for k_icm_hmac" flags
-    size_t rest_cap;  // bytes of d_rest
-    uint32_t *d_any;  // word: = wave_seq when the last k_icm_wave left a
-                      // group to k_icm_hmac
-    uint32_t wave_seq;
-    unsigned long long *d_wave_cnt;   // [0] groups taken, [1] groups left
-    int wave_off;     // SRTP_MI355X_WAVE=0: k_icm_wave disabled
 };
 
 // AES-ICM (+ HMAC-SHA1) kernel arguments
@@ -48,12 +39,6 @@ struct IcmArgs {
     const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;            // uniform key slot, ~0 if keys differ
-    // wave path hand-off (srtp_icm_wave.hip): group g of 64 packets was left
-    // to k_icm_hmac when rest[g] != 0; *any == any_seq when any group was.
-    // NULL rest: k_icm_hmac takes every packet.
-    const uint8_t *rest;
-    const uint32_t *any;
-    uint32_t any_seq;
 };
 
 // AES-GCM kernel arguments
@@ -85,12 +70,6 @@ int srtp_gpu_fail(hipError_t e, const char *what);
 template <int NR>
 int launch_icm_nr(const IcmArgs &A, bool auth, bool prot, int ncu,
                   hipStream_t st);
-
-// k_icm_wave launcher (srtp_icm_wave.hip): returns 1 when it launched (the
-// caller then launches k_icm_hmac with A.rest / A.any set), 0 when the
-// configuration has no wave kernel, -1 on error
-int launch_icm_wave(srtp_gpu_t *g, IcmArgs &A, int nr, bool auth, bool prot,
-                    hipStream_t st);
 
 // k_gcm launchers (srtp_gcm.hip, one object per NR in {10,14})
 template <int NR>

@@ -2882,18 +2882,6 @@ void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
         *host_batches = ctx ? ctx->dt.host_batches : 0;
 }
 
-void srtp_mi355x_wave_stats(srtp_t ctx, uint64_t *wave_groups,
-                            uint64_t *rest_groups)
-{
-    uint64_t c[2] = { 0, 0 };
-    if (ctx && ctx->gpu)
-        (void)srtp_gpu_wave_stats(ctx->gpu, c);
-    if (wave_groups)
-        *wave_groups = c[0];
-    if (rest_groups)
-        *rest_groups = c[1];
-}
-
 /* Test hook (no GPU): drives the protect pre-pass index / replay logic of a
  * fresh stream over a sequence of sequence numbers, as srtp_protect would
  * (srtp.c:2662-2690).  pending_roc != 0 emulates srtp_stream_set_roc()

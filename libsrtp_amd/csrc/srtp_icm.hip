@@ -1,7 +1,7 @@
 // srtp_icm.hip -- k_icm_hmac: AES-ICM keystream + XOR + HMAC-SHA1 for SRTP
 // protect / unprotect, one lane per packet, any mix of keys, lengths and
-// header sizes (the general path; uniform-key batches of equal-length
-// packets take k_icm_wave first, srtp_icm_wave.hip).
+// header sizes; uniform-key batches take the lane-quad cooperative memory
+// path in the steady state.
 //
 // Replaces, on the GPU, the per-packet crypto libsrtp's srtp_protect /
 // srtp_unprotect run through the cipher/auth vtables:
@@ -580,8 +580,6 @@ void k_icm_hmac(IcmArgs A)
     __shared__ u32x4 s_tab[LDSB / 16];
     if (A.abort && *A.abort)
         return;
-    if (A.rest && *A.any != A.any_seq)
-        return;   // k_icm_wave took every packet
     if (NR)
         load_aes_tables<TAB4>(s_tab);
     __syncthreads();
@@ -597,8 +595,7 @@ void k_icm_hmac(IcmArgs A)
     const uint32_t first = blockIdx.x * blockDim.x + (threadIdx.x & ~63u) +
                            16 * (L & 3) + (L >> 2);
     for (uint32_t i = first; i < A.n; i += stride)
-        if (!A.rest || A.rest[i >> 6])
-            icm_packet<NR, TAB4, AUTH, PROTECT, UNIFORM>(A, i, T, rk);
+        icm_packet<NR, TAB4, AUTH, PROTECT, UNIFORM>(A, i, T, rk);
 }
 
 }   // namespace

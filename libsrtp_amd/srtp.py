@@ -147,8 +147,7 @@ def lib():
         "srtp_mi355x_prepass_stats": ([P, C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
-        "srtp_mi355x_wave_stats": ([P, C.POINTER(C.c_uint64),
-                                    C.POINTER(C.c_uint64)], None),
+
         "srtp_get_version_string": ([], C.c_char_p),
     }
     for name, (args, res) in sig.items():
@@ -387,12 +386,6 @@ class Session:
     def prepass_last_abort(self):
         """reason bits of the most recent device pre-pass fallback (0: none)"""
         return self.L.srtp_mi355x_prepass_last_abort(self.h)
-
-    def wave_stats(self):
-        """(groups by k_icm_wave, groups left to k_icm_hmac) so far"""
-        w, r = C.c_uint64(), C.c_uint64()
-        self.L.srtp_mi355x_wave_stats(self.h, C.byref(w), C.byref(r))
-        return w.value, r.value
 
     def prepass_stats(self):
         """(device-API batches done by the GPU pre-pass, by the host)"""

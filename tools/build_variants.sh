@@ -1,17 +1,28 @@
 #!/bin/bash
-# Builds timing-experiment variants of libsrtp_mi355x.so into exp_build/<name>/
-# usage: tools/build_variants.sh name "-DFLAG ..." [name "-D..."]...
+# Builds timing-experiment variants of libsrtp_mi355x.so into
+# exp_build/<name>/: one kernel translation unit recompiled with extra flags
+# (srtp_icm_wave.hip by default, TU=srtp_gcm_nr14 for the GCM-256 kernel),
+# every other object taken from libsrtp_amd/build.  Compiles run in parallel.
+# usage: [TU=srtp_gcm_nr14] tools/build_variants.sh name "-DFLAG ..." [name "-D..."]...
 set -e
-make -s -C "$(cd "$(dirname "$0")/.." && pwd)/libsrtp_amd"
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
+make -s -j8 -C "$ROOT/libsrtp_amd"
+TU=${TU:-srtp_icm_wave}
+case $TU in
+  srtp_gcm_nr*) SRC=$ROOT/libsrtp_amd/csrc/srtp_gcm.hip; EXTRA="-DGCM_NR=${TU#srtp_gcm_nr}";;
+  srtp_icm_nr*) SRC=$ROOT/libsrtp_amd/csrc/srtp_icm.hip; EXTRA="-DICM_NR=${TU#srtp_icm_nr}";;
+  *) SRC=$ROOT/libsrtp_amd/csrc/$TU.hip; EXTRA="";;
+esac
+OTHERS=$(ls $ROOT/libsrtp_amd/build/*.o | grep -v "/$TU.o$")
+pids=()
+names=()
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   d=$ROOT/exp_build/$name; mkdir -p $d
-  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 $flags \
-     -I$ROOT/include -I$ROOT/libsrtp_amd/csrc -c $ROOT/libsrtp_amd/csrc/srtp_kernels.hip -o $d/k.o &
-  gcc -O2 -fPIC -std=gnu11 -I$ROOT/include -I$ROOT/libsrtp_amd/csrc -c $ROOT/libsrtp_amd/csrc/srtp_host.c -o $d/h.o
-  gcc -O2 -fPIC -std=gnu11 -I$ROOT/include -I$ROOT/libsrtp_amd/csrc -c $ROOT/libsrtp_amd/csrc/host_crypto.c -o $d/c.o
-  wait
-  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libsrtp_mi355x.so $d/k.o $d/h.o $d/c.o $ROOT/libsrtp_amd/build/srtp_prepass.o
-  echo built $name
+  ( /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 $EXTRA $flags \
+       -I$ROOT/include -I$ROOT/libsrtp_amd/csrc -c $SRC -o $d/k.o &&
+    /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $d/libsrtp_mi355x.so \
+       $d/k.o $OTHERS && echo "built $name" ) &
+  pids+=($!)
 done
+for p in "${pids[@]}"; do wait $p; done

@@ -243,6 +243,9 @@ int main(int argc, char **argv)
     uint8_t *in, *out;
     if (hipMalloc(&in, bytes) || hipMalloc(&out, bytes))
         return 1;
+    // argv[3] = 1: in place (the SRTP kernels protect in place)
+    if (argc > 3 && atoi(argv[3]) == 1)
+        out = in;
     hipMemset(in, 1, bytes);
     const double algo = (double)n * NCH * 64 * 2;
     const char *names[] = { "lane", "quad", "spread", "oct", "linear" };
