@@ -109,6 +109,10 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
             if (c + GCM_PF < nfc)
                 load_chunk4(ring[GCM_PF - 1], pin + 64 * (c + GCM_PF));
             uint32_t ks[4][4];
+#ifdef GCM_EXP_NOAES   // timing experiment only: no keystream
+            for (int t = 0; t < 4; t++)
+                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = t;
+#else
 #pragma unroll
             for (int g = 0; g < 4; g += 2) {
                 const uint32_t jb[2] = { (4 * c + g + 2) << 8,
@@ -116,6 +120,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
                 aes_ctr<2, NR, false>(
                     *reinterpret_cast<uint32_t(*)[2][4]>(&ks[g]), jb, C, rk, T);
             }
+#endif
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 const u32x4 o = { cur[t].x ^ ks[t][0], cur[t].y ^ ks[t][1],
@@ -126,7 +131,11 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
                 x[1] ^= bswap(ctv.y);
                 x[2] ^= bswap(ctv.z);
                 x[3] ^= bswap(ctv.w);
+#ifdef GCM_EXP_NOGHASH   // timing experiment only: fold instead of multiply
+                x[0] ^= x[3] >> 1;
+#else
                 ghash_mul(x, G);
+#endif
             }
         }
         j = 4 * nfc;
@@ -201,6 +210,8 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
     __shared__ u32x4 s_tab[(AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 16];
     if (A.abort && *A.abort)
         return;
+    if (A.rest && *A.any != A.any_seq)
+        return;   // k_gcm_wave took every group
     load_aes_tables<false>(s_tab);
     if (UNIFORM) {
         const u32x4 *src =
@@ -223,7 +234,8 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
          i += stride)
-        gcm_packet<NR, PROTECT, UNIFORM>(A, i, T, G, rk);
+        if (!A.rest || A.rest[i >> 6])
+            gcm_packet<NR, PROTECT, UNIFORM>(A, i, T, G, rk);
 }
 
 }   // namespace

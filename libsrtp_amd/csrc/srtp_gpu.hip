@@ -1,8 +1,8 @@
 // srtp_gpu.hip -- the thin extern "C" FFI (srtp_dev.h) between the C host
 // engine and the HIP kernels: device context, key table, kernel dispatch,
 // plus the small kernels (speculative-unprotect undo, SRTCP, header parse).
-// The RTP crypto kernels live in srtp_icm.hip and srtp_gcm.hip
-// (srtp_gpu_int.h).
+// The RTP crypto kernels live in srtp_icm.hip, srtp_gcm.hip and
+// srtp_gcm_wave.hip (srtp_gpu_int.h).
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -427,6 +427,13 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
+    A.rest = nullptr;
+    A.any = nullptr;
+    A.any_seq = 0;
+    // uniform-key batches: the cooperative wave kernel first; it leaves
+    // the groups it cannot take to k_gcm
+    if (launch_gcm_wave(g, A, NR, PROT, st) < 0)
+        return -1;
     return launch_gcm_nr<NR>(A, PROT, g->ncu, st);
 }
 
@@ -482,6 +489,8 @@ int srtp_gpu_open(srtp_gpu_t **gp)
                                  dev));
     if (g->ncu <= 0)
         g->ncu = 256;
+    const char *wv = getenv("SRTP_MI355X_WAVE");
+    g->wave_off = wv && wv[0] == '0';
     HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&g->ev0));
     HIPCHK(hipEventCreate(&g->ev1));
@@ -497,6 +506,8 @@ void srtp_gpu_close(srtp_gpu_t *g)
     srtp_gpu_pp_free(g->pp);
     (void)hipFree(g->d_keys);
     (void)hipFree(g->d_ghash);
+    (void)hipFree(g->d_rest);
+    (void)hipFree(g->d_any);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);
     (void)hipStreamDestroy(g->stream);

@@ -16,7 +16,7 @@ import pytest
 
 import libsrtp_amd as L
 from oracle import pyoracle as O
-from tests.test_gpu_parity import policy, rtp_packet
+from tests.test_gpu_parity import POLICIES, policy, rtp_packet
 
 pytestmark = pytest.mark.gpu
 
@@ -66,20 +66,21 @@ def _layout(rng, pkts, trailer, base_skew):
     return off, cur + 64
 
 
-def _run(seed, ngroups, inplace, mixed_every=0, nssrc=1, tail=0):
+def _run(seed, ngroups, inplace, mixed_every=0, nssrc=1, tail=0,
+         pname="icm128_hmac80"):
     import torch
     _gpu()
     rng = random.Random(seed)
     ssrcs = [0xcafebabe + 7919 * k for k in range(nssrc)]
     if nssrc == 1:
-        pol = policy("icm128_hmac80", ssrc=ssrcs[0], seed=seed)
+        pol = policy(pname, ssrc=ssrcs[0], seed=seed)
     else:   # ssrc_any_outbound template: every stream clones one key
-        pol = policy("icm128_hmac80", ssrc=0, ssrc_type=3, seed=seed)
+        pol = policy(pname, ssrc=0, ssrc_type=3, seed=seed)
     seq = {s: rng.randrange(0x10000) for s in ssrcs}
     pkts = _groups(rng, ngroups, mixed_every, ssrcs, seq)
     pkts += _groups(rng, 1, 0, ssrcs, seq)[:tail]
     n = len(pkts)
-    trailer = 10
+    trailer = POLICIES[pname][4]
     ioff, isize = _layout(rng, pkts, trailer, 16 * rng.randrange(4))
     if inplace:
         ooff, osize = ioff, isize
@@ -125,6 +126,29 @@ def _run(seed, ngroups, inplace, mixed_every=0, nssrc=1, tail=0):
             e = ooff[i] + olen[i]
             nxt = ooff[i + 1] if i + 1 < n else len(out)
             assert out[e:nxt] == before[e:nxt], ("stray write after", i)
+    # unprotect the protected arena (every 5th packet tampered) into a fresh
+    # arena: plaintext == the original packets, tampered ones auth_fail
+    tam = torch.tensor([i for i in range(n) if i % 5 == 3], dtype=torch.int64)
+    src = d_out.clone()
+    flip = torch.tensor(ooff, dtype=torch.int64)[tam] + \
+        torch.tensor(olen, dtype=torch.int64)[tam] - 1
+    src[flip.to(dev)] ^= 1
+    roff, rsize = _layout(rng, pkts, trailer, 16 * rng.randrange(4))
+    dst = torch.full((rsize,), 0x3c, dtype=torch.uint8, device=dev)
+    rlen = t(olen, torch.int32)
+    rcap = t([len(p) for p in pkts], torch.int32)
+    rst = torch.zeros(n, dtype=torch.int32, device=dev)
+    r = L.Session([pol])
+    assert r.unprotect_device(src, t(ooff, torch.int64), rlen, dst,
+                              t(roff, torch.int64), rcap, rst) == 0
+    back = dst.cpu().numpy().tobytes()
+    rst, rcap = rst.cpu().tolist(), rcap.cpu().tolist()
+    for i, p in enumerate(pkts):
+        if i % 5 == 3:
+            assert rst[i] == 7, (i, rst[i])   # srtp_err_status_auth_fail
+            continue
+        assert rst[i] == 0 and rcap[i] == len(p), (i, rst[i], rcap[i])
+        assert back[roff[i]:roff[i] + len(p)] == p, i
 
 
 def test_shapes_one_stream_out_of_place():
@@ -172,3 +196,17 @@ def test_shapes_roc_wrap():
     for i, p in enumerate(pkts):
         rc, ref = orc.protect(p, slot)
         assert rc == 0 and out[i * slot:i * slot + len(ref)] == ref, i
+
+
+@pytest.mark.parametrize("pname", ["gcm128_16", "gcm256_16", "gcm256_8"])
+def test_shapes_gcm_out_of_place(pname):
+    _run(21, ngroups=40, inplace=False, tail=9, pname=pname)
+
+
+@pytest.mark.parametrize("pname", ["gcm128_16", "gcm256_16"])
+def test_shapes_gcm_in_place_mixed(pname):
+    _run(22, ngroups=30, inplace=True, mixed_every=3, pname=pname)
+
+
+def test_shapes_gcm_template_many_ssrcs():
+    _run(23, ngroups=20, inplace=False, nssrc=7, tail=3, pname="gcm256_16")
