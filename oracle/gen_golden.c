@@ -10,9 +10,10 @@
  * against libsrtp_ref_ossl.so (adds AES-GCM-128/256 and AES-ICM-192).
  *
  * All inputs are generated from splitmix64 with fixed seeds; nothing here is
- * transcribed from the reference except the srtp_driver.c test key and the
- * 28-byte packet of srtp_validate() (test/srtp_driver.c:2342-2426,
- * 5844-5851), which anchor the fixture to the reference's own KAT.
+ * transcribed from the reference except the srtp_driver.c test keys and the
+ * published packet KATs of test/srtp_driver.c (srtp_validate*, empty
+ * payload: see k_kats), which anchor the fixture to the reference's own
+ * known answers -- the generator exits 1 unless the build reproduces them.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -589,6 +590,210 @@ static void set_gcm_256_8(srtp_crypto_policy_t *p)
     p->auth_tag_len = 8;
 }
 
+
+/* ---------------------------------------------------------------------- */
+/* Published packet KATs of test/srtp_driver.c.  The reference build must
+ * reproduce every published byte (the generator exits 1 otherwise); the
+ * rows are then emitted under "kats" so the oracle and the GPU path are
+ * checked against the same published vectors.                            */
+
+typedef struct {
+    const char *name, *cite;
+    void (*set)(srtp_crypto_policy_t *);
+    const uint8_t *key; /* NULL: no key material (null cipher, null auth) */
+    size_t key_len;
+    int mki;            /* two master keys with the driver's 4-byte MKI ids */
+    uint32_t ssrc;
+    const char *rtp, *srtp; /* srtp NULL: only the length is published */
+    size_t srtp_len;
+    const char *rtcp, *srtcp;
+    size_t srtcp_len;
+} kat_t;
+
+/* test/srtp_driver.c:5853-5875 */
+static const uint8_t k_test_key_2[46] = {
+    0xf0, 0xf0, 0x49, 0x14, 0xb5, 0x13, 0xf2, 0x76, 0x3a, 0x1b, 0x1f, 0xa1,
+    0x30, 0xf1, 0x0e, 0x29, 0x98, 0xf6, 0xf6, 0xe4, 0x3e, 0x43, 0x09, 0xd1,
+    0xe6, 0x22, 0xa0, 0xe3, 0x32, 0xb9, 0xf1, 0xb6, 0xc3, 0x17, 0xf2, 0xda,
+    0xbe, 0x35, 0x77, 0x93, 0xb6, 0x96, 0x0b, 0x3a, 0xab, 0xe6
+};
+static const uint8_t k_test_mki_1[4] = { 0xe1, 0xf9, 0x7a, 0x0d };
+static const uint8_t k_test_mki_2[4] = { 0xf3, 0xa1, 0x46, 0x71 };
+#ifdef REF_OSSL
+/* test/srtp_driver.c:4114-4121 */
+static const uint8_t k_test_192_key[38] = {
+    0x73, 0xed, 0xc6, 0x6c, 0x4f, 0xa1, 0x57, 0x76, 0xfb, 0x57, 0xf9, 0x50,
+    0x5c, 0x17, 0x13, 0x65, 0x50, 0xff, 0xda, 0x71, 0xf3, 0xe8, 0xe5, 0xf1,
+    0xc8, 0x52, 0x2f, 0x3a, 0xcd, 0x4c, 0xe8, 0x6d, 0x5a, 0xdd, 0x78, 0xed,
+    0xbb, 0x11
+};
+#endif
+
+#define AB16 "abababababababababababababababab"
+#define RTP28 "800f1234decafbadcafebabe" AB16
+#define RTCP24 "81c8000bcafebabe" AB16
+
+static const kat_t k_kats[] = {
+#ifndef REF_OSSL
+    { "srtp_validate", "test/srtp_driver.c:2342-2498",
+      srtp_crypto_policy_set_rtp_default, k_test_key, 46, 0, 0xcafebabe,
+      RTP28, "800f1234decafbadcafebabe4e55dc4ce79978d88ca4d215949d2402"
+             "b78d6acc99ea179b8dbb", 38,
+      RTCP24, "81c8000bcafebabe7128035be487b9bdbef89041f977a5a8"
+              "80000001993e08cd54d6c1230798", 38 },
+    { "srtp_validate_mki", "test/srtp_driver.c:2500-2668",
+      srtp_crypto_policy_set_rtp_default, k_test_key, 46, 1, 0xcafebabe,
+      RTP28, "800f1234decafbadcafebabe4e55dc4ce79978d88ca4d215949d2402"
+             "e1f97a0db78d6acc99ea179b8dbb", 42,
+      RTCP24, "81c8000bcafebabe7128035be487b9bdbef89041f977a5a8"
+              "80000001e1f97a0d993e08cd54d6c1230798", 42 },
+    { "srtp_validate_null_sha1_80", "test/srtp_driver.c:2677-2827",
+      srtp_crypto_policy_set_null_cipher_hmac_sha1_80, k_test_key, 46, 0,
+      0xcafebabe, RTP28, RTP28 "aba136270b679134ce9b", 38,
+      RTCP24, RTCP24 "00000001fe88c7fdfd37ebce615d", 38 },
+    { "srtp_validate_null_null", "test/srtp_driver.c:2836-2997",
+      srtp_crypto_policy_set_null_cipher_hmac_null, NULL, 0, 0, 0xcafebabe,
+      RTP28, RTP28, 28, RTCP24, RTCP24 "00000001", 28 },
+    { "srtp_validate_aes_256", "test/srtp_driver.c:4206-4315",
+      srtp_crypto_policy_set_aes_cm_256_hmac_sha1_80, k_test_256_key, 46, 0,
+      0xcafebabe, RTP28,
+      "800f1234decafbadcafebabef1d9de17ff251ff1aa007774b0b4b40d"
+      "a08d9d9a5b3a55d8873b", 38, NULL, NULL, 0 },
+    { "srtp_test_empty_payload", "test/srtp_driver.c:4364-4437",
+      srtp_crypto_policy_set_rtp_default, k_test_key, 46, 0, 0xcafebabe,
+      "800f000100000001cafebabe", NULL, 22, NULL, NULL, 0 },
+#else
+    { "srtp_validate_gcm", "test/srtp_driver.c:3386-3547",
+      srtp_crypto_policy_set_aes_gcm_128_16_auth, k_test_key_gcm, 28, 0,
+      0xcafebabe, RTP28,
+      "800f1234decafbadcafebabec5002ede04cfdd2eb91159e0880aa06e"
+      "d2976826f796b201df3131a127e8a392", 44,
+      RTCP24, "81c8000bcafebabec98b8b5df0392a55852b6c21ac8e7025"
+              "c52c6fbea2b3b446ea31123ba88ce61e80000001", 44 },
+    { "srtp_validate_aes_192", "test/srtp_driver.c:4111-4197",
+      srtp_crypto_policy_set_aes_cm_192_hmac_sha1_80, k_test_192_key, 38, 0,
+      0x00000000, "800f0000decafbad00000000" AB16,
+      "800f0000decafbad00000000d98865552f2762c3ef37f837acfdb712"
+      "2d6bc4dc84c76f74aea5", 38, NULL, NULL, 0 },
+    { "srtp_test_empty_payload_gcm", "test/srtp_driver.c:4440-4513",
+      srtp_crypto_policy_set_aes_gcm_128_16_auth, k_test_key, 46, 0,
+      0xcafebabe, "800f000100000001cafebabe", NULL, 28, NULL, NULL, 0 },
+#endif
+};
+
+static size_t unhex(const char *h, uint8_t *out)
+{
+    size_t n = strlen(h) / 2;
+    for (size_t i = 0; i < n; i++) {
+        unsigned v;
+        sscanf(h + 2 * i, "%2x", &v);
+        out[i] = (uint8_t)v;
+    }
+    return n;
+}
+
+static void kat_fail(const kat_t *k, const char *what)
+{
+    fprintf(stderr, "reference build fails %s (%s): %s\n", k->name, k->cite,
+            what);
+    exit(1);
+}
+
+static void gen_kats(void)
+{
+    fputs(",\n  \"kats\": [\n", g_out);
+    for (size_t ki = 0; ki < sizeof(k_kats) / sizeof(k_kats[0]); ki++) {
+        const kat_t *k = &k_kats[ki];
+        srtp_policy_t pol;
+        uint8_t keys[2][64], mkis[2][16];
+        srtp_master_key_t mk[2], *mkp[2];
+        memset(&pol, 0, sizeof pol);
+        memset(keys, 0, sizeof keys);
+        memset(mkis, 0, sizeof mkis);
+        k->set(&pol.rtp);
+        k->set(&pol.rtcp);
+        pol.ssrc.type = ssrc_specific;
+        pol.ssrc.value = k->ssrc;
+        if (k->key)
+            memcpy(keys[0], k->key, k->key_len);
+        if (k->mki) {
+            memcpy(keys[1], k_test_key_2, 46);
+            memcpy(mkis[0], k_test_mki_1, 4);
+            memcpy(mkis[1], k_test_mki_2, 4);
+            for (int i = 0; i < 2; i++) {
+                mk[i].key = keys[i];
+                mk[i].mki_id = mkis[i];
+                mkp[i] = &mk[i];
+            }
+            pol.keys = mkp;
+            pol.num_master_keys = 2;
+            pol.use_mki = true;
+            pol.mki_size = 4;
+        } else {
+            pol.key = keys[0];
+        }
+        pol.window_size = 128;
+        srtp_t snd, rcv;
+        if (srtp_create(&snd, &pol) || srtp_create(&rcv, &pol))
+            kat_fail(k, "srtp_create");
+        fprintf(g_out, "%s    {\"name\": \"%s\", \"cite\": \"%s\", \"snd\": ",
+                ki ? ",\n" : "", k->name, k->cite);
+        emit_policy(&pol, keys, mkis, k->mki ? 2 : 1);
+        fputs(", \"rcv\": ", g_out);
+        emit_policy(&pol, keys, mkis, k->mki ? 2 : 1);
+        fputs(", \"ops\": [", g_out);
+        g_first_item = 1;
+
+        uint8_t in[128], exp[128], out[128];
+        size_t in_len, exp_len = 0, olen;
+        srtp_err_status_t st;
+        /* RTP: protect the plaintext, then unprotect the published packet
+         * (or, with only a length published, the reference's own output) */
+        in_len = unhex(k->rtp, in);
+        olen = sizeof out;
+        st = srtp_protect(snd, in, in_len, out, &olen, 0);
+        emit_op("snd", "protect", in, in_len, in_len + 64, 0, (int)st, out,
+                olen);
+        if (st || olen != k->srtp_len)
+            kat_fail(k, "srtp_protect length");
+        if (k->srtp) {
+            exp_len = unhex(k->srtp, exp);
+            if (exp_len != olen || memcmp(exp, out, olen))
+                kat_fail(k, "srtp_protect bytes");
+        } else {
+            memcpy(exp, out, olen);
+            exp_len = olen;
+        }
+        olen = sizeof out;
+        st = srtp_unprotect(rcv, exp, exp_len, out, &olen);
+        emit_op("rcv", "unprotect", exp, exp_len, exp_len, 0, (int)st, out,
+                olen);
+        if (st || olen != in_len || memcmp(out, in, in_len))
+            kat_fail(k, "srtp_unprotect");
+        if (k->rtcp) {
+            in_len = unhex(k->rtcp, in);
+            olen = sizeof out;
+            st = srtp_protect_rtcp(snd, in, in_len, out, &olen, 0);
+            emit_op("snd", "protect_rtcp", in, in_len, in_len + 64, 0,
+                    (int)st, out, olen);
+            exp_len = unhex(k->srtcp, exp);
+            if (st || olen != k->srtcp_len || exp_len != olen ||
+                memcmp(exp, out, olen))
+                kat_fail(k, "srtp_protect_rtcp");
+            olen = sizeof out;
+            st = srtp_unprotect_rtcp(rcv, exp, exp_len, out, &olen);
+            emit_op("rcv", "unprotect_rtcp", exp, exp_len, exp_len, 0,
+                    (int)st, out, olen);
+            if (st || olen != in_len || memcmp(out, in, in_len))
+                kat_fail(k, "srtp_unprotect_rtcp");
+        }
+        fputs("\n    ]}", g_out);
+        srtp_dealloc(snd);
+        srtp_dealloc(rcv);
+    }
+    fputs("\n  ]", g_out);
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 2) {
@@ -664,7 +869,9 @@ int main(int argc, char **argv)
     gen_template_case(0, srtp_crypto_policy_set_aes_gcm_256_16_auth,
                       "template_gcm256_16");
 #endif
-    fputs("\n  ]\n}\n", g_out);
+    fputs("\n  ]", g_out);
+    gen_kats();
+    fputs("\n}\n", g_out);
     fclose(g_out);
     srtp_shutdown();
     return 0;

@@ -25,3 +25,33 @@ def all_cases():
 
 def case_ids():
     return [c["name"] for c in all_cases()]
+
+
+def kat_cases():
+    """The published packet KATs of test/srtp_driver.c (srtp_validate*,
+    srtp_test_empty_payload*), reproduced by the reference build before
+    oracle/gen_golden.c emits them."""
+    out = []
+    for f in ("ref_int.json", "ref_ossl.json"):
+        out += load(f)["kats"]
+    return out
+
+
+def replay_ops(case, snd, rcv):
+    """Runs a case's op rows on two session objects exposing protect /
+    unprotect / protect_rtcp / unprotect_rtcp; asserts status and bytes."""
+    H = bytes.fromhex
+    for i, op in enumerate(case["ops"]):
+        s = snd if op["sess"] == "snd" else rcv
+        kind = op["op"]
+        if kind == "protect":
+            st, out = s.protect(H(op["in"]), op["cap"], op["mki_index"])
+        elif kind == "protect_rtcp":
+            st, out = s.protect_rtcp(H(op["in"]), op["cap"], op["mki_index"])
+        elif kind == "unprotect":
+            st, out = s.unprotect(H(op["in"]), op["cap"])
+        else:
+            st, out = s.unprotect_rtcp(H(op["in"]), op["cap"])
+        assert st == op["status"], (case["name"], i, kind, st, op["status"])
+        if st == 0:
+            assert out.hex() == op["out"], (case["name"], i, kind)

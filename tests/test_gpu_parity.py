@@ -9,7 +9,7 @@ import pytest
 
 import libsrtp_amd as L
 from oracle import pyoracle as O
-from tests.golden_util import all_cases, case_ids
+from tests.golden_util import all_cases, case_ids, kat_cases, replay_ops
 
 pytestmark = pytest.mark.gpu
 H = bytes.fromhex
@@ -66,6 +66,28 @@ def test_golden_batched(case):
             if st[k] == 0:
                 assert out[k].hex() == o["out"], (i + k, o["op"])
         i = j
+
+
+@pytest.mark.parametrize("case", kat_cases(), ids=[c["name"] for c in kat_cases()])
+def test_published_kats(case):
+    """test/srtp_driver.c's published packets (srtp_validate*, empty
+    payload), RTP and RTCP, through the single-packet C ABI."""
+    _gpu()
+    replay_ops(case, L.Session([case["snd"]]), L.Session([case["rcv"]]))
+
+
+@pytest.mark.parametrize("case", kat_cases(), ids=[c["name"] for c in kat_cases()])
+def test_published_kats_batched(case):
+    _gpu()
+    snd, rcv = L.Session([case["snd"]]), L.Session([case["rcv"]])
+    for op in case["ops"]:
+        s = snd if op["sess"] == "snd" else rcv
+        fn = {"protect": s.protect_batch, "unprotect": s.unprotect_batch,
+              "protect_rtcp": s.protect_rtcp_batch,
+              "unprotect_rtcp": s.unprotect_rtcp_batch}[op["op"]]
+        st, out = fn([H(op["in"])], [op["cap"]])
+        assert st[0] == op["status"], (case["name"], op["op"])
+        assert out[0].hex() == op["out"], (case["name"], op["op"])
 
 
 # --------------------------------------------------------------------------
