@@ -370,11 +370,20 @@ double srtp_mi355x_last_kernel_ms(srtp_t ctx);
  * their usage limit -- DESIGN.md "Device pre-pass") */
 void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
                                uint64_t *host_batches);
+/* device pre-pass batches of more than one stream that could not use the
+ * order-free form (a stream with more packets in the batch than its replay
+ * window, a gap of 2^15 or more) and ran the sorted chain path */
+uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx);
 /* why the most recent srtp_protect_device fallback left the device
  * pre-pass (0: none so far): 1 unknown SSRC (template clone), 2 stream with MKI / pending ROC
  * / receiver direction, 4 sequence number not advancing by 1..2^15-1,
  * 64 empty session, 128 a key near its usage limit */
 int srtp_mi355x_prepass_last_abort(srtp_t ctx);
+/* of the most recent unprotect batch (host-buffer or device API): post-pass
+ * rounds, crypto launches and restore (undo) launches.  Rounds stay small
+ * under forged traffic: see srtp_host.c unprotect_core. */
+void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
+                                 uint32_t *launches, uint32_t *undo_launches);
 /* 1 when a HIP device is usable from this process */
 int srtp_mi355x_gpu_available(void);
 

@@ -167,13 +167,15 @@ typedef struct srtp_gpu_pp_batch {
     void *stream;
     uint32_t uniform_key;   /* as srtp_gpu_batch_t */
     uint32_t mask;
+    int sorted;             /* out: the sorted chain path ran (not the
+                               order-free form) */
 } srtp_gpu_pp_batch_t;
 
 /* pre-pass + crypto for protect.  *fallback != 0: nothing was written (no
  * packet, status or stream state) and the batch must take the host path;
  * the value is the abort reason: 1 unknown SSRC, 2 ineligible stream,
  * 4 sequence outside the chain domain (bits may combine). */
-int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback);
 
 /* plumbing between the two HIP translation units */

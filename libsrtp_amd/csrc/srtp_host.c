@@ -18,7 +18,13 @@
  * in order with the real authentication results (srtp.c:2994-3167), and
  * re-runs ("redo") any packet whose index estimate changed because an
  * earlier packet failed.  Outputs and statuses are therefore identical to
- * calling the reference once per packet.
+ * calling the reference once per packet.  Redo rounds are bounded: results
+ * are kept per (packet, index), forged packets stop being speculated as
+ * accepted, and after UNP_SPEC_ROUNDS the residue runs in exact rounds
+ * (one unresolved packet per SSRC per launch).  Packets that end with an
+ * error have their speculative decryption undone, so the buffer of a
+ * rejected packet holds its ciphertext, as with the reference (which
+ * verifies before decrypting).
  */
 #include "srtp_mi355x.h"
 
@@ -156,6 +162,7 @@ typedef struct {
     uint64_t uses_bound;    /* packets run on the device since the upload  */
     uint32_t uniform, mask;
     uint64_t fast_batches, host_batches;
+    uint64_t sorted_batches; /* fast batches that needed the sorted path  */
     int last_abort;         /* reason of the most recent fallback         */
 } devtab_t;
 
@@ -172,6 +179,9 @@ struct srtp_ctx_t_ {
     uint32_t variant_mask;
     stage_t st;
     uint64_t epoch;
+    struct {
+        uint32_t rounds, launches, undo_launches;
+    } ustat; /* of the most recent unprotect batch */
     int timing;
     double last_ms;
     devtab_t dt;
@@ -1272,12 +1282,67 @@ static srtp_err_status_t pre_protect(srtp_t ctx, const pkt_sum_t *s,
  * unprotect pre-pass (speculative) and post-pass (exact, in order)
  * ---------------------------------------------------------------------- */
 typedef struct {
-    srtp_err_status_t sverdict; /* state-independent verdict              */
-    uint64_t est;               /* speculative estimate sent to the GPU    */
-    int gpu;                    /* crypto was run for this packet          */
-    int redo;
-    hkey_t *key;
+    srtp_err_status_t sverdict; /* state-independent verdict (this round)  */
+    uint64_t est;               /* index the crypto last ran at            */
+    int gpu;                    /* the crypto has run (at est)             */
+    int auth;                   /* ... and authenticated                   */
+    int failed;                 /* authentication failed at some index     */
+    int dirty;                  /* output = input ^ keystream of `dm`      */
+    hkey_t *key;                /* key of the last run                     */
+    srtp_dev_meta_t dm;         /* meta of the last run                    */
 } upkt_t;
+
+/* how the pre-pass treats a packet whose crypto has not run at its
+ * speculated index */
+enum {
+    UNP_OPTIMISTIC = 0, /* accepted, unless it already failed elsewhere */
+    UNP_CAUTIOUS = 1,   /* not accepted                                  */
+    UNP_EXACT = 2       /* runs alone: later packets of its SSRC wait     */
+};
+#define UNP_SPEC_ROUNDS 4
+
+/* SSRC set with O(1) generation clear (redo / exact-round blocking) */
+typedef struct {
+    uint32_t *k, *gen_of;
+    size_t cap;
+    uint32_t gen;
+} sset_t;
+
+static int sset_init(sset_t *t, size_t n)
+{
+    t->cap = 16;
+    while (t->cap < 2 * n)
+        t->cap *= 2;
+    t->k = (uint32_t *)malloc(t->cap * 4);
+    t->gen_of = (uint32_t *)calloc(t->cap, 4);
+    t->gen = 1;
+    return t->k && t->gen_of ? 0 : -1;
+}
+
+static void sset_free(sset_t *t)
+{
+    free(t->k);
+    free(t->gen_of);
+}
+
+static int sset_has(const sset_t *t, uint32_t x)
+{
+    for (size_t h = map_hash(x, t->cap); t->gen_of[h] == t->gen;
+         h = (h + 1) & (t->cap - 1))
+        if (t->k[h] == x)
+            return 1;
+    return 0;
+}
+
+static void sset_add(sset_t *t, uint32_t x)
+{
+    size_t h = map_hash(x, t->cap);
+    for (; t->gen_of[h] == t->gen; h = (h + 1) & (t->cap - 1))
+        if (t->k[h] == x)
+            return;
+    t->gen_of[h] = t->gen;
+    t->k[h] = x;
+}
 
 /* per-batch provisional streams (unknown SSRC + template) */
 typedef struct {
@@ -1374,16 +1439,20 @@ static srtp_err_status_t un_static(const srtp_stream_ctx_t *st,
     return srtp_err_status_ok;
 }
 
-/* speculative pre-pass for packet s; returns 1 if the GPU must run it */
+/* speculative pre-pass for packet s; returns 1 if the GPU must run it.
+ * `blk` holds the SSRCs an exact round has already given a packet to. */
 static int pre_unprotect(srtp_t ctx, provset_t *ps, const pkt_sum_t *s,
                          size_t cap, const uint8_t *mki_bytes, upkt_t *u,
-                         srtp_dev_meta_t *meta)
+                         srtp_dev_meta_t *meta, int mode, sset_t *blk)
 {
-    memset(u, 0, sizeof *u);
     if (s->err) {
         u->sverdict = (srtp_err_status_t)s->err;
         return 0;
     }
+    /* (sverdict is state-independent: a value from an earlier round stays
+     * valid; one never computed is 0 and makes the post-pass redo) */
+    if (mode == UNP_EXACT && sset_has(blk, s->ssrc))
+        return 0; /* waits for the earlier packet of its SSRC */
     srtp_stream_ctx_t *st = map_get(ctx, s->ssrc);
     rdbx_t *r = NULL;
     const srtp_stream_ctx_t *kst = st;
@@ -1419,27 +1488,40 @@ static int pre_unprotect(srtp_t ctx, provset_t *ps, const pkt_sum_t *s,
         if (!adv && rdbx_check(r, delta))
             return 0; /* speculatively a replay; the post-pass decides */
     }
-    u->est = est;
-    u->sverdict = un_static(kst, s, cap, mki_bytes, &u->key, meta);
+    hkey_t *k = NULL;
+    u->sverdict = un_static(kst, s, cap, mki_bytes, &k, meta);
     if (u->sverdict)
         return 0;
     meta->roc = (uint32_t)(est >> 16);
-    /* speculate success */
-    if (pv && !pv->created) {
-        pv->created = 1;
-        rdbx_add(&pv->r, delta);
-    } else if (r) {
-        rdbx_accept(r, est, delta, adv);
+    const int known = u->gpu && u->est == est;
+    int accept, run = 0;
+    if (known) {
+        accept = u->auth; /* result already in hand at this index */
+    } else {
+        run = 1;
+        accept = mode == UNP_OPTIMISTIC && !u->failed;
+        if (mode == UNP_EXACT)
+            sset_add(blk, s->ssrc);
+        u->est = est;
+        u->key = k;
     }
-    u->gpu = 1;
-    return 1;
+    if (accept) {
+        if (pv && !pv->created) {
+            pv->created = 1;
+            rdbx_add(&pv->r, delta);
+        } else if (r) {
+            rdbx_accept(r, est, delta, adv);
+        }
+    }
+    return run;
 }
 
 /* exact post-pass for one packet, in batch order.  Returns the final status
  * or -1 when the packet must be re-run (its index changed). */
 static int post_unprotect(srtp_t ctx, const pkt_sum_t *s, upkt_t *u,
-                          int auth_ok, size_t *out_len)
+                          size_t *out_len)
 {
+    const int auth_ok = u->auth;
     if (s->err)
         return s->err;
     srtp_stream_ctx_t *st = map_get(ctx, s->ssrc);
@@ -1670,6 +1752,31 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
     return ret;
 }
 
+/* XORs the keystream of each flagged packet's last run back over its
+ * output (CTR: that restores the ciphertext) */
+static int undo_runs(srtp_t ctx, size_t n, const size_t *list, size_t nl,
+                     upkt_t *u, uint8_t *d_out, const uint64_t *d_out_off,
+                     void *stream)
+{
+    stage_t *sg = &ctx->st;
+    size_t k = 0;
+    for (size_t i = 0; i < n; i++)
+        sg->h_meta[i].info = 0xff0000u;
+    for (size_t j = 0; j < nl; j++) {
+        size_t i = list[j];
+        sg->h_meta[i] = u[i].dm;
+        u[i].dirty = 0;
+        k++;
+    }
+    if (!k)
+        return 0;
+    ctx->ustat.undo_launches++;
+    return srtp_gpu_h2d(ctx->gpu, sg->d_meta, sg->h_meta,
+                        n * sizeof *sg->h_meta, stream) ||
+           srtp_gpu_undo(ctx->gpu, n, d_out, d_out_off, sg->d_meta, stream) ||
+           srtp_gpu_sync(ctx->gpu, stream);
+}
+
 static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
                                         const pkt_sum_t *sum, const size_t *cap,
                                         const uint8_t *const *mki_ptr,
@@ -1681,105 +1788,124 @@ static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
                                         size_t *olen, void *stream)
 {
     stage_t *sg = &ctx->st;
+    const int inplace = d_out == d_in;
     upkt_t *u = (upkt_t *)calloc(n, sizeof(upkt_t));
-    int *pending = (int *)malloc(n * sizeof(int));
-    if (!u || !pending) {
+    size_t *pend = (size_t *)malloc(n * sizeof(size_t));
+    size_t *aux = (size_t *)malloc(n * sizeof(size_t));
+    sset_t blk, redo;
+    memset(&blk, 0, sizeof blk);
+    memset(&redo, 0, sizeof redo);
+    if (!u || !pend || !aux || sset_init(&blk, n) || sset_init(&redo, n)) {
         free(u);
-        free(pending);
+        free(pend);
+        free(aux);
+        sset_free(&blk);
+        sset_free(&redo);
         return srtp_err_status_alloc_fail;
     }
     for (size_t i = 0; i < n; i++)
-        pending[i] = 1;
+        pend[i] = i;
     size_t npend = n;
     srtp_err_status_t ret = srtp_err_status_ok;
-    while (npend) {
+    memset(&ctx->ustat, 0, sizeof ctx->ustat);
+    for (int round = 0; npend; round++) {
+        const int mode = round < 2                 ? UNP_OPTIMISTIC
+                         : round < UNP_SPEC_ROUNDS ? UNP_CAUTIOUS
+                                                   : UNP_EXACT;
         provset_t ps;
         memset(&ps, 0, sizeof ps);
         ctx->epoch++;
-        for (size_t i = 0; i < n; i++) {
-            srtp_dev_meta_t *m = &sg->h_meta[i];
-            memset(m, 0, sizeof *m);
-            m->info = 0xff0000u; /* skip */
-            if (!pending[i])
-                continue;
+        blk.gen++;
+        for (size_t i = 0; i < n; i++)
+            sg->h_meta[i].info = 0xff0000u; /* skip */
+        size_t nrun = 0, nre = 0;
+        for (size_t j = 0; j < npend; j++) {
+            size_t i = pend[j];
+            srtp_dev_meta_t m;
+            memset(&m, 0, sizeof m);
             if (pre_unprotect(ctx, &ps, &sum[i], cap[i],
-                              mki_ptr ? mki_ptr[i] : NULL, &u[i], m))
-                m->info &= ~0xff0000u;
-            else
-                m->info |= 0xff0000u;
+                              mki_ptr ? mki_ptr[i] : NULL, &u[i], &m, mode,
+                              &blk)) {
+                sg->h_meta[i] = m;
+                if (inplace && u[i].dirty)
+                    aux[nre++] = i; /* restore before it runs again */
+                nrun++;
+            }
         }
         provset_free(&ps);
-        if (run_gpu(ctx, 1, n, d_in, d_in_off, d_out, d_out_off, sg->h_meta,
-                    stream) ||
-            srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, n, stream) ||
-            srtp_gpu_sync(ctx->gpu, stream)) {
-            log_msg(srtp_log_level_error, srtp_gpu_last_error());
-            ret = srtp_err_status_fail;
-            break;
-        }
-        /* exact in-order post-pass; a packet whose estimate moved is re-run
-         * together with every later packet of its SSRC */
-        uint32_t *redo_ssrc = NULL;
-        size_t nredo = 0, redo_cap = 0;
-        size_t again = 0;
-        for (size_t i = 0; i < n; i++) {
-            if (!pending[i])
-                continue;
-            int blocked = 0;
-            for (size_t r = 0; r < nredo; r++)
-                if (redo_ssrc[r] == sum[i].ssrc && !sum[i].err) {
-                    blocked = 1;
-                    break;
-                }
-            if (blocked) {
-                again++;
-                continue;
+        if (nre) {
+            /* undo_runs() rewrites h_meta: keep this round's metas aside */
+            srtp_dev_meta_t *keep =
+                (srtp_dev_meta_t *)malloc(n * sizeof *keep);
+            if (!keep) {
+                ret = srtp_err_status_alloc_fail;
+                break;
             }
-            int auth = u[i].gpu ? sg->h_auth[i] : 0;
-            int rc = post_unprotect(ctx, &sum[i], &u[i], auth, &olen[i]);
-            if (rc < 0) {
-                if (nredo == redo_cap) {
-                    redo_cap = redo_cap ? 2 * redo_cap : 8;
-                    redo_ssrc = (uint32_t *)realloc(redo_ssrc, redo_cap * 4);
-                }
-                redo_ssrc[nredo++] = sum[i].ssrc;
-                again++;
-                continue;
-            }
-            status[i] = (srtp_err_status_t)rc;
-            pending[i] = 0;
-        }
-        free(redo_ssrc);
-        npend = again;
-        if (npend) {
-            /* packets still pending that ran speculatively were decrypted
-             * in place under their speculative index: restore them */
-            size_t nundo = 0;
-            for (size_t i = 0; i < n; i++) {
-                srtp_dev_meta_t *m = &sg->h_meta[i];
-                if (pending[i] && u[i].gpu) {
-                    nundo++;
-                } else {
-                    m->info |= 0xff0000u;
-                }
-            }
-            if (nundo && d_out != d_in) {
-                /* out of place: the input is intact, nothing to restore */
-                nundo = 0;
-            }
-            if (nundo &&
-                (srtp_gpu_h2d(ctx->gpu, sg->d_meta, sg->h_meta,
-                              n * sizeof *sg->h_meta, stream) ||
-                 srtp_gpu_undo(ctx->gpu, n, d_out, d_out_off, sg->d_meta,
-                               stream) ||
-                 srtp_gpu_sync(ctx->gpu, stream))) {
+            memcpy(keep, sg->h_meta, n * sizeof *keep);
+            int bad = undo_runs(ctx, n, aux, nre, u, d_out, d_out_off, stream);
+            memcpy(sg->h_meta, keep, n * sizeof *keep);
+            free(keep);
+            if (bad) {
                 ret = srtp_err_status_fail;
                 break;
             }
         }
+        if (nrun) {
+            ctx->ustat.launches++;
+            if (run_gpu(ctx, 1, n, d_in, d_in_off, d_out, d_out_off,
+                        sg->h_meta, stream) ||
+                srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, n, stream) ||
+                srtp_gpu_sync(ctx->gpu, stream)) {
+                log_msg(srtp_log_level_error, srtp_gpu_last_error());
+                ret = srtp_err_status_fail;
+                break;
+            }
+            for (size_t j = 0; j < npend; j++) {
+                size_t i = pend[j];
+                if (SRTP_META_STATUS(sg->h_meta[i].info))
+                    continue;
+                u[i].gpu = 1;
+                u[i].auth = sg->h_auth[i] != 0;
+                u[i].failed |= !u[i].auth;
+                u[i].dirty = 1;
+                u[i].dm = sg->h_meta[i];
+            }
+        }
+        /* exact in-order post-pass; a packet whose estimate moved is re-run
+         * together with every later packet of its SSRC */
+        redo.gen++;
+        size_t again = 0;
+        for (size_t j = 0; j < npend; j++) {
+            size_t i = pend[j];
+            if (!sum[i].err && sset_has(&redo, sum[i].ssrc)) {
+                pend[again++] = i;
+                continue;
+            }
+            int rc = post_unprotect(ctx, &sum[i], &u[i], &olen[i]);
+            if (rc < 0) {
+                sset_add(&redo, sum[i].ssrc);
+                pend[again++] = i;
+                continue;
+            }
+            status[i] = (srtp_err_status_t)rc;
+        }
+        npend = again;
+        ctx->ustat.rounds = (uint32_t)round + 1;
+    }
+    /* rejected packets whose speculative decryption reached the output */
+    if (!ret) {
+        size_t nb = 0;
+        for (size_t i = 0; i < n; i++)
+            if (u[i].dirty && status[i] != srtp_err_status_ok)
+                aux[nb++] = i;
+        if (undo_runs(ctx, n, aux, nb, u, d_out, d_out_off, stream))
+            ret = srtp_err_status_fail;
     }
     free(u);
-    free(pending);
+    free(pend);
+    free(aux);
+    sset_free(&blk);
+    sset_free(&redo);
     return ret;
 }
 
@@ -2078,6 +2204,7 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     }
     if (ctx->timing)
         ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
+    dt->sorted_batches += pb.sorted;
     dt->uses_bound += b->n;
     dt->dirty = 1;
     return 1;
@@ -2867,6 +2994,24 @@ void srtp_mi355x_set_timing(srtp_t ctx, int on)
 double srtp_mi355x_last_kernel_ms(srtp_t ctx) { return ctx ? ctx->last_ms : 0; }
 
 int srtp_mi355x_gpu_available(void) { return srtp_gpu_available(); }
+
+void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
+                                 uint32_t *launches, uint32_t *undo_launches)
+{
+    if (!ctx)
+        return;
+    if (rounds)
+        *rounds = ctx->ustat.rounds;
+    if (launches)
+        *launches = ctx->ustat.launches;
+    if (undo_launches)
+        *undo_launches = ctx->ustat.undo_launches;
+}
+
+uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx)
+{
+    return ctx ? ctx->dt.sorted_batches : 0;
+}
 
 int srtp_mi355x_prepass_last_abort(srtp_t ctx)
 {

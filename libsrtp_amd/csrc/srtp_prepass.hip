@@ -12,7 +12,24 @@
 //   -> segmented inclusive scan of advances (first packet: the exact
 //      estimate from the stream's stored index)  -> replay window update
 //   -> commit (meta, status, out_len, stream state)
-// and every packet's result equals the sequential reference's.  Anything
+// and every packet's result equals the sequential reference's.
+//
+// Many streams (ns > 1, e.g. BASELINE configs[3]: 64k SSRCs) take an
+// order-free form first: every chain packet's index is guessed from its
+// stream's STORED index (index_guess).  When, per stream, every index of
+// the batch is above the stored one and within one replay window of the
+// batch's highest (hi - est < window bits <= 2^15), the reference's
+// in-order walk accepts every packet at exactly that guess (each running
+// top is the stored index or a batch index less than a window away, so
+// each guess is the same, and no packet is ever "old"), whatever the
+// packets' order -- unless two share an index, which the window bitmap
+// catches (atomicOr sees the bit set).  Then the new state is index = hi,
+// window = old window shifted by hi - stored plus one bit per packet, and
+// the whole pre-pass is classify (with the per-stream max and packet
+// count, wave-aggregated) -> window shift -> set bits -> commit: no sort.
+// A batch outside that condition (AB_ORDER: a stream with more packets
+// than its window, or an index at or below the stored one) is re-run
+// through the sorted chain path.  Anything
 // outside the condition (unknown SSRC needing a template clone, a stream
 // with MKI / pending ROC / receiver direction, a non-advancing sequence)
 // raises the abort word: nothing is committed, the crypto kernels exit,
@@ -37,7 +54,8 @@ constexpr uint32_t ST_BAD_PARAM = 2, ST_CIPHER_FAIL = 8, ST_PARSE_ERR = 21,
 constexpr uint32_t NOCHAIN = 0xffffffffu;
 
 // abort reasons (bits of the abort word; any bit -> host path)
-enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4 };
+enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4,
+       AB_ORDER = 8 /* order-free form does not apply: sorted path */ };
 
 struct PpState {
     // stream table
@@ -83,15 +101,134 @@ struct ClassifyArgs {
     uint32_t n;
     srtp_dev_hdr_t *hdr;
     uint32_t *pstat, *skey, *perm, *bcount, *abort;
+    // order-free form only (null otherwise): per-packet index guessed from
+    // the stored index, per-stream highest index
+    uint64_t *est;
+    unsigned long long *new_index;
 };
+
+// index_guess against a stream's stored index (srtp_host.c estimate /
+// index_guess = rdbx.c:112-145, 280-299); returns delta
+__device__ __forceinline__ int64_t guess_index(uint64_t idx, uint32_t seq,
+                                               uint64_t *est)
+{
+    if (idx > SEQ_MEDIAN) {
+        const uint32_t lroc = (uint32_t)(idx >> 16);
+        const uint32_t lseq = (uint32_t)(idx & 0xffffu);
+        uint32_t roc = lroc;
+        int64_t diff = (int64_t)seq - (int64_t)lseq;
+        if (lseq < SEQ_MEDIAN) {
+            if ((int)seq - (int)lseq > (int)SEQ_MEDIAN) {
+                roc = lroc - 1;
+                diff -= 65536;
+            }
+        } else if ((int)lseq - (int)SEQ_MEDIAN > (int)seq) {
+            roc = lroc + 1;
+            diff += 65536;
+        }
+        *est = ((uint64_t)roc << 16) | seq;
+        return diff;
+    }
+    *est = seq;
+    return (int64_t)seq - (int64_t)idx;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)
+{
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// per-stream packet count and highest index of the order-free form: up to
+// four streams per wave are reduced across the wave (one atomic pair each),
+// the rest of the lanes use their own atomics.  Called by every lane.
+__device__ void agg_stream(uint32_t key, uint64_t e, uint32_t *bcount,
+                           unsigned long long *new_index)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    bool done = key == NOCHAIN;
+    for (int it = 0; it < 4; it++) {
+        const uint64_t am = __ballot(!done);
+        if (!am)
+            return;
+        const uint32_t lead = (uint32_t)__shfl((int)key, __ffsll((unsigned long long)am) - 1);
+        const bool mine = !done && key == lead;
+        const uint64_t mm = __ballot(mine);
+        uint64_t v = mine ? e : 0;
+        for (int m = 1; m < 64; m <<= 1) {
+            const uint64_t o = shfl_xor64(v, m);
+            v = o > v ? o : v;
+        }
+        if (lane == (uint32_t)(__ffsll((unsigned long long)mm) - 1)) {
+            atomicAdd(&bcount[lead], (uint32_t)__popcll((unsigned long long)mm));
+            atomicMax(&new_index[lead], (unsigned long long)v);
+        }
+        done = done || mine;
+    }
+    if (!done) {
+        atomicAdd(&bcount[key], 1u);
+        atomicMax(&new_index[key], (unsigned long long)e);
+    }
+}
+
+__device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i);
 
 // parse, stream lookup, the per-packet checks of pre_protect that do not
 // depend on stream state (srtp_host.c pre_protect; srtp.c:2515-2600)
 __global__ void k_pp_classify(ClassifyArgs A)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= A.n)
+    uint32_t key = NOCHAIN;
+    uint64_t e = 0;
+    if (i < A.n) {
+        key = classify_one(A, i);
+        if (A.est && key != NOCHAIN) {
+            const uint32_t seq = A.hdr[i].seq_len & 0xffffu;
+            // at or below the stored index (a replay, or an advance the
+            // guess from the stored index cannot see): the sorted path
+            // decides
+            if (guess_index(A.st[key].index, seq, &e) < 1)
+                atomicOr(A.abort, AB_ORDER);
+            A.est[i] = e;
+        }
+    }
+    if (A.est)
+        agg_stream(key, e, A.bcount, A.new_index);
+}
+
+// order-free form: the replay bit of every chain packet (window already
+// shifted to the stream's highest index by k_pp_window)
+__global__ void k_pp_usetbits(const uint32_t *skey, const uint64_t *est,
+                              const srtp_dev_stream_t *st, uint32_t ns,
+                              uint32_t n, const uint64_t *new_index,
+                              uint32_t *wnew, uint32_t *abort)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
         return;
+    const uint32_t s = skey[i];
+    if (s >= ns)
+        return;
+    const uint64_t hi = new_index[s], e = est[i];
+    const uint32_t bits = st[s].win_bits;
+    // every running top of the in-order walk is the stored index or one of
+    // the batch's indices (all within bits <= 2^15 of each other), so each
+    // guess equals the one from the stored index
+    if (hi - e >= bits) {
+        atomicOr(abort, AB_ORDER);
+        return;
+    }
+    const uint32_t bit = bits - 1 - (uint32_t)(hi - e);
+    const uint32_t m = 1u << (bit & 31);
+    if (atomicOr(&wnew[st[s].win_off + (bit >> 5)], m) & m)
+        atomicOr(abort, AB_SEQUENCE);   // two packets with one index: host
+}
+
+// one packet of k_pp_classify: header, stream, status code; returns the
+// chain key (stream id) or NOCHAIN
+__device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i)
+{
     const uint64_t off = A.in_off[i];
     const uint32_t len = A.in_len[i];
     const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
@@ -140,6 +277,7 @@ __global__ void k_pp_classify(ClassifyArgs A)
     }
     A.pstat[i] = code;
     A.skey[i] = key;
+    return key;
 }
 
 // One stream (the common case of a single-session sender): the stable sort
@@ -524,10 +662,11 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
     return 0;
 }
 
-int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback)
 {
     *fallback = 1;
+    b->sorted = 0;
     PpState *P = pp_of(g);
     const size_t n = b->n;
     if (!n) {
@@ -542,6 +681,14 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     const uint32_t N = (uint32_t)n, ns = P->ns;
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
 
+    // many streams: the order-free form first (no sort); AB_ORDER -> again
+    // through the sorted chain path.  SRTP_PP_SORTED=1 forces the latter.
+    static const bool force_sorted = [] {
+        const char *e = getenv("SRTP_PP_SORTED");
+        return e && *e == '1';
+    }();
+    bool unordered = ns > 1 && !force_sorted;
+    for (;;) {
     PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
     PPCHK(hipMemsetAsync(P->bcount, 0, ns * 4ull, stream));
     PPCHK(hipMemsetAsync(P->new_index, 0, ns * 8ull, stream));
@@ -562,11 +709,25 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     C.perm = P->perm;
     C.bcount = P->bcount;
     C.abort = P->abort;
+    C.est = unordered ? P->est : nullptr;
+    C.new_index = unordered ? (unsigned long long *)P->new_index : nullptr;
     hipLaunchKernelGGL(k_pp_classify, gp, blk, 0, stream, C);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "classify"))
         return -1;
 
+    CommitArgs K;
+    if (unordered) {
+        hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
+                           P->new_index, P->win, P->wnew);
+        hipLaunchKernelGGL(k_pp_usetbits, gp, blk, 0, stream, P->skey, P->est,
+                           P->st, ns, N, P->new_index, P->wnew, P->abort);
+        PPCHK(hipGetLastError());
+        if (pp_step(stream, "usetbits"))
+            return -1;
+        K.skey2 = P->skey;   // packet order: perm is the identity
+        K.perm2 = P->perm;
+    } else {
     // stable sort by stream id; NOCHAIN keys truncate to all-ones > any sid
     int end_bit = 1;
     while ((1u << end_bit) <= ns && end_bit < 32)
@@ -611,9 +772,9 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
                        P->st, ns, N, P->new_index, P->wnew);
     if (pp_step(stream, "setbits"))
         return -1;
-    CommitArgs K;
-    K.skey2 = P->skey2;
-    K.perm2 = P->perm2;
+        K.skey2 = P->skey2;
+        K.perm2 = P->perm2;
+    }
     K.pstat = P->pstat;
     K.est = P->est;
     K.hdr = P->hdr;
@@ -652,8 +813,14 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
     PPCHK(hipMemcpyAsync(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost,
                          stream));
     PPCHK(hipStreamSynchronize(stream));
+    if (unordered && *P->h_abort == AB_ORDER) {
+        unordered = false;   // nothing was committed: the sorted path
+        continue;
+    }
+    b->sorted = !unordered;
     *fallback = (int)*P->h_abort;   // abort reason bits (AB_*), 0 = done
     return 0;
+    }
 }
 
 }   // extern "C"

@@ -147,6 +147,9 @@ def lib():
         "srtp_mi355x_prepass_stats": ([P, C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
+        "srtp_mi355x_prepass_sorted_batches": ([P], C.c_uint64),
+        "srtp_mi355x_unprotect_stats": ([P] + [C.POINTER(C.c_uint32)] * 3,
+                                        None),
 
         "srtp_get_version_string": ([], C.c_char_p),
     }
@@ -392,6 +395,17 @@ class Session:
         d, h = C.c_uint64(), C.c_uint64()
         self.L.srtp_mi355x_prepass_stats(self.h, C.byref(d), C.byref(h))
         return d.value, h.value
+
+    def prepass_sorted_batches(self):
+        """device pre-pass batches that needed the sorted chain path"""
+        return self.L.srtp_mi355x_prepass_sorted_batches(self.h)
+
+    def unprotect_stats(self):
+        """(rounds, crypto launches, undo launches) of the last unprotect
+        batch"""
+        v = [C.c_uint32() for _ in range(3)]
+        self.L.srtp_mi355x_unprotect_stats(self.h, *[C.byref(x) for x in v])
+        return tuple(x.value for x in v)
 
     def close(self):
         if self.h:

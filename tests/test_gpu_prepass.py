@@ -241,3 +241,102 @@ def test_device_api_orders_after_torch_default_stream():
         assert int((st != 0).sum()) == 0, b
         assert bool((cap == 12 + payload + 10).all()), b
     assert lib.prepass_stats() == (3, 0), lib.prepass_last_abort()
+
+
+# --------------------------------------------------------------------------
+# the order-free form of the many-stream pre-pass (no sort): packets of a
+# stream may arrive in any order inside one replay window
+
+def _interleaved(rng, ssrcs, seq0, per, shuffle_within=0, steps=(1, 1, 1, 2)):
+    """per packets per stream, streams interleaved at random; each stream's
+    sequence numbers advance by `steps`; with shuffle_within > 0 neighbouring
+    packets of one stream may be swapped (reordering inside the window)"""
+    chains = {}
+    for s in ssrcs:
+        q, seqs = seq0[s], []
+        for _ in range(per):
+            seqs.append(q & 0xffff)
+            q += rng.choice(steps)
+        if shuffle_within:
+            for k in range(len(seqs) - 1):
+                if rng.random() < shuffle_within:
+                    seqs[k], seqs[k + 1] = seqs[k + 1], seqs[k]
+        chains[s] = seqs
+        seq0[s] = q
+    order = [s for s in ssrcs for _ in range(per)]
+    rng.shuffle(order)
+    pos = {s: 0 for s in ssrcs}
+    pk = []
+    for s in order:
+        pk.append(rtp_packet(rng, s, chains[s][pos[s]], rng.choice([0, 33, 160])))
+        pos[s] += 1
+    return pk
+
+
+def _stream_set(n, name="icm128_hmac80"):
+    ssrcs = [0x20000000 + 7 * k for k in range(n)]
+    pols = [policy(name, ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    return ssrcs, L.Session(pols), O.Session(pols)
+
+
+def test_order_free_reordered_streams_stay_on_device():
+    _gpu()
+    rng = random.Random(501)
+    ssrcs, lib, orc = _stream_set(300)
+    seq0 = {s: rng.randrange(1, 0x10000) for s in ssrcs}
+    for b in range(3):
+        # <= 50 packets, advances of 1..2: every batch spans < 128 indices
+        pk = _interleaved(rng, ssrcs, seq0, 50, shuffle_within=0.2)
+        _check(lib, orc, pk, [len(p) + 16 for p in pk])
+    assert lib.prepass_stats() == (3, 0), lib.prepass_last_abort()
+    assert lib.prepass_sorted_batches() == 0
+    for s in ssrcs[::37]:
+        assert lib.get_roc(s)[1] == orc.get_roc(s)[1]
+
+
+def test_order_free_long_chain_takes_sorted_path():
+    """a stream with more packets than its 128-packet window in one batch"""
+    _gpu()
+    rng = random.Random(502)
+    ssrcs, lib, orc = _stream_set(5, "gcm128_16")
+    seq0 = {s: 0xff00 + 3 * k for k, s in enumerate(ssrcs)}
+    pk = _interleaved(rng, ssrcs, seq0, 200)
+    _check(lib, orc, pk, [len(p) + 32 for p in pk])
+    assert lib.prepass_stats() == (1, 0)
+    assert lib.prepass_sorted_batches() == 1
+
+
+def test_order_free_duplicate_goes_to_host():
+    _gpu()
+    rng = random.Random(503)
+    ssrcs, lib, orc = _stream_set(50)
+    seq0 = {s: 100 for s in ssrcs}
+    pk = _interleaved(rng, ssrcs, seq0, 20)
+    pk.insert(500, pk[17])                      # replay inside the batch
+    _check(lib, orc, pk, [len(p) + 16 for p in pk])
+    assert lib.prepass_stats() == (0, 1)
+    # and the next clean batch is back on the device
+    pk = _interleaved(rng, ssrcs, seq0, 20)
+    _check(lib, orc, pk, [len(p) + 16 for p in pk])
+    assert lib.prepass_stats() == (1, 1)
+
+
+def test_configs3_shape_64k_distinct_key_streams():
+    """BASELINE configs[3] at its own stream count: 65,536 streams with
+    distinct master keys x 160-byte payloads, packets round-robin, two
+    batches (2 and 3 packets per stream); every byte against the oracle."""
+    _gpu()
+    rng = random.Random(504)
+    ns = 65536
+    ssrcs = [0x10000000 + k for k in range(ns)]
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k) for k, s in
+            enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq0 = 0x7ff0
+    for per in (2, 3):
+        pk = [rtp_packet(rng, ssrcs[i % ns], (seq0 + i // ns) & 0xffff, 160)
+              for i in range(ns * per)]
+        _check(lib, orc, pk, [len(p) + 16 for p in pk])
+        seq0 += per
+    assert lib.prepass_stats() == (2, 0), lib.prepass_last_abort()
+    assert lib.prepass_sorted_batches() == 0
