@@ -6,11 +6,17 @@ protect, one stream (SSRC 0xcafebabe), 2^20 packets x 1400-byte payload
 (1412-byte RTP packets -> 1422-byte SRTP packets) resident in HBM.  One step
 = srtp_protect_device() over the whole batch: header parse, the in-order
 index / replay / key-limit pre-pass, and the HIP crypto kernels, in place.
-Before each step the 16-bit sequence numbers are advanced on the device (a
-new batch of packets, as a sender would produce; replay protection would
-otherwise reject a repeated index).
+Every step gets its own batch (the sender's next W+K batches: the same
+packets with the 16-bit sequence numbers advanced, as a sender would
+produce them; replay protection rejects a repeated index), all built in HBM
+before the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config icm128|gcm256|g711]
+--op unprotect: the receive side of the same workload -- the batches are
+protected (untimed) by a sender session, and one step is
+srtp_unprotect_device() over one batch, in place, on the receiver session.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+                  [--config icm128|gcm256|g711] [--op protect|unprotect]
 
 Multi-GPU: one process per GPU (torch.distributed.run, nccl = RCCL), each
 rank protects its own 2^20-packet batch of its own stream (weak scaling).
@@ -80,6 +86,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="icm128", choices=sorted(CONFIGS))
+    ap.add_argument("--op", default="protect", choices=["protect", "unprotect"])
     ap.add_argument("--packets", type=int, default=0,
                     help="override packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -126,7 +133,8 @@ def measure_traffic(a, kname):
         d = os.path.join(base, ctr)
         cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o",
                "p", "--", sys.executable, os.path.abspath(__file__),
-               "--config", a.config, "--steps", "2", "--warmup", "1",
+               "--config", a.config, "--op", a.op, "--steps", "2",
+               "--warmup", "1",
                "--no-cpu-baseline", "--traffic", "off"]
         if a.packets:
             cmd += ["--packets", str(a.packets)]
@@ -270,55 +278,68 @@ def main():
                     for k, key in enumerate(keys)]
     sess = L.Session(policies)
 
-    # packet arena in HBM: slot = roundup16(rtp_len + tag)
+    # packet arenas in HBM, one per step: slot = roundup16(rtp_len + tag)
     rtp_len = 12 + payload
     slot = (rtp_len + tag + 15) & ~15
+    nb = a.warmup + a.steps
+    if nb * n * slot > (200 << 30):
+        raise SystemExit("bench: %d batches x %d B do not fit the 200 GiB "
+                         "arena budget" % (nb, n * slot))
     g = torch.Generator(device=dev).manual_seed(0x5352545030303031 & 0x7fffffff)
-    arena = torch.randint(0, 256, (n, slot), dtype=torch.uint8, device=dev,
-                          generator=g)
-    arena[:, 0] = 0x80
-    arena[:, 1] = 96
-    arena[:, 4:8] = 0
+    base_arena = torch.randint(0, 256, (n, slot), dtype=torch.uint8,
+                               device=dev, generator=g)
+    base_arena[:, 0] = 0x80
+    base_arena[:, 1] = 96
+    base_arena[:, 4:8] = 0
     idx = torch.arange(n, dtype=torch.int64, device=dev)
     if nstreams == 1:
-        arena[:, 8:12] = torch.tensor(list(ssrc.to_bytes(4, "big")),
-                                      dtype=torch.uint8, device=dev)
+        base_arena[:, 8:12] = torch.tensor(list(ssrc.to_bytes(4, "big")),
+                                           dtype=torch.uint8, device=dev)
     else:
         pk_ssrc = base + idx % nstreams         # round-robin over streams
         for k in range(4):
-            arena[:, 8 + k] = ((pk_ssrc >> (24 - 8 * k)) & 0xff).to(torch.uint8)
+            base_arena[:, 8 + k] = ((pk_ssrc >> (24 - 8 * k)) & 0xff).to(
+                torch.uint8)
     pk_seq = idx // nstreams                     # per-stream packet number
     per_stream = (n + nstreams - 1) // nstreams
-    flat = arena.view(-1)
+    arenas = []
+    for k in range(nb):
+        ar = base_arena.clone()
+        seq = (pk_seq + 0x1234 + k * per_stream) & 0xffff
+        ar[:, 2] = (seq >> 8).to(torch.uint8)
+        ar[:, 3] = (seq & 0xff).to(torch.uint8)
+        arenas.append(ar.view(-1))
+    del base_arena
     off = torch.arange(n, dtype=torch.int64, device=dev) * slot
     in_len = torch.full((n,), rtp_len, dtype=torch.int32, device=dev)
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
+    if a.op == "unprotect":
+        # the sender's side, untimed: protect every batch in place; the
+        # receiver (`sess`) then unprotects them in order
+        snd = L.Session([dict(p, ssrc_type=1) for p in policies])
+        srtp_len = torch.empty(n, dtype=torch.int32, device=dev)
+        for ar in arenas:
+            srtp_len.fill_(slot)
+            if snd.protect_device(ar, off, in_len, ar, off, srtp_len,
+                                  status, stream=stream) != 0 or \
+                    int((status != 0).sum()):
+                raise RuntimeError("bench: protecting the receive batches")
+        snd.close()
+        in_len = srtp_len
     sess.set_timing(True)
-
-    # The sender's next batch: the same slots with the sequence numbers
-    # advanced by one batch (replay protection rejects a repeated index).
-    # The big-endian sequence bytes of every step are prepared up front, so
-    # the timed step is one 2-byte-per-packet copy plus srtp_protect_device.
-    # out_len keeps the protected lengths (<= slot) between steps: enough
-    # capacity for the next batch, so it is filled once.
-    seqb = []
-    for k in range(a.warmup + a.steps):
-        seq = (pk_seq + 0x1234 + k * per_stream) & 0xffff
-        seqb.append(torch.stack([(seq >> 8), (seq & 0xff)], 1)
-                    .to(torch.uint8).contiguous())
-    out_len.fill_(slot)
     torch.cuda.synchronize()
     k_step = [0]
+    fn = sess.protect_device if a.op == "protect" else sess.unprotect_device
 
     def step():
-        arena[:, 2:4].copy_(seqb[k_step[0]])
+        ar = arenas[k_step[0]]
         k_step[0] += 1
-        st = sess.protect_device(flat, off, in_len, flat, off, out_len,
-                                 status, stream=stream)
+        out_len.fill_(slot)
+        st = fn(ar, off, in_len, ar, off, out_len, status, stream=stream)
         if st != 0:
-            raise RuntimeError("srtp_protect_device: %s" % st)
+            raise RuntimeError("srtp_%s_device: %s" % (a.op, st))
         return sess.last_kernel_ms()
 
     dt, kms = timed_steps(step, a.steps, a.warmup, world,
@@ -329,7 +350,7 @@ def main():
     total_pk = n * a.steps * world
     value = total_pk / dt
     kernel_ms = sum(kms) / len(kms)
-    algo_bytes = n * (rtp_len + rtp_len + tag)   # read rtp + write srtp
+    algo_bytes = n * (rtp_len + rtp_len + tag)   # rtp + srtp, read + write
     achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
     if rank != 0:
         return
@@ -339,6 +360,7 @@ def main():
     out = {
         "metric": "SRTP packets/sec + payload GB/s, device-resident, "
                   "1M×1400B batch",
+        "op": a.op,
         "value": value,
         "unit": "pkt/s",
         "n_gpus": world,

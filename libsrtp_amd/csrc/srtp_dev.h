@@ -124,14 +124,22 @@ int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
                    srtp_dev_hdr_t *hdr_out, void *stream);
 
 /* ---- device pre-pass (DESIGN.md "Device pre-pass") --------------------
- * A device mirror of the session's streams lets srtp_protect_device run the
- * in-order index / replay / key-usage pre-pass on the GPU.  The host stays
- * authoritative: it uploads the table, the GPU advances it, and the host
- * pulls it back before any host-side use of stream state. */
+ * A device mirror of the session's streams lets srtp_protect_device and
+ * srtp_unprotect_device run the in-order index / replay / key-usage
+ * pre-pass on the GPU.  The host stays authoritative: it uploads the table,
+ * the GPU advances it, and the host pulls it back before any host-side use
+ * of stream state. */
 enum {
-    SRTP_DS_ELIGIBLE = 1, /* sender/unknown direction, no MKI, no pending ROC */
-    SRTP_DS_ICM_CONF = 2  /* AES-ICM encrypting: 2^16 keystream-block limit */
+    SRTP_DS_ELIGIBLE = 1,    /* protect: sender/unknown direction, no MKI,
+                                no pending ROC */
+    SRTP_DS_ICM_CONF = 2,    /* AES-ICM encrypting: 2^16 keystream blocks */
+    SRTP_DS_RX_ELIGIBLE = 4, /* unprotect: receiver/unknown direction, no
+                                MKI, no pending ROC */
+    SRTP_DS_AEAD = 8         /* AES-GCM: key usage counted before the tag
+                                check (srtp.c:2390-2406) */
 };
+/* srtp_dev_stream_t.dir: directions the device batches used the stream in */
+enum { SRTP_DIR_TX = 1, SRTP_DIR_RX = 2 };
 
 typedef struct srtp_dev_stream {
     uint32_t ssrc;
@@ -141,7 +149,7 @@ typedef struct srtp_dev_stream {
     uint32_t trailer;   /* tag + MKI bytes appended by protect               */
     uint32_t win_bits;  /* replay window bits (multiple of 32)               */
     uint32_t win_off;   /* word offset of the window in the window arena     */
-    uint32_t pad;
+    uint32_t dir;       /* SRTP_DIR_* bits set by device batches             */
     uint64_t index;     /* rdbx index (ROC << 16 | SEQ)                      */
     uint64_t uses;      /* packets charged to the key since the upload       */
 } srtp_dev_stream_t;
@@ -177,6 +185,17 @@ typedef struct srtp_gpu_pp_batch {
  * 4 sequence outside the chain domain (bits may combine). */
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback);
+
+/* pre-pass + crypto + commit for unprotect (the order-free form only: per
+ * stream every index above the stored one and within one replay window of
+ * the batch's highest, no duplicate, no MKI, no packet with a length /
+ * capacity error).  Packets failing authentication get auth_fail, leave the
+ * stream state alone and have their decryption undone.  *fallback != 0:
+ * nothing was written and the host path must run the batch (bits: 1
+ * unknown SSRC, 2 ineligible stream, 8 order / replay domain, 16 a packet
+ * with a static error). */
+int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
+                          int *fallback);
 
 /* plumbing between the two HIP translation units */
 void **srtp_gpu_pp_slot(srtp_gpu_t *g);

@@ -160,7 +160,8 @@ typedef struct {
     uint32_t nwords;
     uint64_t num_left_min;  /* over the keys of eligible streams           */
     uint64_t uses_bound;    /* packets run on the device since the upload  */
-    uint32_t uniform, mask;
+    uint32_t uniform, mask;       /* over the protect-eligible streams    */
+    uint32_t rx_uniform, rx_mask; /* over the unprotect-eligible streams  */
     uint64_t fast_batches, host_batches;
     uint64_t sorted_batches; /* fast batches that needed the sorted path  */
     int last_abort;         /* reason of the most recent fallback         */
@@ -2078,9 +2079,9 @@ static int dev_build(srtp_t ctx)
     if (!dt->sv || !dt->hs || !dt->hwin || !hk || !hv)
         goto out;
     dt->num_left_min = UINT64_MAX;
-    dt->uniform = 0xffffffffu;
-    dt->mask = 0;
-    int first = 1;
+    dt->uniform = dt->rx_uniform = 0xffffffffu;
+    dt->mask = dt->rx_mask = 0;
+    int first = 1, rx_first = 1;
     uint32_t woff = 0;
     for (uint32_t sid = 0; sid < ns; sid++) {
         srtp_stream_ctx_t *st = ctx->list[sid];
@@ -2104,8 +2105,23 @@ static int dev_build(srtp_t ctx)
             first = 0;
             dt->mask |= 1u << k->variant;
         }
+        if (!st->use_mki && st->rdbx.pending_roc == 0 &&
+            st->direction != DIR_SENDER) {
+            d->flags |= SRTP_DS_RX_ELIGIBLE;
+            if (k->num_left < dt->num_left_min)
+                dt->num_left_min = k->num_left;
+            if (rx_first)
+                dt->rx_uniform = k->slot;
+            else if (dt->rx_uniform != k->slot)
+                dt->rx_uniform = 0xffffffffu;
+            rx_first = 0;
+            dt->rx_mask |= 1u << k->variant;
+        }
         if (k->family == SRTP_DEV_ICM && (st->rtp_services & sec_serv_conf))
             d->flags |= SRTP_DS_ICM_CONF;
+        if (k->family == SRTP_DEV_GCM)
+            d->flags |= SRTP_DS_AEAD;
+        d->dir = 0;
         d->trailer = (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
         d->win_bits = (uint32_t)st->rdbx.bits;
         d->win_off = woff;
@@ -2156,11 +2172,13 @@ static void dev_pull(srtp_t ctx)
         const srtp_dev_stream_t *d = &dt->hs[sid];
         st->rdbx.index = d->index;
         memcpy(st->rdbx.w, dt->hwin + d->win_off, st->rdbx.bits / 8);
-        if (d->uses) {
-            st->keys->k[0].num_left -= d->uses;
-            if (st->direction == DIR_UNKNOWN)
-                st->direction = DIR_SENDER;
-        }
+        st->keys->k[0].num_left -= d->uses;
+        /* a device batch never used a stream against its direction (the
+         * eligibility flags), so no ssrc_collision event is due here */
+        if (st->direction == DIR_UNKNOWN && (d->dir & SRTP_DIR_TX))
+            st->direction = DIR_SENDER;
+        if (st->direction == DIR_UNKNOWN && (d->dir & SRTP_DIR_RX))
+            st->direction = DIR_RECEIVER;
     }
 }
 
@@ -2261,14 +2279,69 @@ out:
     return ret;
 }
 
+/* the device unprotect pre-pass (srtp_prepass.hip srtp_gpu_pp_unprotect);
+ * 1 done on the GPU, 0 host path, -1 device error */
+static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
+{
+    devtab_t *dt = &ctx->dt;
+    if (!ctx->n || b->n > 0x7fffffffu) {
+        dt->last_abort = 64;
+        return 0;
+    }
+    if (!dt->valid && dev_build(ctx))
+        return -1;
+    if (dt->num_left_min == UINT64_MAX ||
+        dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT) {
+        dt->last_abort = 128;
+        return 0;
+    }
+    srtp_gpu_pp_batch_t pb;
+    memset(&pb, 0, sizeof pb);
+    pb.n = b->n;
+    pb.in = b->in;
+    pb.in_off = b->in_off;
+    pb.in_len = b->in_len;
+    pb.out = b->out;
+    pb.out_off = b->out_off;
+    pb.out_len = b->out_len;
+    pb.status = b->status;
+    pb.stream = b->stream;
+    pb.uniform_key = dt->rx_uniform;
+    pb.mask = dt->rx_mask;
+    int fallback = 1;
+    srtp_gpu_set_timing(ctx->gpu, ctx->timing);
+    if (srtp_gpu_pp_unprotect(ctx->gpu, &pb, &fallback))
+        return -1;
+    if (fallback) {
+        dt->last_abort = fallback;
+        return 0;
+    }
+    if (ctx->timing)
+        ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
+    dt->uses_bound += b->n;
+    dt->dirty = 1;
+    return 1;
+}
+
 srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
                                         const srtp_device_batch_t *b)
 {
     if (!ctx || !b)
         return srtp_err_status_bad_param;
-    dev_pull(ctx);
     if (!b->n)
         return srtp_err_status_ok;
+    int fast = unprotect_device_fast(ctx, b);
+    if (fast < 0) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        return srtp_err_status_fail;
+    }
+    if (fast) {
+        ctx->dt.fast_batches++;
+        memset(&ctx->ustat, 0, sizeof ctx->ustat);
+        ctx->ustat.rounds = ctx->ustat.launches = 1;
+        return srtp_err_status_ok;
+    }
+    dev_pull(ctx);
     ctx->dt.host_batches++;
     size_t n = b->n;
     pkt_sum_t *sum = (pkt_sum_t *)malloc(n * sizeof *sum);

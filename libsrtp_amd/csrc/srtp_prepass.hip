@@ -1,4 +1,5 @@
-// srtp_prepass.hip -- the protect pre-pass of srtp_protect_device on the GPU.
+// srtp_prepass.hip -- the pre-passes of srtp_protect_device and
+// srtp_unprotect_device on the GPU (unprotect: see k_pu_classify below).
 //
 // The host pre-pass (srtp_host.c pre_protect, following srtp/srtp.c:
 // 2493-2712 and 2088-2233) walks the batch in order: stream lookup, key
@@ -55,7 +56,8 @@ constexpr uint32_t NOCHAIN = 0xffffffffu;
 
 // abort reasons (bits of the abort word; any bit -> host path)
 enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4,
-       AB_ORDER = 8 /* order-free form does not apply: sorted path */ };
+       AB_ORDER = 8, /* order-free form does not apply: sorted path */
+       AB_STATIC = 16 /* unprotect: a packet with a length/capacity error */ };
 
 struct PpState {
     // stream table
@@ -76,6 +78,10 @@ struct PpState {
              *perm2 = nullptr;
     uint64_t *val = nullptr, *est = nullptr;
     srtp_dev_meta_t *meta = nullptr;
+    uint8_t *auth = nullptr;        // unprotect: tag verdict per packet
+    uint64_t *top = nullptr;        // unprotect chain: highest accepted before
+    uint32_t *bcount2 = nullptr;    // unprotect: authenticated per stream
+    uint64_t *new_index2 = nullptr; // unprotect: highest authenticated
     void *cub = nullptr;
     size_t cub_bytes = 0;
     uint32_t *abort = nullptr;      // device word
@@ -254,7 +260,7 @@ __device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i)
             atomicOr(A.abort, AB_UNKNOWN_SSRC);   // template clone: host
         } else {
             const srtp_dev_stream_t &S = A.st[sid];
-            if (!(S.flags & SRTP_DS_ELIGIBLE))
+            if (!(S.flags & SRTP_DS_ELIGIBLE) || (S.dir & SRTP_DIR_RX))
                 atomicOr(A.abort, AB_INELIGIBLE);
             // key usage (key.c:74) of packets that leave the chain here;
             // chain packets are counted per stream from the sorted segment
@@ -469,9 +475,240 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
     if (s >= ns || *abort)
         return;
     st[s].uses += bcount[s];
+    if (bcount[s])
+        st[s].dir |= SRTP_DIR_TX;
     const uint64_t ni = new_index[s];
     if (ni == 0)
         return;
+    st[s].index = ni;
+    const uint32_t off = st[s].win_off, words = st[s].win_bits >> 5;
+    for (uint32_t w = 0; w < words; w++)
+        win[off + w] = wnew[off + w];
+}
+
+// ---------------------------------------------------------------------------
+// Unprotect (srtp_unprotect_device): the order-free form of the receive
+// pre-pass (srtp.c:2820-3172, srtp_host.c pre_unprotect / post_unprotect).
+// Candidates are packets whose stream is known and eligible, whose index
+// (guessed from the stored index) is above it, and that pass every length
+// check; a packet failing a length check aborts the batch to the host (its
+// status would depend on the replay check, srtp.c:2905-2990).  After the
+// crypto kernel has verified the tags, only authenticated packets move the
+// replay window and index (rdbx_add after the tag check, srtp.c:3157-3167).
+
+__device__ __forceinline__ uint32_t lookup_sid(const uint32_t *hkey,
+                                               const uint32_t *hval,
+                                               uint32_t hmask, uint32_t ssrc)
+{
+    uint32_t p = map_hash(ssrc, hmask);
+    for (uint32_t probe = 0; probe <= hmask; probe++) {
+        const uint32_t v = hval[p];
+        if (v == NOCHAIN)
+            return NOCHAIN;
+        if (hkey[p] == ssrc)
+            return v;
+        p = (p + 1) & hmask;
+    }
+    return NOCHAIN;
+}
+
+__global__ void k_pu_classify(ClassifyArgs A)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t key = NOCHAIN;
+    uint64_t e = 0;
+    if (i < A.n) {
+        const uint64_t off = A.in_off[i];
+        const uint32_t len = A.in_len[i];
+        const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
+        A.hdr[i] = h;
+        A.perm[i] = i;
+        uint32_t code = 0;
+        if (h.enc_start >> 24) {
+            code = h.enc_start >> 24;   // header does not parse: no stream
+        } else {
+            const uint32_t sid = lookup_sid(A.hkey, A.hval, A.hmask, h.ssrc);
+            if (sid == NOCHAIN) {
+                atomicOr(A.abort, AB_UNKNOWN_SSRC);   // template clone: host
+            } else {
+                const srtp_dev_stream_t &S = A.st[sid];
+                const uint32_t tag = S.trailer;       // no MKI on this path
+                if (!(S.flags & SRTP_DS_RX_ELIGIBLE) || (S.dir & SRTP_DIR_TX))
+                    atomicOr(A.abort, AB_INELIGIBLE);
+                // srtp_host.c un_static (srtp.c:2905-2990, 2298-2352)
+                if (len < tag || h.enc_start > len - tag ||
+                    ((S.flags & SRTP_DS_AEAD) && len - h.enc_start < tag) ||
+                    A.cap[i] < len - tag ||
+                    ((S.flags & SRTP_DS_ICM_CONF) &&
+                     (len - tag - h.enc_start + 15) / 16 > 0xffffu)) {
+                    atomicOr(A.abort, AB_STATIC);
+                } else {
+                    key = sid;
+                    if (A.est) {   // order-free form
+                        const uint32_t seq = h.seq_len & 0xffffu;
+                        if (guess_index(S.index, seq, &e) < 1)
+                            atomicOr(A.abort, AB_ORDER);
+                        A.est[i] = e;
+                    }
+                }
+            }
+        }
+        A.pstat[i] = code;
+        A.skey[i] = key;
+    }
+    if (A.est)
+        agg_stream(key, e, A.bcount, A.new_index);
+}
+
+// The kernels below walk position k of an order: the packet order itself
+// for the order-free form (perm = identity, est per packet), or the stable
+// stream-sorted order of the chain form (perm2, est per sorted position).
+
+// meta of every candidate for the crypto kernel (all others skipped); on an
+// abort every packet is skipped, so the undo pass after the crypto is a
+// no-op too
+__global__ void k_pu_meta(const uint32_t *skey, const uint32_t *perm,
+                          const uint64_t *est, const srtp_dev_hdr_t *hdr,
+                          const srtp_dev_stream_t *st, uint32_t ns, uint32_t n,
+                          const uint32_t *abort, srtp_dev_meta_t *meta,
+                          uint8_t *auth)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint32_t i = perm[k];
+    srtp_dev_meta_t m;
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;
+    const uint32_t s = skey[k];
+    if (!*abort && s < ns) {
+        const srtp_dev_stream_t &S = st[s];
+        const srtp_dev_hdr_t h = hdr[i];
+        m.key = S.key;
+        m.roc = (uint32_t)(est[k] >> 16);
+        m.info = h.enc_start | (S.variant << 24);
+        m.len = h.len - S.trailer;
+    }
+    meta[i] = m;
+    auth[i] = 1;   // kernels without a tag check leave it: accepted
+}
+
+// chain form: the reference guesses each index from the highest ACCEPTED
+// one before it (top), not from the previous packet.  top comes from an
+// exclusive max-scan of the authenticated estimates; every packet's guess
+// from its top must equal the chain's estimate (it does unless a run of
+// rejected packets spans 2^15 indices, or a fresh stream's first accepted
+// packet is preceded by rejected ones across a wrap); est > top always
+// holds (the chain increases), so no packet is old.  A mismatch sends the
+// batch to the host.
+__global__ void k_pu_accepted_est(const uint32_t *skey2, const uint32_t *perm2,
+                                  const uint64_t *est, const uint8_t *auth,
+                                  uint32_t ns, uint32_t n, uint64_t *val)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    val[k] = skey2[k] < ns && auth[perm2[k]] ? est[k] : 0;
+}
+
+__global__ void k_pu_top_check(const uint32_t *skey2, const uint32_t *perm2,
+                               const srtp_dev_hdr_t *hdr, const uint64_t *est,
+                               const uint64_t *top, const srtp_dev_stream_t *st,
+                               uint32_t ns, uint32_t n, uint32_t *abort)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n)
+        return;
+    const uint32_t s = skey2[k];
+    if (s >= ns)
+        return;
+    // top[k]: exclusive scan restarting (at 0) on each stream
+    uint64_t t = top[k];
+    if (t < st[s].index)
+        t = st[s].index;
+    uint64_t g;
+    guess_index(t, hdr[perm2[k]].seq_len & 0xffffu, &g);
+    if (g != est[k])
+        atomicOr(abort, AB_ORDER);
+}
+
+// the verdicts: status / length per packet, the authenticated packets'
+// per-stream count and highest index; the meta of authenticated packets
+// is cleared so that the undo pass restores only the rejected ones (after
+// an abort nothing is cleared: the undo restores every packet for the host)
+__global__ void k_pu_accept(const uint32_t *skey, const uint32_t *perm,
+                            const uint64_t *est, const uint32_t *pstat,
+                            const srtp_dev_hdr_t *hdr,
+                            const srtp_dev_stream_t *st, uint32_t ns,
+                            uint32_t n, const uint32_t *abort,
+                            const uint8_t *auth, srtp_dev_meta_t *meta,
+                            int32_t *status, uint32_t *out_len,
+                            uint32_t *bcount2,
+                            unsigned long long *new_index2)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = k < n && !*abort;
+    uint32_t key = NOCHAIN;
+    uint64_t e = 0;
+    if (live) {
+        const uint32_t i = perm[k];
+        const uint32_t s = skey[k];
+        if (s >= ns) {
+            status[i] = (int32_t)pstat[i];   // header errors; out_len kept
+        } else if (auth[i]) {
+            key = s;
+            e = est[k];
+            status[i] = 0;
+            out_len[i] = hdr[i].len - st[s].trailer;
+            meta[i].info = 0xff0000u;        // keep: nothing to undo
+        } else {
+            status[i] = 7;                   // srtp_err_status_auth_fail
+        }
+    }
+    agg_stream(key, e, bcount2, new_index2);
+}
+
+// the authenticated packets' replay bits still inside the window shifted
+// to their highest index
+__global__ void k_pu_setbits(const uint32_t *skey, const uint32_t *perm,
+                             const uint64_t *est, const srtp_dev_stream_t *st,
+                             uint32_t ns, uint32_t n, const uint32_t *abort,
+                             const uint8_t *auth, const uint64_t *new_index2,
+                             uint32_t *wnew)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || *abort)
+        return;
+    const uint32_t s = skey[k];
+    if (s >= ns || !auth[perm[k]])
+        return;
+    const uint32_t bits = st[s].win_bits;
+    const uint64_t dist = new_index2[s] - est[k];
+    if (dist < bits) {
+        const uint32_t bit = bits - 1 - (uint32_t)dist;
+        atomicOr(&wnew[st[s].win_off + (bit >> 5)], 1u << (bit & 31));
+    }
+}
+
+__global__ void k_pu_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
+                                   const uint64_t *new_index2,
+                                   const uint32_t *bcount,
+                                   const uint32_t *bcount2,
+                                   const uint32_t *wnew, uint32_t *win,
+                                   const uint32_t *abort)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns || *abort)
+        return;
+    // key usage: AES-GCM counts every packet that reached the tag check
+    // (srtp_unprotect_aead), AES-ICM / HMAC the authenticated ones
+    st[s].uses += (st[s].flags & SRTP_DS_AEAD) ? bcount[s] : bcount2[s];
+    const uint64_t ni = new_index2[s];
+    if (ni == 0)
+        return;
+    st[s].dir |= SRTP_DIR_RX;
     st[s].index = ni;
     const uint32_t off = st[s].win_off, words = st[s].win_bits >> 5;
     for (uint32_t w = 0; w < words; w++)
@@ -549,7 +786,8 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     while (c < n)
         c *= 2;
     void *old[] = { P->hdr, P->pstat, P->skey, P->skey2, P->perm,
-                    P->perm2, P->val, P->est, P->meta, P->cub };
+                    P->perm2, P->val, P->est, P->meta, P->cub, P->auth,
+                    P->top };
     for (void *o : old)
         if (o)
             PPCHK(hipFree(o));
@@ -562,6 +800,8 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipMalloc((void **)&P->val, c * 8));
     PPCHK(hipMalloc((void **)&P->est, c * 8));
     PPCHK(hipMalloc((void **)&P->meta, c * sizeof(srtp_dev_meta_t)));
+    PPCHK(hipMalloc((void **)&P->auth, c));
+    PPCHK(hipMalloc((void **)&P->top, c * 8));
     // temp storage for the largest sort and scan of c items
     size_t a = 0, b = 0;
     PPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, a, P->skey, P->skey2,
@@ -575,9 +815,15 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
         P->skey, IsChain());
     PPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, c1, it, P->perm, (int)c,
                                            stream));
+    size_t c2 = 0;
+    PPCHK(hipcub::DeviceScan::ExclusiveScanByKey(
+        nullptr, c2, P->skey2, P->val, P->top, hipcub::Max(), (uint64_t)0,
+        (int)c, hipcub::Equality(), stream));
     P->cub_bytes = a > b ? a : b;
     if (c1 > P->cub_bytes)
         P->cub_bytes = c1;
+    if (c2 > P->cub_bytes)
+        P->cub_bytes = c2;
     PPCHK(hipMalloc(&P->cub, P->cub_bytes));
     P->n_cap = c;
     return 0;
@@ -593,10 +839,10 @@ void srtp_gpu_pp_free(void *p)
     if (!P)
         return;
     void *bufs[] = { P->st, P->win, P->wnew, P->hkey, P->hval, P->bcount,
-                     P->seg_first,
+                     P->seg_first, P->bcount2, P->new_index2,
                      P->new_index, P->hdr, P->pstat, P->skey, P->skey2,
                      P->perm, P->perm2, P->val, P->est, P->meta, P->cub,
-                     P->abort };
+                     P->auth, P->top, P->abort };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -613,10 +859,12 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     PpState *P = pp_of(g);
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
     uint32_t c1 = P->ns_cap, c2 = P->ns_cap, c5 = P->ns_cap,
-             c3 = P->nwords_cap;
+             c6 = P->ns_cap, c7 = P->ns_cap, c3 = P->nwords_cap;
     if (regrow(&P->st, &P->ns_cap, ns + 1) ||
         regrow(&P->bcount, &c1, ns + 1) || regrow(&P->new_index, &c2, ns + 1) ||
         regrow(&P->seg_first, &c5, ns + 1) ||
+        regrow(&P->bcount2, &c6, ns + 1) ||
+        regrow(&P->new_index2, &c7, ns + 1) ||
         regrow(&P->win, &P->nwords_cap, nwords + 1) ||
         regrow(&P->wnew, &c3, nwords + 1))
         return -1;
@@ -819,6 +1067,165 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     }
     b->sorted = !unordered;
     *fallback = (int)*P->h_abort;   // abort reason bits (AB_*), 0 = done
+    return 0;
+    }
+}
+
+int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
+                          int *fallback)
+{
+    *fallback = 1;
+    b->sorted = 0;
+    PpState *P = pp_of(g);
+    const size_t n = b->n;
+    if (!n) {
+        *fallback = 0;
+        return 0;
+    }
+    if (!P->st || !P->ns || n > 0x7fffffffu)
+        return 0;
+    hipStream_t stream = (hipStream_t)b->stream;   // NULL = the null stream
+    if (reserve_packets(P, n, stream) || pp_step(stream, "reserve"))
+        return -1;
+    const uint32_t N = (uint32_t)n, ns = P->ns;
+    const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
+    static const bool force_sorted = [] {
+        const char *e = getenv("SRTP_PP_SORTED");
+        return e && *e == '1';
+    }();
+    // one stream: the chain form directly (a sender's batch usually holds
+    // more packets than the replay window); several: order-free first
+    bool unordered = ns > 1 && !force_sorted;
+    for (;;) {
+    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
+    PPCHK(hipMemsetAsync(P->bcount, 0, ns * 4ull, stream));
+    PPCHK(hipMemsetAsync(P->new_index, 0, ns * 8ull, stream));
+    PPCHK(hipMemsetAsync(P->bcount2, 0, ns * 4ull, stream));
+    PPCHK(hipMemsetAsync(P->new_index2, 0, ns * 8ull, stream));
+
+    ClassifyArgs C;
+    C.in = b->in;
+    C.in_off = b->in_off;
+    C.in_len = b->in_len;
+    C.cap = b->out_len;
+    C.st = P->st;
+    C.hkey = P->hkey;
+    C.hval = P->hval;
+    C.hmask = P->hcap - 1;
+    C.n = N;
+    C.hdr = P->hdr;
+    C.pstat = P->pstat;
+    C.skey = P->skey;
+    C.perm = P->perm;
+    C.bcount = P->bcount;
+    C.abort = P->abort;
+    C.est = unordered ? P->est : nullptr;
+    C.new_index = unordered ? (unsigned long long *)P->new_index : nullptr;
+    hipLaunchKernelGGL(k_pu_classify, gp, blk, 0, stream, C);
+    PPCHK(hipGetLastError());
+    const uint32_t *ks, *kp;   // the order the kernels below walk
+    if (unordered) {
+        // order-free conditions and duplicates over every candidate
+        hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
+                           P->new_index, P->win, P->wnew);
+        hipLaunchKernelGGL(k_pp_usetbits, gp, blk, 0, stream, P->skey, P->est,
+                           P->st, ns, N, P->new_index, P->wnew, P->abort);
+        ks = P->skey;
+        kp = P->perm;
+    } else {
+        // chain form: stable stream order, advances, segmented sum
+        size_t tb = P->cub_bytes;
+        if (ns == 1) {
+            hipcub::TransformInputIterator<uint32_t, IsChain, const uint32_t *>
+                it(P->skey, IsChain());
+            PPCHK(hipcub::DeviceScan::ExclusiveSum(P->cub, tb, it, P->perm,
+                                                   (int)N, stream));
+            hipLaunchKernelGGL(k_pp_partition1, gp, blk, 0, stream, P->skey,
+                               P->perm, N, P->skey2, P->perm2);
+        } else {
+            int end_bit = 1;
+            while ((1u << end_bit) <= ns && end_bit < 32)
+                end_bit++;
+            PPCHK(hipcub::DeviceRadixSort::SortPairs(
+                P->cub, tb, P->skey, P->skey2, P->perm, P->perm2, (int)N, 0,
+                end_bit, stream));
+        }
+        hipLaunchKernelGGL(k_pp_delta, gp, blk, 0, stream, P->skey2, P->perm2,
+                           P->hdr, P->st, ns, N, P->val, P->seg_first,
+                           P->abort);
+        tb = P->cub_bytes;
+        PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
+            P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
+            hipcub::Equality(), stream));
+        // candidates per stream (AES-GCM key usage)
+        hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est,
+                           ns, N, P->seg_first, P->bcount, P->new_index);
+        ks = P->skey2;
+        kp = P->perm2;
+    }
+    hipLaunchKernelGGL(k_pu_meta, gp, blk, 0, stream, ks, kp, P->est, P->hdr,
+                       P->st, ns, N, P->abort, P->meta, P->auth);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "pu_prepass"))
+        return -1;
+
+    srtp_gpu_batch_t cb = {};
+    cb.n = n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;
+    cb.auth_ok = P->auth;
+    cb.uniform_key = b->uniform_key;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = P->abort;
+    if (srtp_gpu_run(g, 1, &cb))
+        return -1;
+    if (pp_step(stream, "pu_crypto"))
+        return -1;
+
+    if (!unordered) {
+        size_t tb = P->cub_bytes;
+        hipLaunchKernelGGL(k_pu_accepted_est, gp, blk, 0, stream, P->skey2,
+                           P->perm2, P->est, P->auth, ns, N, P->val);
+        PPCHK(hipcub::DeviceScan::ExclusiveScanByKey(
+            P->cub, tb, P->skey2, P->val, P->top, hipcub::Max(), (uint64_t)0,
+            (int)N, hipcub::Equality(), stream));
+        hipLaunchKernelGGL(k_pu_top_check, gp, blk, 0, stream, P->skey2,
+                           P->perm2, P->hdr, P->est, P->top, P->st, ns, N,
+                           P->abort);
+    }
+    hipLaunchKernelGGL(k_pu_accept, gp, blk, 0, stream, ks, kp, P->est,
+                       P->pstat, P->hdr, P->st, ns, N, P->abort, P->auth,
+                       P->meta, b->status, b->out_len, P->bcount2,
+                       (unsigned long long *)P->new_index2);
+    // the window again, from the stored one, for the authenticated packets
+    hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
+                       P->new_index2, P->win, P->wnew);
+    hipLaunchKernelGGL(k_pu_setbits, gp, blk, 0, stream, ks, kp, P->est,
+                       P->st, ns, N, P->abort, P->auth, P->new_index2,
+                       P->wnew);
+    hipLaunchKernelGGL(k_pu_commit_stream, gs, blk, 0, stream, P->st, ns,
+                       P->new_index2, P->bcount, P->bcount2, P->wnew, P->win,
+                       P->abort);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "pu_commit"))
+        return -1;
+    // rejected packets (all of them after a post-crypto abort): their
+    // speculative decryption is undone
+    if (srtp_gpu_undo(g, n, b->out, b->out_off, P->meta, stream))
+        return -1;
+    PPCHK(hipMemcpyAsync(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost,
+                         stream));
+    PPCHK(hipStreamSynchronize(stream));
+    if (unordered && *P->h_abort == AB_ORDER) {
+        unordered = false;   // nothing ran or changed: the chain form
+        continue;
+    }
+    b->sorted = !unordered;
+    *fallback = (int)*P->h_abort;
     return 0;
     }
 }

@@ -141,3 +141,128 @@ def test_rejected_buffers_hold_no_plaintext(name, inplace):
             assert got[12:body] != plain[i][12:body], i
             assert got[12:body] in (pk[i][12:body], bytes([0x3c]) * (body - 12))
     assert nrej > 100
+
+
+# --------------------------------------------------------------------------
+# the device unprotect pre-pass (srtp_gpu_pp_unprotect): receive batches of
+# known streams stay on the GPU, forged / tampered packets included
+
+def _multi_stream_batches(rng, name, ns, per, nbatch, tamper):
+    ssrcs = [0x30000000 + 11 * k for k in range(ns)]
+    pols = [policy(name, ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    snd = O.Session(pols)
+    seq = {s: rng.randrange(1, 0x10000) for s in ssrcs}
+    batches = []
+    for _ in range(nbatch):
+        order = [s for s in ssrcs for _ in range(per)]
+        rng.shuffle(order)
+        pk, kinds = [], []
+        for s in order:
+            p = rtp_packet(rng, s, seq[s] & 0xffff, rng.choice([0, 20, 160]))
+            seq[s] += 1
+            rc, sp = snd.protect(p, len(p) + 64)
+            assert rc == 0
+            if rng.random() < tamper:
+                b = bytearray(sp)
+                b[-1] ^= 0x40
+                sp = bytes(b)
+                kinds.append("tampered")
+            else:
+                kinds.append("genuine")
+            pk.append(sp)
+        batches.append((pk, kinds))
+    return pols, batches
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16", "null_hmac80"])
+@pytest.mark.parametrize("inplace", [True, False], ids=["inplace", "outofplace"])
+def test_device_unprotect_prepass(name, inplace):
+    _gpu()
+    rng = random.Random(14)
+    pols, batches = _multi_stream_batches(rng, name, 40, 30, 3, 0.05)
+    lib, orc = L.Session(pols), O.Session(pols)
+    for bi, (pk, kinds) in enumerate(batches):
+        ref = [orc.unprotect(p, len(p)) for p in pk]
+        st, olen, host, offs = _device_unprotect(lib, pk, inplace)
+        for i, (rc, o) in enumerate(ref):
+            assert st[i] == rc, (bi, i, kinds[i], st[i], rc)
+            got = host[offs[i]:offs[i] + len(pk[i])]
+            if rc == 0:
+                assert olen[i] == len(o) and got[:len(o)] == o, (bi, i)
+            elif inplace:
+                assert got == pk[i], (bi, i)     # ciphertext restored
+    assert lib.prepass_stats() == (3, 0), lib.prepass_last_abort()
+    # state left by the device is what the host path continues from
+    _, more = _multi_stream_batches(random.Random(15), name, 40, 2, 1, 0)
+    for p in more[0][0][:20]:
+        assert lib.unprotect(p, len(p))[0] == orc.unprotect(p, len(p))[0]
+
+
+def test_device_unprotect_replayed_batch_goes_to_host():
+    _gpu()
+    rng = random.Random(16)
+    pols, batches = _multi_stream_batches(rng, "icm128_hmac80", 8, 20, 2, 0)
+    lib, orc = L.Session(pols), O.Session(pols)
+    pk = batches[0][0]
+    for p in pk:
+        orc.unprotect(p, len(p))
+    st, _, _, _ = _device_unprotect(lib, pk, False)
+    assert st == [0] * len(pk)
+    # the same packets again: every one a replay (host path decides)
+    ref = [orc.unprotect(p, len(p))[0] for p in pk]
+    st, _, _, _ = _device_unprotect(lib, pk, False)
+    assert st == ref and set(ref) == {9}
+    assert lib.prepass_stats() == (1, 1)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+@pytest.mark.parametrize("inplace", [True, False], ids=["inplace", "outofplace"])
+def test_device_unprotect_chain_one_stream(name, inplace):
+    """one stream, more packets than the replay window: the chain form
+    (stream order, advances, segmented sum; acceptance checked against the
+    highest authenticated index before each packet)"""
+    _gpu()
+    rng = random.Random(17)
+    pols, batches = _multi_stream_batches(rng, name, 1, 3000, 2, 0.05)
+    lib, orc = L.Session(pols), O.Session(pols)
+    for bi, (pk, kinds) in enumerate(batches):
+        ref = [orc.unprotect(p, len(p)) for p in pk]
+        st, olen, host, offs = _device_unprotect(lib, pk, inplace)
+        for i, (rc, o) in enumerate(ref):
+            assert st[i] == rc, (bi, i, kinds[i], st[i], rc)
+            got = host[offs[i]:offs[i] + len(pk[i])]
+            if rc == 0:
+                assert got[:len(o)] == o, (bi, i)
+            elif inplace:
+                assert got == pk[i], (bi, i)
+    assert lib.prepass_stats() == (2, 0), lib.prepass_last_abort()
+    assert lib.get_roc(0x30000000)[1] == orc.get_roc(0x30000000)[1]
+
+
+def test_device_unprotect_chain_long_rejected_run_goes_to_host():
+    """forged packets advancing the chain by 3 x 20000 indices: from the
+    second one on, the reference's guess from the last accepted index
+    (above 2^15, so with ROC inference) differs from the chain's -- the
+    host path decides"""
+    _gpu()
+    rng = random.Random(18)
+    pol = policy("icm128_hmac80", ssrc=SSRC, seed=3)
+    snd, orc, lib = O.Session([pol]), O.Session([pol]), L.Session([pol])
+    pk, seq = [], 40000
+    for k in range(200):
+        p = rtp_packet(rng, SSRC, seq & 0xffff, 40)
+        pk.append(snd.protect(p, len(p) + 64)[1])
+        seq += 1
+    for _ in range(3):
+        seq += 20000
+        p = rtp_packet(rng, SSRC, seq & 0xffff, 40)
+        snd.protect(p, len(p) + 64)         # the sender's index moves on
+        pk.append(p + rng.randbytes(10))    # what arrives is forged
+    for k in range(50):
+        seq += 1
+        p = rtp_packet(rng, SSRC, seq & 0xffff, 40)
+        pk.append(snd.protect(p, len(p) + 64)[1])
+    ref = [orc.unprotect(p, len(p))[0] for p in pk]
+    st, _, _, _ = _device_unprotect(lib, pk, True)
+    assert st == ref
+    assert lib.prepass_stats() == (0, 1)

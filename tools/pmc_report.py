@@ -15,7 +15,8 @@ def main():
     d, kern = sys.argv[1], sys.argv[2]
     pk = int(sys.argv[3]) if len(sys.argv) > 3 else 1 << 20
     vals = {}
-    for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"),
+                              recursive=True)):
         acc = collections.defaultdict(float)
         disp = collections.defaultdict(set)
         for r in csv.DictReader(open(f)):
@@ -25,6 +26,15 @@ def main():
             disp[r["Counter_Name"]].add(r["Dispatch_Id"])
         for k, v in acc.items():
             vals[k] = v / max(1, len(disp[k]))
+    # reduced on the box by tools/pmc_reduce.py: per kernel means (kernels
+    # matching the substring are summed: e.g. both launches of one step)
+    for f in sorted(glob.glob(os.path.join(d, "**", "pmc_summary.csv"),
+                              recursive=True)):
+        acc = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if kern in r["Kernel_Name"]:
+                acc[r["Counter_Name"]] += float(r["Mean_Per_Dispatch"])
+        vals.update(acc)
     for k in sorted(vals):
         print("%-28s %16.1f" % (k, vals[k]))
     g = vals.get

@@ -11,6 +11,7 @@ mkdir -p "$out"
 echo "[prof] kernel trace"
 timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/kt" -o kt \
     -- python3 bench.py $args > "$out/kt.log" 2>&1 || { tail -5 "$out/kt.log"; exit 1; }
+python3 tools/pmc_reduce.py "$out/kt"
 passes=(
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"
   "SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT"
@@ -24,4 +25,5 @@ for p in "${passes[@]}"; do
   rc=$?
   echo "[prof] pass $i rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 "$out/p$i.log"; exit $rc; fi
+  python3 tools/pmc_reduce.py "$out/p$i"
 done
