@@ -90,7 +90,7 @@ def parse():
     ap.add_argument("--packets", type=int, default=0,
                     help="override packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+    ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
                     help="auto: measure roofline.traffic with two rocprofv3 "
@@ -187,38 +187,64 @@ def timed_steps(step, steps, warmup, world, sync=None):
     return dt, res
 
 
-def cpu_baseline(cfg, payload, seconds):
-    """The reference on the host: srtp_protect() per packet, one srtp_t per
-    thread (oracle/bench_ref.c over oracle/_ref/libsrtp_ref_*.so).  The
-    OpenSSL-backed build is used when present -- libsrtp's recommended, and
-    faster, configuration (4.5x the internal kernel for
-    ICM+HMAC on one core); the internal-kernel build otherwise (no GCM)."""
+def _ref_rate(lib_path, op, payload, gcm, threads, seconds):
+    """packets/s of the reference build at lib_path: calibrate on one thread,
+    then ~`seconds` of work on `threads` threads"""
+    L = C.CDLL(lib_path)
+    fn = L.ref_bench if op == "protect" else L.ref_bench_unprotect
+    fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    secs = C.c_double()
+    n = fn(1, 8192, payload, int(gcm), C.byref(secs))
+    per_thread = max(8192, int(n / max(secs.value, 1e-6) * seconds))
+    done = fn(threads, per_thread, payload, int(gcm), C.byref(secs))
+    return done / secs.value, done
+
+
+def cpu_baseline(cfg, op, payload, seconds):
+    """The reference on the host: srtp_protect() (or srtp_unprotect()) per
+    packet, one srtp_t per thread (oracle/bench_ref.c over
+    oracle/_ref/bench_ref_*.so, cisco/libsrtp built from its own sources).
+    Both crypto backends are timed: OpenSSL 3 (libsrtp's recommended, and
+    faster, configuration) is `value`; the built-in crypto kernel that
+    north_star names is `internal_kernel` (it has no AES-GCM).  Threads: the
+    CPUs this process may run on, capped at 16 -- the one-GPU box grants a
+    16-CPU share of a larger host (`host_cpus`)."""
     gcm = cfg == "gcm256"
     ref = os.path.join(ROOT, "oracle", "_ref")
-    lib, backend = os.path.join(ref, "bench_ref_ossl.so"), \
-        "OpenSSL 3 crypto backend"
-    if not os.path.exists(lib) and not gcm:
-        lib, backend = os.path.join(ref, "bench_ref_int.so"), \
-            "internal crypto kernel"
-    if not os.path.exists(lib):
+    ossl = os.path.join(ref, "bench_ref_ossl.so")
+    intk = os.path.join(ref, "bench_ref_int.so")
+    affinity = len(os.sched_getaffinity(0))
+    threads = max(1, min(16, affinity))
+    call = "srtp_%s()" % op
+    res = {}
+    if os.path.exists(ossl):
+        res["ossl"] = _ref_rate(ossl, op, payload, gcm, threads, seconds)
+    if os.path.exists(intk) and not gcm:
+        res["int"] = _ref_rate(intk, op, payload, gcm, threads, seconds)
+    if not res:
         return None
-    L = C.CDLL(lib)
-    L.ref_bench.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int,
-                            C.POINTER(C.c_double)]
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    secs = C.c_double()
-    # calibrate on one thread, then size the sample to ~`seconds`
-    n = L.ref_bench(1, 2000, payload, int(gcm), C.byref(secs))
-    per_thread_rate = n / max(secs.value, 1e-6)
-    per_thread = max(1000, int(per_thread_rate * seconds))
-    done = L.ref_bench(threads, per_thread, payload, int(gcm), C.byref(secs))
-    return {"value": done / secs.value, "unit": "pkt/s", "cores": threads,
-            "kind": "reference",
-            "sample": "%d x srtp_protect() of %d-byte payloads, %d threads x "
-                      "1 srtp_t, cisco/libsrtp 3.0.0 with the %s, built from "
-                      "source (oracle/Makefile.ref)"
-                      % (done, payload, threads, backend),
-            "payload_GBps": done * payload / secs.value / 1e9}
+    main_key = "ossl" if "ossl" in res else "int"
+    backend = {"ossl": "OpenSSL 3 crypto backend",
+               "int": "built-in crypto kernel"}
+    rate, done = res[main_key]
+    out = {"value": rate, "unit": "pkt/s", "cores": threads,
+           "kind": "reference",
+           "sample": "%d x %s of %d-byte payloads, %d threads x 1 srtp_t, "
+                     "cisco/libsrtp 3.0.0 with the %s, built from source "
+                     "(oracle/Makefile.ref)" % (done, call, payload, threads,
+                                                 backend[main_key]),
+           "payload_GBps": rate * payload / 1e9,
+           "host_cpus": os.cpu_count(), "affinity_cpus": affinity}
+    if main_key == "ossl":
+        if "int" in res:
+            r2, d2 = res["int"]
+            out["internal_kernel"] = {
+                "value": r2, "unit": "pkt/s", "cores": threads,
+                "sample": "%d x %s, same threads, %s" % (d2, call,
+                                                         backend["int"])}
+        else:
+            out["internal_kernel"] = None   # no AES-GCM in that kernel
+    return out
 
 
 def distribute_keys(keys_hex, world, dev):
@@ -329,6 +355,10 @@ def main():
         snd.close()
         in_len = srtp_len
     sess.set_timing(True)
+    # out_len: capacities in, lengths out.  Filled once: a step leaves the
+    # lengths it produced (<= slot), which are exactly the capacities the
+    # next batch of the same shape needs.
+    out_len.fill_(slot)
     torch.cuda.synchronize()
     k_step = [0]
     fn = sess.protect_device if a.op == "protect" else sess.unprotect_device
@@ -336,7 +366,6 @@ def main():
     def step():
         ar = arenas[k_step[0]]
         k_step[0] += 1
-        out_len.fill_(slot)
         st = fn(ar, off, in_len, ar, off, out_len, status, stream=stream)
         if st != 0:
             raise RuntimeError("srtp_%s_device: %s" % (a.op, st))
@@ -356,7 +385,7 @@ def main():
         return
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(a.config, payload, a.cpu_seconds)
+        cpu = cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
     out = {
         "metric": "SRTP packets/sec + payload GB/s, device-resident, "
                   "1M×1400B batch",

@@ -7,6 +7,11 @@
  *
  * int ref_bench(int threads, long pkts_per_thread, int payload,
  *               int gcm, double *seconds)  -> packets protected
+ *
+ * Receive side: ref_bench_unprotect() -- each thread protects its pool
+ * (untimed) with a sender srtp_t, then srtp_unprotect()s it in place on a
+ * receiver srtp_t (timed), pool after pool; *seconds is the slowest
+ * thread's unprotect time.
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -18,9 +23,17 @@
 
 typedef struct {
     long n;
-    int payload, gcm, pool;
+    int payload, gcm, pool, unprotect;
     long done;
+    double secs; /* unprotect: time spent in srtp_unprotect */
 } job_t;
+
+static double now(void)
+{
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
 
 static const uint8_t key46[46] = {
     0xe1, 0xf9, 0x7a, 0x0d, 0x3e, 0x01, 0x8b, 0xe0, 0xd6, 0x4f, 0xa3, 0x2c,
@@ -46,6 +59,12 @@ static void *run(void *arg)
     p.window_size = 128;
     if (srtp_create(&s, &p))
         return NULL;
+    srtp_t r = NULL;
+    if (j->unprotect) {
+        p.ssrc.type = ssrc_any_inbound;
+        if (srtp_create(&r, &p))
+            return NULL;
+    }
     size_t slot = (size_t)(12 + j->payload + 64 + 63) & ~(size_t)63;
     uint8_t *buf = (uint8_t *)aligned_alloc(64, slot * (size_t)j->pool);
     uint64_t x = 0x5352545030303031ULL ^ (uint64_t)(uintptr_t)j;
@@ -56,25 +75,49 @@ static void *run(void *arg)
         buf[i] = (uint8_t)x;
     }
     uint16_t seq = 0x1234;
-    for (long i = 0; i < j->n; i++) {
-        uint8_t *pk = buf + slot * (size_t)(i % j->pool);
-        pk[0] = 0x80;
-        pk[1] = 96;
-        pk[2] = (uint8_t)(seq >> 8);
-        pk[3] = (uint8_t)seq;
-        pk[8] = 0xca; pk[9] = 0xfe; pk[10] = 0xba; pk[11] = 0xbe;
-        size_t len = slot;
-        if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0)
-            j->done++;
-        seq++;
+    size_t *plen = (size_t *)malloc(sizeof(size_t) * (size_t)j->pool);
+    for (long i = 0; i < j->n;) {
+        long m = j->unprotect ? j->pool : 1;
+        if (m > j->n - i)
+            m = j->n - i;
+        for (long q = 0; q < m; q++) {
+            uint8_t *pk = buf + slot * (size_t)((i + q) % j->pool);
+            pk[0] = 0x80;
+            pk[1] = 96;
+            pk[2] = (uint8_t)(seq >> 8);
+            pk[3] = (uint8_t)seq;
+            pk[8] = 0xca; pk[9] = 0xfe; pk[10] = 0xba; pk[11] = 0xbe;
+            size_t len = slot;
+            plen[q] = 0;
+            if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0) {
+                if (!j->unprotect)
+                    j->done++;
+                plen[q] = len;
+            }
+            seq++;
+        }
+        if (j->unprotect) {
+            double t0 = now();
+            for (long q = 0; q < m; q++) {
+                uint8_t *pk = buf + slot * (size_t)((i + q) % j->pool);
+                size_t len = slot;
+                if (plen[q] && srtp_unprotect(r, pk, plen[q], pk, &len) == 0)
+                    j->done++;
+            }
+            j->secs += now() - t0;
+        }
+        i += m;
     }
+    free(plen);
     free(buf);
     srtp_dealloc(s);
+    if (r)
+        srtp_dealloc(r);
     return NULL;
 }
 
-int ref_bench(int threads, long pkts_per_thread, int payload, int gcm,
-              double *seconds)
+static int bench(int threads, long pkts_per_thread, int payload, int gcm,
+                 int unprotect, double *seconds)
 {
     static int inited;
     if (!inited) {
@@ -93,15 +136,34 @@ int ref_bench(int threads, long pkts_per_thread, int payload, int gcm,
         jobs[t].payload = payload;
         jobs[t].gcm = gcm;
         jobs[t].pool = 4096;
+        jobs[t].unprotect = unprotect;
         jobs[t].done = 0;
+        jobs[t].secs = 0;
         pthread_create(&th[t], NULL, run, &jobs[t]);
     }
     long done = 0;
+    double slowest = 0;
     for (int t = 0; t < threads; t++) {
         pthread_join(th[t], NULL);
         done += jobs[t].done;
+        if (jobs[t].secs > slowest)
+            slowest = jobs[t].secs;
     }
     clock_gettime(CLOCK_MONOTONIC, &b);
-    *seconds = (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    *seconds = unprotect ? slowest
+                         : (double)(b.tv_sec - a.tv_sec) +
+                               1e-9 * (double)(b.tv_nsec - a.tv_nsec);
     return (int)done;
+}
+
+int ref_bench(int threads, long pkts_per_thread, int payload, int gcm,
+              double *seconds)
+{
+    return bench(threads, pkts_per_thread, payload, gcm, 0, seconds);
+}
+
+int ref_bench_unprotect(int threads, long pkts_per_thread, int payload,
+                        int gcm, double *seconds)
+{
+    return bench(threads, pkts_per_thread, payload, gcm, 1, seconds);
 }
