@@ -41,7 +41,8 @@ def main():
     print()
     if g("SQ_WAVES"):
         w = g("SQ_WAVES")
-        print("per packet: VALU %.0f  LDS %.0f  VMEM_RD %.1f  VMEM_WR %.1f" % (
+        print("per 64 packets (wave-instructions): VALU %.0f  LDS %.0f  "
+              "VMEM_RD %.1f  VMEM_WR %.1f" % (
             64 * g("SQ_INSTS_VALU", 0) / pk, 64 * g("SQ_INSTS_LDS", 0) / pk,
             64 * g("SQ_INSTS_VMEM_RD", 0) / pk,
             64 * g("SQ_INSTS_VMEM_WR", 0) / pk))
