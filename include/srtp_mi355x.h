@@ -3,7 +3,8 @@
  *
  * Drop-in surface: every declaration in the first half keeps the name,
  * signature, struct layout and enum values of cisco/libsrtp 3.0.0's public
- * header (include/srtp.h; symbol list srtp.def:1-69), so C code written
+ * header (include/srtp.h; symbol list srtp.def:1-69 incl. the crypto-kernel
+ * plugin ABI of srtp.def:46-69, below), so C code written
  * against libsrtp compiles and links against this library unchanged.  Each
  * group cites the reference declaration it replaces.
  *
@@ -340,8 +341,10 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx,
  * in_off[i] + roundup16(in_len[i]).  Output goes to out + out_off[i] (may be
  * the same bytes as the input: in place) with capacity out_len[i]; on
  * success out_len[i] is overwritten with the output length.  status[i] is an
- * int32 srtp_err_status_t.  `stream` is a hipStream_t (NULL: the session's
- * own stream); the call returns after the batch has completed.
+ * int32 srtp_err_status_t.  `stream` is a hipStream_t; NULL means the HIP
+ * null stream (PyTorch's default stream handle is 0), so work queued there
+ * before the call is ordered before it.  The call returns after the batch
+ * has completed.
  */
 typedef struct srtp_device_batch_t {
     size_t n;
@@ -386,6 +389,220 @@ void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
                                  uint32_t *launches, uint32_t *undo_launches);
 /* 1 when a HIP device is usable from this process */
 int srtp_mi355x_gpu_available(void);
+
+/* ========================================================================
+ * The crypto-kernel plugin ABI (srtp.def:46-69): libsrtp's cipher / auth
+ * vtables (crypto/include/cipher.h:60-260, auth.h:55-200), the type
+ * registry with srtp_replace_cipher_type / srtp_replace_auth_type
+ * (crypto/kernel/crypto_kernel.c:270-440) and the utilities srtp.def
+ * exports with them.  Layouts and semantics follow the reference.  The
+ * built-in types are GPU-backed: every encrypt / decrypt / compute call of
+ * AES-ICM-128/192/256, AES-GCM-128/256 and HMAC-SHA1 is one HIP launch
+ * (srtp_plugin.c -> srtp_gpu_raw); the null cipher and null auth need no
+ * device.  A replacement type must pass its own known answers and the
+ * built-in type's (as in the reference), i.e. compute the same function, so
+ * the packet path keeps the GPU kernels for that algorithm id.
+ * ====================================================================== */
+typedef enum {
+    srtp_direction_encrypt,
+    srtp_direction_decrypt,
+    srtp_direction_any
+} srtp_cipher_direction_t;
+
+typedef struct srtp_cipher_t *srtp_cipher_pointer_t;
+typedef srtp_err_status_t (*srtp_cipher_alloc_func_t)(srtp_cipher_pointer_t *cp,
+                                                      size_t key_len,
+                                                      size_t tag_len);
+typedef srtp_err_status_t (*srtp_cipher_init_func_t)(void *state,
+                                                     const uint8_t *key);
+typedef srtp_err_status_t (*srtp_cipher_dealloc_func_t)(
+    srtp_cipher_pointer_t cp);
+typedef srtp_err_status_t (*srtp_cipher_set_aad_func_t)(void *state,
+                                                        const uint8_t *aad,
+                                                        size_t aad_len);
+typedef srtp_err_status_t (*srtp_cipher_encrypt_func_t)(void *state,
+                                                        const uint8_t *src,
+                                                        size_t src_len,
+                                                        uint8_t *dst,
+                                                        size_t *dst_len);
+typedef srtp_err_status_t (*srtp_cipher_decrypt_func_t)(void *state,
+                                                        const uint8_t *src,
+                                                        size_t src_len,
+                                                        uint8_t *dst,
+                                                        size_t *dst_len);
+typedef srtp_err_status_t (*srtp_cipher_set_iv_func_t)(
+    void *state, uint8_t *iv, srtp_cipher_direction_t direction);
+
+typedef struct srtp_cipher_test_case_t {
+    size_t key_length_octets;
+    const uint8_t *key;
+    uint8_t *idx;
+    size_t plaintext_length_octets;
+    const uint8_t *plaintext;
+    size_t ciphertext_length_octets;
+    const uint8_t *ciphertext;
+    size_t aad_length_octets;
+    const uint8_t *aad;
+    size_t tag_length_octets;
+    const struct srtp_cipher_test_case_t *next_test_case;
+} srtp_cipher_test_case_t;
+
+typedef struct srtp_cipher_type_t {
+    srtp_cipher_alloc_func_t alloc;
+    srtp_cipher_dealloc_func_t dealloc;
+    srtp_cipher_init_func_t init;
+    srtp_cipher_set_aad_func_t set_aad;
+    srtp_cipher_encrypt_func_t encrypt;
+    srtp_cipher_decrypt_func_t decrypt;
+    srtp_cipher_set_iv_func_t set_iv;
+    const char *description;
+    const srtp_cipher_test_case_t *test_data;
+    srtp_cipher_type_id_t id;
+} srtp_cipher_type_t;
+
+typedef struct srtp_cipher_t {
+    const srtp_cipher_type_t *type;
+    void *state;
+    size_t key_len;
+    srtp_cipher_type_id_t algorithm;
+} srtp_cipher_t;
+
+size_t srtp_cipher_get_key_length(const srtp_cipher_t *c);
+srtp_err_status_t srtp_cipher_type_self_test(const srtp_cipher_type_t *ct);
+srtp_err_status_t srtp_cipher_type_test(
+    const srtp_cipher_type_t *ct, const srtp_cipher_test_case_t *test_data);
+uint64_t srtp_cipher_bits_per_second(srtp_cipher_t *c, size_t octets_in_buffer,
+                                     size_t num_trials);
+srtp_err_status_t srtp_cipher_type_alloc(const srtp_cipher_type_t *ct,
+                                         srtp_cipher_t **c, size_t key_len,
+                                         size_t tlen);
+srtp_err_status_t srtp_cipher_dealloc(srtp_cipher_t *c);
+srtp_err_status_t srtp_cipher_init(srtp_cipher_t *c, const uint8_t *key);
+srtp_err_status_t srtp_cipher_set_iv(srtp_cipher_t *c, uint8_t *iv,
+                                     srtp_cipher_direction_t direction);
+srtp_err_status_t srtp_cipher_output(srtp_cipher_t *c, uint8_t *buffer,
+                                     size_t *num_octets_to_output);
+srtp_err_status_t srtp_cipher_encrypt(srtp_cipher_t *c, const uint8_t *src,
+                                      size_t src_len, uint8_t *dst,
+                                      size_t *dst_len);
+srtp_err_status_t srtp_cipher_decrypt(srtp_cipher_t *c, const uint8_t *src,
+                                      size_t src_len, uint8_t *dst,
+                                      size_t *dst_len);
+srtp_err_status_t srtp_cipher_set_aad(srtp_cipher_t *c, const uint8_t *aad,
+                                      size_t aad_len);
+srtp_err_status_t srtp_replace_cipher_type(const srtp_cipher_type_t *ct,
+                                           srtp_cipher_type_id_t id);
+
+typedef const struct srtp_auth_type_t *srtp_auth_type_pointer;
+typedef struct srtp_auth_t *srtp_auth_pointer_t;
+typedef srtp_err_status_t (*srtp_auth_alloc_func)(srtp_auth_pointer_t *ap,
+                                                  size_t key_len,
+                                                  size_t out_len);
+typedef srtp_err_status_t (*srtp_auth_init_func)(void *state,
+                                                 const uint8_t *key,
+                                                 size_t key_len);
+typedef srtp_err_status_t (*srtp_auth_dealloc_func)(srtp_auth_pointer_t ap);
+typedef srtp_err_status_t (*srtp_auth_compute_func)(void *state,
+                                                    const uint8_t *buffer,
+                                                    size_t octets_to_auth,
+                                                    size_t tag_len,
+                                                    uint8_t *tag);
+typedef srtp_err_status_t (*srtp_auth_update_func)(void *state,
+                                                   const uint8_t *buffer,
+                                                   size_t octets_to_auth);
+typedef srtp_err_status_t (*srtp_auth_start_func)(void *state);
+
+/* the reference's auth.h macros */
+#define srtp_auth_type_alloc(at, a, klen, outlen)                              \
+    ((at)->alloc((a), (klen), (outlen)))
+#define srtp_auth_init(a, key)                                                 \
+    (((a)->type)->init((a)->state, (key), ((a)->key_len)))
+#define srtp_auth_compute(a, buf, len, res)                                    \
+    (((a)->type)->compute((a)->state, (buf), (len), (a)->out_len, (res)))
+#define srtp_auth_update(a, buf, len)                                          \
+    (((a)->type)->update((a)->state, (buf), (len)))
+#define srtp_auth_start(a) (((a)->type)->start((a)->state))
+#define srtp_auth_dealloc(c) (((c)->type)->dealloc(c))
+
+typedef struct srtp_auth_test_case_t {
+    size_t key_length_octets;
+    const uint8_t *key;
+    size_t data_length_octets;
+    const uint8_t *data;
+    size_t tag_length_octets;
+    const uint8_t *tag;
+    const struct srtp_auth_test_case_t *next_test_case;
+} srtp_auth_test_case_t;
+
+typedef struct srtp_auth_type_t {
+    srtp_auth_alloc_func alloc;
+    srtp_auth_dealloc_func dealloc;
+    srtp_auth_init_func init;
+    srtp_auth_compute_func compute;
+    srtp_auth_update_func update;
+    srtp_auth_start_func start;
+    const char *description;
+    const srtp_auth_test_case_t *test_data;
+    srtp_auth_type_id_t id;
+} srtp_auth_type_t;
+
+typedef struct srtp_auth_t {
+    const srtp_auth_type_t *type;
+    void *state;
+    size_t out_len;
+    size_t key_len;
+    size_t prefix_len;
+} srtp_auth_t;
+
+size_t srtp_auth_get_key_length(const struct srtp_auth_t *a);
+size_t srtp_auth_get_tag_length(const struct srtp_auth_t *a);
+size_t srtp_auth_get_prefix_length(const struct srtp_auth_t *a);
+srtp_err_status_t srtp_auth_type_self_test(const srtp_auth_type_t *at);
+srtp_err_status_t srtp_auth_type_test(const srtp_auth_type_t *at,
+                                      const srtp_auth_test_case_t *test_data);
+srtp_err_status_t srtp_replace_auth_type(const srtp_auth_type_t *ct,
+                                         srtp_auth_type_id_t id);
+
+/* crypto/include/err.h:83-124, crypto_kernel.h:166 */
+typedef enum {
+    srtp_err_level_error,
+    srtp_err_level_warning,
+    srtp_err_level_info,
+    srtp_err_level_debug
+} srtp_err_reporting_level_t;
+typedef struct {
+    bool on;
+    const char *name;
+} srtp_debug_module_t;
+void srtp_err_report(srtp_err_reporting_level_t level, const char *format,
+                     ...);
+srtp_err_status_t srtp_crypto_kernel_load_debug_module(
+    srtp_debug_module_t *new_dm);
+
+/* crypto/include/datatypes.h:81, 158, 239-242; rdbx.h:78-87 */
+char *srtp_octet_string_hex_string(const void *str, size_t length);
+bool srtp_octet_string_equal(const uint8_t *a, const uint8_t *b, size_t len);
+typedef struct {
+    size_t length;
+    uint32_t *word;
+} bitvector_t;
+typedef uint64_t srtp_xtd_seq_num_t;
+typedef struct {
+    srtp_xtd_seq_num_t index;
+    bitvector_t bitmask;
+} srtp_rdbx_t;
+size_t srtp_rdbx_get_window_size(const srtp_rdbx_t *rdbx);
+
+/* extension: the built-in (GPU-backed) type registered for an id -- the
+ * reference's srtp_aes_icm_128, srtp_hmac, ... objects (NULL if none) --
+ * and whatever type the registry now holds for it after a replacement */
+const srtp_cipher_type_t *srtp_mi355x_builtin_cipher_type(
+    srtp_cipher_type_id_t id);
+const srtp_auth_type_t *srtp_mi355x_builtin_auth_type(srtp_auth_type_id_t id);
+const srtp_cipher_type_t *srtp_mi355x_registered_cipher_type(
+    srtp_cipher_type_id_t id);
+const srtp_auth_type_t *srtp_mi355x_registered_auth_type(
+    srtp_auth_type_id_t id);
 
 #ifdef __cplusplus
 }

@@ -197,6 +197,37 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
 int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                           int *fallback);
 
+/* ---- single-buffer operations of the crypto-kernel API ---------------
+ * (cipher.h / auth.h vtables of the reference, srtp_plugin.c): one GPU
+ * launch per call, host buffers in and out (copied through device scratch).
+ *   SRTP_RAW_ICM:  dst = src ^ (lead[0..nlead) || AES(ctr + j), j = 0..)
+ *                  with ICM's 16-bit block counter in ctr bytes 14..15;
+ *                  ks_last = the keystream of the last block generated
+ *   SRTP_RAW_GCM_SEAL / _OPEN: AES-GCM with iv (12 B), aad; seal writes
+ *                  ciphertext || tag (tag_len) to dst, open verifies the tag
+ *                  after src[0, len) (ok = 1 / 0) and writes the plaintext
+ *   SRTP_RAW_HMAC: dst[0..20) = HMAC-SHA1 from the key's ipad/opad
+ *                  midstates over src[0, len) */
+enum { SRTP_RAW_ICM = 0, SRTP_RAW_GCM_SEAL = 1, SRTP_RAW_GCM_OPEN = 2,
+       SRTP_RAW_HMAC = 3 };
+typedef struct srtp_gpu_raw {
+    int op;
+    const srtp_dev_key_t *key;   /* host: rk / rounds / h / ipad / opad */
+    const uint8_t *src;
+    uint8_t *dst;
+    size_t len;
+    uint8_t ctr[16];
+    uint8_t lead[16];
+    uint32_t nlead;
+    uint8_t ks_last[16];         /* out */
+    uint8_t iv[12];
+    const uint8_t *aad;
+    size_t aad_len;
+    uint32_t tag_len;
+    int ok;                      /* out (GCM open) */
+} srtp_gpu_raw_t;
+int srtp_gpu_raw(srtp_gpu_t *g, srtp_gpu_raw_t *r);
+
 /* plumbing between the two HIP translation units */
 void **srtp_gpu_pp_slot(srtp_gpu_t *g);
 void *srtp_gpu_stream_of(srtp_gpu_t *g);

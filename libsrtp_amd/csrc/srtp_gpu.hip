@@ -377,6 +377,139 @@ __global__ void k_parse(const uint8_t *in, const uint64_t *in_off,
     hdr[i] = srtp_parse_rtp(in + off, off, in_len[i]);
 }
 
+// ---------------------------------------------------------------------------
+// Single-buffer operations of the crypto-kernel API (srtp_gpu_raw): one
+// workgroup; AES-CTR blocks across the lanes, GHASH / SHA-1 on lane 0 (the
+// API moves one buffer per call: a handful of blocks).
+struct RawDev {
+    int op;
+    const srtp_dev_key_t *key;
+    const uint8_t *src;
+    uint8_t *dst;
+    uint32_t len, nlead, aad_len, tag_len;
+    uint8_t ctr[16], lead[16], iv[12];
+    const uint8_t *aad;
+    uint8_t *res;   // [0,16) keystream of the last ICM block, [16] GCM ok
+};
+
+template <int NR>
+DEV void raw_icm(const RawDev &A, const AesLds &T)
+{
+    GlobalKey rk{ A.key };
+    const uint32_t body = A.len > A.nlead ? A.len - A.nlead : 0;
+    const uint32_t nb = (body + 15) / 16;
+    if (threadIdx.x == 0)
+        for (uint32_t b = 0; b < A.nlead && b < A.len; b++)
+            A.dst[b] = A.src[b] ^ A.lead[b];
+    uint32_t c[4];
+    for (int w = 0; w < 4; w++)
+        c[w] = (uint32_t)A.ctr[4 * w] | (uint32_t)A.ctr[4 * w + 1] << 8 |
+               (uint32_t)A.ctr[4 * w + 2] << 16 | (uint32_t)A.ctr[4 * w + 3] << 24;
+    const uint32_t c16 = (uint32_t)A.ctr[14] << 8 | A.ctr[15];
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) {
+        const uint32_t k = (c16 + j) & 0xffffu;   // the caller checked 0xffff
+        uint32_t x0 = c[0], x1 = c[1], x2 = c[2];
+        uint32_t x3 = (c[3] & 0xffffu) | (k >> 8) << 16 | (k & 0xffu) << 24;
+        aes_block<NR, false>(x0, x1, x2, x3, rk, T);
+        const uint32_t ks[4] = { x0, x1, x2, x3 };
+        const uint32_t o = A.nlead + 16 * j;
+        for (uint32_t b = 0; b < 16 && o + b < A.len; b++)
+            A.dst[o + b] = A.src[o + b] ^ (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+        if (j == nb - 1)
+            for (uint32_t b = 0; b < 16; b++)
+                A.res[b] = (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+// GHASH(aad || data || lengths) and E_K(J0): the 16-byte tag before
+// truncation (SP 800-38D 7.1-7.2)
+template <int NR>
+DEV void raw_gcm_tag(const RawDev &A, const uint8_t *data, uint8_t tag[16],
+                     const AesLds &T)
+{
+    Ghash G;
+    G.xh = G.xl = 0;
+    G.hh = (uint64_t)A.key->h[0] << 32 | A.key->h[1];
+    G.hl = (uint64_t)A.key->h[2] << 32 | A.key->h[3];
+    G.fill = 0;
+    for (uint32_t u = 0; u < A.aad_len; u++)
+        G.put(A.aad[u]);
+    G.flush();
+    for (uint32_t u = 0; u < A.len; u++)
+        G.put(data[u]);
+    G.flush();
+    G.xh ^= (uint64_t)A.aad_len * 8;
+    G.xl ^= (uint64_t)A.len * 8;
+    gf128_mul(G.xh, G.xl, G.hh, G.hl);
+    uint32_t ks[4];
+    gcm_block<NR>(A.key, A.iv, 1, ks, T);
+    for (int u = 0; u < 16; u++) {
+        const uint64_t half = u < 8 ? G.xh : G.xl;
+        tag[u] = (uint8_t)(half >> (56 - 8 * (u & 7))) ^
+                 (uint8_t)(ks[u >> 2] >> (8 * (u & 3)));
+    }
+}
+
+template <int NR>
+DEV void raw_gcm(const RawDev &A, bool seal, const AesLds &T)
+{
+    if (!seal && threadIdx.x == 0) {   // verify before the buffer changes
+        uint8_t tag[16];
+        raw_gcm_tag<NR>(A, A.src, tag, T);
+        uint32_t diff = 0;
+        for (uint32_t u = 0; u < A.tag_len; u++)
+            diff |= tag[u] ^ A.src[A.len + u];
+        A.res[16] = diff == 0;
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; 16 * j < A.len; j += blockDim.x) {
+        uint32_t ks[4];
+        gcm_block<NR>(A.key, A.iv, j + 2, ks, T);
+        for (uint32_t b = 0; b < 16 && 16 * j + b < A.len; b++)
+            A.dst[16 * j + b] =
+                A.src[16 * j + b] ^ (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
+    }
+    __syncthreads();
+    if (seal && threadIdx.x == 0) {
+        uint8_t tag[16];
+        raw_gcm_tag<NR>(A, A.dst, tag, T);
+        for (uint32_t u = 0; u < A.tag_len; u++)
+            A.dst[A.len + u] = tag[u];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_raw(RawDev A)
+{
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    load_aes_tables<false>(s_tab);
+    __syncthreads();
+    const AesLds T = make_aes_lds(s_tab);
+    if (A.op == SRTP_RAW_HMAC) {
+        if (threadIdx.x == 0) {
+            uint32_t oh[5];
+            hmac_sha1_bytes(A.key, A.src, A.len, oh);
+            for (int u = 0; u < 20; u++)
+                A.dst[u] = (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3)));
+        }
+        return;
+    }
+    const uint32_t nr = A.key->rounds;
+    if (A.op == SRTP_RAW_ICM) {
+        if (nr == 10)
+            raw_icm<10>(A, T);
+        else if (nr == 12)
+            raw_icm<12>(A, T);
+        else
+            raw_icm<14>(A, T);
+        return;
+    }
+    const bool seal = A.op == SRTP_RAW_GCM_SEAL;
+    if (nr == 10)
+        raw_gcm<10>(A, seal, T);
+    else
+        raw_gcm<14>(A, seal, T);
+}
+
 }   // namespace
 
 // ===========================================================================
@@ -511,6 +644,7 @@ void srtp_gpu_close(srtp_gpu_t *g)
     (void)hipFree(g->d_ghash);
     (void)hipFree(g->d_rest);
     (void)hipFree(g->d_any);
+    (void)hipFree(g->d_raw);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);
     (void)hipStreamDestroy(g->stream);
@@ -668,5 +802,65 @@ int srtp_gpu_sync(srtp_gpu_t *g, void *stream)
 
 double srtp_gpu_last_kernel_ms(srtp_gpu_t *g) { return g->last_ms; }
 void srtp_gpu_set_timing(srtp_gpu_t *g, int on) { g->timing = on; }
+
+
+int srtp_gpu_raw(srtp_gpu_t *g, srtp_gpu_raw_t *r)
+{
+    // scratch layout: key | src (+ tag) | dst (+ tag) | aad | results
+    const size_t ksz = (sizeof(srtp_dev_key_t) + 255) & ~(size_t)255;
+    const size_t dsz = (r->len + 16 + 255) & ~(size_t)255;
+    const size_t asz = (r->aad_len + 255) & ~(size_t)255;
+    const size_t need = ksz + 2 * dsz + asz + 256;
+    if (r->len > 0xffffff00u || r->aad_len > 0xffffff00u)
+        return srtp_gpu_fail(hipErrorInvalidValue, "raw: buffer too large");
+    if (need > g->raw_cap) {
+        (void)hipFree(g->d_raw);
+        g->d_raw = nullptr;
+        g->raw_cap = 0;
+        HIPCHK(hipMalloc((void **)&g->d_raw, need));
+        g->raw_cap = need;
+    }
+    uint8_t *dk = g->d_raw, *ds = dk + ksz, *dd = ds + dsz, *da = dd + dsz,
+            *dr = da + asz;
+    hipStream_t st = g->stream;
+    HIPCHK(hipMemcpyAsync(dk, r->key, sizeof(srtp_dev_key_t),
+                          hipMemcpyHostToDevice, st));
+    const size_t in_len =
+        r->len + (r->op == SRTP_RAW_GCM_OPEN ? r->tag_len : 0);
+    if (in_len)
+        HIPCHK(hipMemcpyAsync(ds, r->src, in_len, hipMemcpyHostToDevice, st));
+    if (r->aad_len)
+        HIPCHK(hipMemcpyAsync(da, r->aad, r->aad_len, hipMemcpyHostToDevice,
+                              st));
+    HIPCHK(hipMemsetAsync(dr, 0, 32, st));
+    RawDev A = {};
+    A.op = r->op;
+    A.key = (const srtp_dev_key_t *)dk;
+    A.src = ds;
+    A.dst = dd;
+    A.len = (uint32_t)r->len;
+    A.nlead = r->nlead;
+    A.aad_len = (uint32_t)r->aad_len;
+    A.tag_len = r->tag_len;
+    memcpy(A.ctr, r->ctr, 16);
+    memcpy(A.lead, r->lead, 16);
+    memcpy(A.iv, r->iv, 12);
+    A.aad = da;
+    A.res = dr;
+    hipLaunchKernelGGL(k_raw, dim3(1), dim3(256), 0, st, A);
+    HIPCHK(hipGetLastError());
+    const size_t out_len =
+        r->op == SRTP_RAW_HMAC
+            ? 20
+            : r->len + (r->op == SRTP_RAW_GCM_SEAL ? r->tag_len : 0);
+    if (out_len)
+        HIPCHK(hipMemcpyAsync(r->dst, dd, out_len, hipMemcpyDeviceToHost, st));
+    uint8_t res[32];
+    HIPCHK(hipMemcpyAsync(res, dr, 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    memcpy(r->ks_last, res, 16);
+    r->ok = res[16];
+    return 0;
+}
 
 }   // extern "C"

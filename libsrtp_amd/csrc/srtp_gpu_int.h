@@ -32,7 +32,11 @@ struct srtp_gpu {
     size_t rest_cap;  // bytes of d_rest
     uint32_t *d_any;  // = wave_seq when the last wave kernel left a group
     uint32_t wave_seq;
-    int wave_off;     // SRTP_MI355X_WAVE=0: wave kernels disabled
+    int wave_off;     // k_gcm_wave disabled (SRTP_MI355X_WAVE != 1)
+    // single-buffer cipher / auth calls of the crypto-kernel API
+    // (srtp_plugin.c -> srtp_gpu_raw): scratch grown on demand
+    uint8_t *d_raw;
+    size_t raw_cap;
 };
 
 // AES-ICM (+ HMAC-SHA1) kernel arguments

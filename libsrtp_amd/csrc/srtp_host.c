@@ -60,6 +60,14 @@ static void log_msg(srtp_log_level_t lvl, const char *msg)
         fprintf(stderr, "%s", msg);
 }
 
+/* for srtp_plugin.c (srtp_err_report, debug-module listing) */
+void srtp_mi355x_log(int level, const char *msg)
+    __attribute__((visibility("hidden")));
+void srtp_mi355x_log(int level, const char *msg)
+{
+    log_msg((srtp_log_level_t)level, msg);
+}
+
 static void default_event_reporter(srtp_event_data_t *d)
 {
     static const char *what[] = { "SSRC collision",
@@ -2418,11 +2426,11 @@ out:
 }
 
 /* ------------------------------------------------------------------------
- * SRTCP (RFC 3711 3.4) for AES-ICM / null cipher with HMAC-SHA1 / null auth.
- * Host: stream lookup, E-bit / 31-bit index trailer, replay database
- * (crypto/replay/rdb.c).  GPU: keystream, trailer + MKI placement, HMAC and
- * tag verification (k_rtcp).  AEAD SRTCP (srtp.c:3894-4300) is not on the
- * GPU path: srtp_err_status_no_such_op.
+ * SRTCP (RFC 3711 3.4) for AES-ICM / null cipher with HMAC-SHA1 / null auth,
+ * and AEAD SRTCP with AES-GCM-128/256 (srtp.c:3894-4300).  Host: stream
+ * lookup, E-bit / 31-bit index trailer, replay database
+ * (crypto/replay/rdb.c).  GPU (k_rtcp): keystream, trailer + MKI placement,
+ * HMAC-SHA1 or GCM tag, and tag verification.
  * ---------------------------------------------------------------------- */
 #define SRTCP_HDR_LEN 8u          /* octets_in_rtcp_header             */
 #define SRTCP_TRAILER_LEN 4u      /* sizeof(srtcp_trailer_t)           */
@@ -2968,13 +2976,22 @@ const char *srtp_get_version_string(void)
 
 unsigned int srtp_get_version(void) { return (3u << 24) | (0u << 16) | 0u; }
 
+/* the debug-module registry lives with the crypto-kernel registry
+ * (srtp_plugin.c; crypto_kernel.c:210-260) */
+srtp_err_status_t srtp_mi355x_set_debug_module(const char *name, bool v)
+    __attribute__((visibility("hidden")));
+void srtp_mi355x_list_debug_modules(void) __attribute__((visibility("hidden")));
+
 srtp_err_status_t srtp_set_debug_module(const char *mod_name, bool v)
 {
-    (void)v;
-    return mod_name ? srtp_err_status_ok : srtp_err_status_bad_param;
+    return srtp_mi355x_set_debug_module(mod_name, v);
 }
 
-srtp_err_status_t srtp_list_debug_modules(void) { return srtp_err_status_ok; }
+srtp_err_status_t srtp_list_debug_modules(void)
+{
+    srtp_mi355x_list_debug_modules();
+    return srtp_err_status_ok;
+}
 
 static srtp_err_status_t trailer_of(const srtp_stream_ctx_t *s, int is_rtp,
                                     size_t mki_index, size_t *len)

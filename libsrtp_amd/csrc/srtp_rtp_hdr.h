@@ -1,6 +1,8 @@
 // srtp_rtp_hdr.h -- device-side RTP header parse shared by the parse kernel
-// and the device pre-pass.  Follows srtp_get_rtp_hdr_len / the extension
-// walk of srtp/srtp.c:1872-1905 (protect) as restated in oracle/srtp_oracle.c.
+// and the device pre-passes.  Follows srtp_get_rtp_hdr_len (srtp/srtp.c:
+// 96-125: fixed header + CSRCs) and srtp_validate_rtp_header (srtp.c:
+// 307-336: length checks, the one-word extension header and its length) as
+// restated in oracle/srtp_oracle.c.
 #ifndef SRTP_RTP_HDR_H
 #define SRTP_RTP_HDR_H
 

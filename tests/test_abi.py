@@ -21,7 +21,8 @@ def declared_functions():
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     text = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", text)
     names = set()
-    for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\(", text):
+    # a name followed by "(" -- but not "(*": a function-pointer typedef
+    for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\((?!\s*\*)", text):
         name = m.group(1)
         if name.startswith("srtp_") and not name.endswith("_func_t"):
             names.add(name)
