@@ -134,6 +134,14 @@ int main(int argc, char **argv)
     size_t payload = argc > 2 ? strtoull(argv[2], 0, 0) : 1400;
     size_t batch = argc > 3 ? strtoull(argv[3], 0, 0) : 8192;
     size_t chunk = argc > 4 ? strtoull(argv[4], 0, 0) : 64;
+    /* optional: a dump of the master key and of every (RTP sent, SRTP the
+     * sink received) pair, for an independent check of the wire bytes
+     * (tests/test_gpu_udp_relay.py compares them with the oracle) */
+    FILE *dump = argc > 5 ? fopen(argv[5], "wb") : NULL;
+    if (argc > 5 && !dump) {
+        perror(argv[5]);
+        return 2;
+    }
     if (payload + 12 + 64 > MAXPKT || !batch || !chunk) {
         fprintf(stderr, "bad arguments\n");
         return 2;
@@ -158,6 +166,8 @@ int main(int argc, char **argv)
     pol.ssrc.type = ssrc_any_inbound;
     if (srtp_create(&rcv, &pol))
         return 1;
+    if (dump)
+        fwrite(key, 1, sizeof key, dump);
 
     struct sockaddr_in a_src, a_relay, a_sink;
     int f_src = udp_bound(&a_src), f_relay = udp_bound(&a_relay),
@@ -234,6 +244,13 @@ int main(int argc, char **argv)
         if (srtp_unprotect_batch(rcv, n, (const uint8_t *const *)got, glen,
                                  back, blen, st))
             return 9;
+        for (size_t i = 0; dump && i < n; i++) {
+            const uint16_t a = (uint16_t)plen[i], b = (uint16_t)glen[i];
+            fwrite(&a, 2, 1, dump);
+            fwrite(plain[i], 1, a, dump);
+            fwrite(&b, 2, 1, dump);
+            fwrite(got[i], 1, b, dump);
+        }
         for (size_t i = 0; i < n; i++) {
             if (st[i] == 0 && blen[i] == plen[i] &&
                 memcmp(back[i], plain[i], plen[i]) == 0)
@@ -247,6 +264,8 @@ int main(int argc, char **argv)
            "\"relay_s\": %.4f, \"verified\": %zu, \"failed\": %zu}\n",
            total, payload, batch, chunk, t_relay > 0 ? total / t_relay : 0.0,
            t_relay, verified, failed);
+    if (dump)
+        fclose(dump);
     srtp_dealloc(snd);
     srtp_dealloc(rcv);
     close(f_src);
