@@ -28,6 +28,7 @@
  */
 #include "srtp_mi355x.h"
 
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -153,6 +154,10 @@ typedef struct {
     srtp_dev_meta_t *h_meta, *d_meta;
     uint8_t *h_auth, *d_auth;
     srtp_dev_hdr_t *h_hdr, *d_hdr;
+    /* host-buffer batches on the device pre-pass: lengths in, capacities
+     * in / lengths out, statuses out */
+    uint32_t *h_len, *d_len, *h_cap, *d_cap;
+    int32_t *h_st, *d_st;
     size_t n_cap;
 } stage_t;
 
@@ -998,6 +1003,12 @@ static void stage_free(stage_t *st)
     srtp_gpu_free(st->d_auth);
     srtp_gpu_host_free(st->h_hdr);
     srtp_gpu_free(st->d_hdr);
+    srtp_gpu_host_free(st->h_len);
+    srtp_gpu_free(st->d_len);
+    srtp_gpu_host_free(st->h_cap);
+    srtp_gpu_free(st->d_cap);
+    srtp_gpu_host_free(st->h_st);
+    srtp_gpu_free(st->d_st);
     memset(st, 0, sizeof *st);
 }
 
@@ -1635,6 +1646,9 @@ static int stage_reserve(srtp_t ctx, size_t n, size_t arena)
         REALLOC_PAIR(h_meta, d_meta, srtp_dev_meta_t)
         REALLOC_PAIR(h_auth, d_auth, uint8_t)
         REALLOC_PAIR(h_hdr, d_hdr, srtp_dev_hdr_t)
+        REALLOC_PAIR(h_len, d_len, uint32_t)
+        REALLOC_PAIR(h_cap, d_cap, uint32_t)
+        REALLOC_PAIR(h_st, d_st, int32_t)
 #undef REALLOC_PAIR
         st->n_cap = c;
     }
@@ -1696,9 +1710,155 @@ static int run_gpu(srtp_t ctx, int op, size_t n, const uint8_t *in,
 
 static size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
+/* 1 if any mki_index[i] is non-zero (the device pre-pass has no MKI) */
+static int memchr_nonzero(const size_t *v, size_t n)
+{
+    for (size_t i = 0; i < n; i++)
+        if (v[i])
+            return 1;
+    return 0;
+}
+
 /* ------------------------------------------------------------------------
  * batch API over host buffers
  * ---------------------------------------------------------------------- */
+static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b);
+static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b);
+
+/* a parallel for over [0, n) on up to 8 host threads: the gather into and
+ * scatter out of the pinned staging arena of host-buffer batches */
+typedef struct {
+    void (*fn)(void *arg, size_t lo, size_t hi);
+    void *arg;
+    size_t lo, hi;
+} par_job_t;
+
+static void *par_run(void *p)
+{
+    par_job_t *j = (par_job_t *)p;
+    j->fn(j->arg, j->lo, j->hi);
+    return NULL;
+}
+
+static void par_for(size_t n, void (*fn)(void *, size_t, size_t), void *arg)
+{
+    size_t t = n / 16384;
+    if (t > 8)
+        t = 8;
+    if (t < 2) {
+        fn(arg, 0, n);
+        return;
+    }
+    pthread_t th[8];
+    par_job_t jobs[8];
+    size_t started = 0;
+    for (size_t k = 0; k < t; k++) {
+        jobs[k].fn = fn;
+        jobs[k].arg = arg;
+        jobs[k].lo = n * k / t;
+        jobs[k].hi = n * (k + 1) / t;
+        if (k > 0 && pthread_create(&th[k], NULL, par_run, &jobs[k]) == 0)
+            started |= (size_t)1 << k;
+        else if (k > 0)
+            fn(arg, jobs[k].lo, jobs[k].hi);   /* no thread: inline */
+    }
+    fn(arg, jobs[0].lo, jobs[0].hi);
+    for (size_t k = 1; k < t; k++)
+        if (started & ((size_t)1 << k))
+            pthread_join(th[k], NULL);
+}
+
+typedef struct {
+    stage_t *sg;
+    const uint8_t *const *in;
+    const size_t *in_len;
+    uint8_t *const *out;
+    size_t *out_len;
+    const srtp_err_status_t *status;
+    size_t extra; /* slot room after the input: protect's trailer */
+} gather_t;
+
+static void gather_part(void *p, size_t lo, size_t hi)
+{
+    gather_t *g = (gather_t *)p;
+    for (size_t i = lo; i < hi; i++)
+        memcpy(g->sg->h_arena + g->sg->h_off[i], g->in[i], g->in_len[i]);
+}
+
+static void scatter_part(void *p, size_t lo, size_t hi)
+{
+    gather_t *g = (gather_t *)p;
+    for (size_t i = lo; i < hi; i++)
+        if (g->sg->h_st[i] == 0) {
+            memcpy(g->out[i], g->sg->h_arena + g->sg->h_off[i],
+                   g->sg->h_cap[i]);
+            g->out_len[i] = g->sg->h_cap[i];
+        }
+}
+
+/* Host-buffer batch on the device pre-pass: gather into the pinned arena,
+ * one H2D, srtp_{un}protect_device's GPU pre-pass + kernels, one D2H,
+ * scatter.  Returns 1 when done, 0 when the batch must take the host
+ * pre-pass path (nothing was changed), -1 on a device error. */
+static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
+                             const uint8_t *const *in, const size_t *in_len,
+                             uint8_t *const *out, size_t *out_len,
+                             srtp_err_status_t *status)
+{
+    if (n < 64 || n > 0x7fffffffu)
+        return 0;   /* small batches: the host path has less overhead */
+    const size_t extra = unprotect ? 0 : SRTP_MAX_TRAILER_LEN;
+    size_t arena = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (in_len[i] > 0xffff || out_len[i] > 0xffffffffu)
+            return 0;
+        arena += r16(in_len[i] + extra);
+    }
+    if (stage_reserve(ctx, n, arena))
+        return -1;
+    stage_t *sg = &ctx->st;
+    size_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        sg->h_off[i] = off;
+        sg->h_len[i] = (uint32_t)in_len[i];
+        sg->h_cap[i] = (uint32_t)out_len[i];
+        off += r16(in_len[i] + extra);
+    }
+    gather_t g = { sg, in, in_len, out, out_len, status, extra };
+    par_for(n, gather_part, &g);
+    void *hs = HS(ctx);
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_len, sg->h_len, n * 4, hs) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_cap, sg->h_cap, n * 4, hs))
+        return -1;
+    srtp_device_batch_t b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.in = sg->d_arena;
+    b.in_off = sg->d_off;
+    b.in_len = sg->d_len;
+    b.out = sg->d_arena;
+    b.out_off = sg->d_off;
+    b.out_len = sg->d_cap;
+    b.status = sg->d_st;
+    b.stream = hs;
+    int fast = unprotect ? unprotect_device_fast(ctx, &b)
+                         : protect_device_fast(ctx, &b);
+    if (fast <= 0)
+        return fast;
+    ctx->dt.fast_batches++;
+    if (srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, hs) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_cap, sg->d_cap, n * 4, hs) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_st, sg->d_st, n * 4, hs) ||
+        srtp_gpu_sync(ctx->gpu, hs))
+        return -1;
+    par_for(n, scatter_part, &g);
+    for (size_t i = 0; i < n; i++)
+        status[i] = (srtp_err_status_t)sg->h_st[i];
+    return 1;
+}
+
 srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
                                      const uint8_t *const *rtp,
                                      const size_t *rtp_len,
@@ -1708,9 +1868,19 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
-    dev_pull(ctx);
     if (!n)
         return srtp_err_status_ok;
+    if (!mki_index || !memchr_nonzero(mki_index, n)) {
+        int fast = batch_device_fast(ctx, 0, n, rtp, rtp_len, srtp, srtp_len,
+                                     status);
+        if (fast < 0) {
+            log_msg(srtp_log_level_error, srtp_gpu_last_error());
+            return srtp_err_status_fail;
+        }
+        if (fast)
+            return srtp_err_status_ok;
+    }
+    dev_pull(ctx);
     size_t arena = 0;
     for (size_t i = 0; i < n; i++)
         arena += r16(rtp_len[i] + SRTP_MAX_TRAILER_LEN);
@@ -1926,9 +2096,17 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
-    dev_pull(ctx);
     if (!n)
         return srtp_err_status_ok;
+    int fast = batch_device_fast(ctx, 1, n, srtp, srtp_len, rtp, rtp_len,
+                                 status);
+    if (fast < 0) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        return srtp_err_status_fail;
+    }
+    if (fast)
+        return srtp_err_status_ok;
+    dev_pull(ctx);
     size_t arena = 0;
     for (size_t i = 0; i < n; i++)
         arena += r16(srtp_len[i]);

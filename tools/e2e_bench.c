@@ -8,8 +8,11 @@
  *           runs the host pre-pass and the kernels, copies D2H and out)
  *   pinned  the application keeps a pinned packet arena: hipMemcpyAsync H2D,
  *           srtp_protect_device() (GPU pre-pass + kernels), hipMemcpyAsync D2H
+ *   pipelined  the same arena in `chunks` pieces over three HIP streams:
+ *           H2D(k+1) on a copy stream || protect(k) on the compute stream ||
+ *           D2H(k-1) on a second copy stream (PCIe is full duplex)
  *
- *   usage: e2e_bench [packets] [payload] [iters]
+ *   usage: e2e_bench [packets] [payload] [iters] [chunks]
  *   prints one JSON line.
  */
 #include <hip/hip_runtime_api.h>
@@ -83,6 +86,7 @@ int main(int argc, char **argv)
     size_t n = argc > 1 ? strtoul(argv[1], 0, 0) : (1u << 20);
     size_t payload = argc > 2 ? strtoul(argv[2], 0, 0) : 1400;
     int iters = argc > 3 ? atoi(argv[3]) : 5;
+    size_t chunks = argc > 4 ? strtoul(argv[4], 0, 0) : 16;
     size_t len = 12 + payload, slot = (len + 10 + 15) & ~(size_t)15;
     uint8_t key[30];
     for (int i = 0; i < 30; i++)
@@ -154,6 +158,68 @@ int main(int argc, char **argv)
     uint64_t dev_b = 0, host_b = 0;
     srtp_mi355x_prepass_stats(s1, &dev_b, &host_b);
 
+    /* ---- pipelined: chunks over three streams ------------------------- */
+    if (chunks < 1 || n % chunks) {
+        fprintf(stderr, "packets must be a multiple of chunks\n");
+        return 2;
+    }
+    const size_t cn = n / chunks;
+    hipStream_t s_h2d, s_d2h;
+    CHECK(hipStreamCreateWithFlags(&s_h2d, hipStreamNonBlocking));
+    CHECK(hipStreamCreateWithFlags(&s_d2h, hipStreamNonBlocking));
+    hipEvent_t *ev_in = (hipEvent_t *)malloc(chunks * sizeof(hipEvent_t));
+    hipEvent_t *ev_done = (hipEvent_t *)malloc(chunks * sizeof(hipEvent_t));
+    for (size_t k = 0; k < chunks; k++) {
+        CHECK(hipEventCreateWithFlags(&ev_in[k], hipEventDisableTiming));
+        CHECK(hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming));
+    }
+    srtp_t s3 = make_session(key);
+    seq0 = 0x1234;
+    double t_pipe = 0;
+    size_t pipe_bad = 0;
+    for (int it = -1; it < iters; it++) {
+        fill(h_arena, slot, n, len, seq0);
+        seq0 += (uint32_t)n;
+        double t0 = now();
+        for (size_t k = 0; k <= chunks; k++) {
+            if (k < chunks) {   /* stage chunk k in */
+                CHECK(hipMemcpyAsync(d_arena + k * cn * slot,
+                                     h_arena + k * cn * slot, cn * slot,
+                                     hipMemcpyHostToDevice, s_h2d));
+                CHECK(hipMemcpyAsync(d_olen + k * cn, h_cap + k * cn, cn * 4,
+                                     hipMemcpyHostToDevice, s_h2d));
+                CHECK(hipEventRecord(ev_in[k], s_h2d));
+            }
+            if (k == 0)
+                continue;
+            /* protect chunk k-1 while chunk k is in flight */
+            const size_t j = k - 1;
+            CHECK(hipStreamWaitEvent(st, ev_in[j], 0));
+            srtp_device_batch_t c = b;
+            c.n = cn;
+            c.in_off = d_off + j * cn;
+            c.in_len = d_len + j * cn;
+            c.out_off = d_off + j * cn;
+            c.out_len = d_olen + j * cn;
+            c.status = d_st + j * cn;
+            CHECK(srtp_protect_device(s3, &c));
+            CHECK(hipEventRecord(ev_done[j], st));
+            CHECK(hipStreamWaitEvent(s_d2h, ev_done[j], 0));
+            CHECK(hipMemcpyAsync(h_arena + j * cn * slot,
+                                 d_arena + j * cn * slot, cn * slot,
+                                 hipMemcpyDeviceToHost, s_d2h));
+        }
+        CHECK(hipStreamSynchronize(s_d2h));
+        if (it >= 0)
+            t_pipe += now() - t0;
+    }
+    t_pipe /= iters;
+    CHECK(hipMemcpy(h_len, d_olen, n * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < n; i++)
+        pipe_bad += h_len[i] != len + 10;
+    uint64_t dev_p = 0, host_p = 0;
+    srtp_mi355x_prepass_stats(s3, &dev_p, &host_p);
+
     /* ---- libsrtp-shaped batch over host pointers --------------------- */
     srtp_t s2 = make_session(key);
     uint8_t *pk = (uint8_t *)malloc(n * slot);
@@ -190,13 +256,20 @@ int main(int argc, char **argv)
            "\"pinned_device_api\": {\"pkt_per_s\": %.1f, \"ms\": %.3f, "
            "\"algorithmic_GBps\": %.2f, \"pcie_bytes\": %.0f, "
            "\"device_prepass_batches\": %llu, \"host_prepass_batches\": %llu}, "
+           "\"pipelined_device_api\": {\"chunks\": %zu, \"pkt_per_s\": %.1f, "
+           "\"ms\": %.3f, \"pcie_GBps_each_way\": %.2f, "
+           "\"device_prepass_batches\": %llu, \"host_prepass_batches\": %llu, "
+           "\"bad_lengths\": %zu}, "
            "\"host_batch_api\": {\"pkt_per_s\": %.1f, \"ms\": %.3f, "
            "\"algorithmic_GBps\": %.2f}}\n",
            n, payload, iters, n / t_pinned, t_pinned * 1e3,
            bytes / t_pinned / 1e9, 2.0 * n * slot + 8.0 * n,
-           (unsigned long long)dev_b, (unsigned long long)host_b,
+           (unsigned long long)dev_b, (unsigned long long)host_b, chunks,
+           n / t_pipe, t_pipe * 1e3, n * (double)slot / t_pipe / 1e9,
+           (unsigned long long)dev_p, (unsigned long long)host_p, pipe_bad,
            n / t_batch, t_batch * 1e3, bytes / t_batch / 1e9);
     srtp_dealloc(s1);
     srtp_dealloc(s2);
-    return 0;
+    srtp_dealloc(s3);
+    return pipe_bad ? 1 : 0;
 }
