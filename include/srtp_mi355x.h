@@ -389,6 +389,10 @@ void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
                                  uint32_t *launches, uint32_t *undo_launches);
 /* 1 when a HIP device is usable from this process */
 int srtp_mi355x_gpu_available(void);
+/* test hook: uses left on the first session key of stream `ssrc` (host
+ * order), to reach the key-usage soft / hard limits in tests */
+srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
+                                                  uint64_t num_left);
 
 /* ========================================================================
  * The crypto-kernel plugin ABI (srtp.def:46-69): libsrtp's cipher / auth

@@ -13,7 +13,7 @@ from . import srtp as _srtp_mod  # noqa: F401  (re-exported names below)
 from .srtp import (  # noqa: F401
     LIB_PATH, lib, build, Status, Policy, CryptoPolicy, MasterKey,
     SSRC_SPECIFIC, SSRC_ANY_INBOUND, SSRC_ANY_OUTBOUND, Session,
-    policy_setter, DeviceBatch,
+    policy_setter, DeviceBatch, EventData, install_event_handler,
 )
 
 # fail loudly at import when the HIP library is absent: there is no fallback

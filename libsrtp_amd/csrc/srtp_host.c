@@ -3276,6 +3276,24 @@ void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
         *undo_launches = ctx->ustat.undo_launches;
 }
 
+/* Test hook: the number of uses left on the first session key of stream
+ * `ssrc` (host order) -- what a test of the reference writes into the
+ * stream's srtp_key_limit_ctx_t to reach the soft / hard limits (key.c:74-90)
+ * without 2^48 packets. */
+srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
+                                                  uint64_t num_left)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    dev_pull(ctx);
+    srtp_stream_ctx_t *st = map_get(ctx, ssrc);
+    if (!st)
+        return srtp_err_status_no_ctx;
+    st->keys->k[0].num_left = num_left;
+    ctx->dt.valid = 0;   /* the device table's key bound is stale */
+    return srtp_err_status_ok;
+}
+
 uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx)
 {
     return ctx ? ctx->dt.sorted_batches : 0;

@@ -148,6 +148,8 @@ def lib():
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
         "srtp_mi355x_prepass_sorted_batches": ([P], C.c_uint64),
+        "srtp_mi355x_debug_set_key_limit": ([P, C.c_uint32, C.c_uint64],
+                                            C.c_int),
         "srtp_mi355x_unprotect_stats": ([P] + [C.POINTER(C.c_uint32)] * 3,
                                         None),
 
@@ -222,6 +224,29 @@ class _PolicyHolder:
             self.keep.append(kb)
             p.key = C.cast(kb, C.c_void_p)
         self.policy = p
+
+
+class EventData(C.Structure):
+    """srtp_event_data_t (include/srtp.h:1690-1700)"""
+    _fields_ = [("session", C.c_void_p), ("ssrc", C.c_uint32),
+                ("event", C.c_int)]
+
+
+EVENT_HANDLER = C.CFUNCTYPE(None, C.POINTER(EventData))
+_handler_keep = []
+
+
+def install_event_handler(fn):
+    """srtp_install_event_handler: fn(event, ssrc) per event; None removes"""
+    L = lib()
+    L.srtp_install_event_handler.argtypes = [C.c_void_p]
+    L.srtp_install_event_handler.restype = C.c_int
+    if fn is None:
+        _handler_keep.clear()
+        return L.srtp_install_event_handler(None)
+    cb = EVENT_HANDLER(lambda p: fn(p.contents.event, p.contents.ssrc))
+    _handler_keep[:] = [cb]
+    return L.srtp_install_event_handler(C.cast(cb, C.c_void_p))
 
 
 class Session:
@@ -395,6 +420,10 @@ class Session:
         d, h = C.c_uint64(), C.c_uint64()
         self.L.srtp_mi355x_prepass_stats(self.h, C.byref(d), C.byref(h))
         return d.value, h.value
+
+    def debug_set_key_limit(self, ssrc, num_left):
+        return Status(self.L.srtp_mi355x_debug_set_key_limit(self.h, ssrc,
+                                                             num_left))
 
     def prepass_sorted_batches(self):
         """device pre-pass batches that needed the sorted chain path"""

@@ -692,6 +692,165 @@ static size_t unhex(const char *h, uint8_t *out)
     return n;
 }
 
+/* ---------------------------------------------------------------------- */
+/* Key-usage limit and SSRC-collision events (srtp.c:1723-1773, key.c:74-90)
+ * with the reference's own bookkeeping: the key limit is lowered by
+ * writing the stream's srtp_key_limit_ctx_t (srtp_priv.h) -- reaching 2^48
+ * packets is not practical -- and every event srtp_handle_event raises
+ * during an op is recorded with it.                                        */
+static int g_nev;
+static uint32_t g_ev[16][2];
+
+static void ev_handler(srtp_event_data_t *d)
+{
+    if (g_nev < 16) {
+        g_ev[g_nev][0] = (uint32_t)d->event;
+        g_ev[g_nev][1] = d->ssrc;
+        g_nev++;
+    }
+}
+
+static void ev_emit_tail(void)
+{
+    fputs(", \"events\": [", g_out);
+    for (int i = 0; i < g_nev; i++)
+        fprintf(g_out, "%s[%u, %u]", i ? ", " : "", g_ev[i][0], g_ev[i][1]);
+    fputs("]}", g_out);
+    g_nev = 0;
+}
+
+/* emit_op without its closing brace, then the events */
+static void ev_op(pair_t *pp, const char *sess, const char *op,
+                  const uint8_t *in, size_t len, size_t cap)
+{
+    uint8_t out[2200];
+    size_t olen = cap;
+    memset(out, 0, sizeof out);
+    g_nev = 0;
+    srtp_t s = sess[0] == 's' ? pp->snd : pp->rcv;
+    srtp_err_status_t st = op[0] == 'p'
+                               ? srtp_protect(s, in, len, out, &olen, 0)
+                               : srtp_unprotect(s, in, len, out, &olen);
+    item_begin();
+    fprintf(g_out, "\"sess\": \"%s\", \"op\": \"%s\", \"in\": ", sess, op);
+    hex(in, len);
+    fprintf(g_out, ", \"cap\": %zu, \"mki_index\": 0, \"status\": %d, "
+                   "\"out\": ", cap, (int)st);
+    if (st == 0)
+        hex(out, olen);
+    else
+        fputs("null", g_out);
+    ev_emit_tail();
+    if (st == 0 && op[0] == 'p') {
+        memcpy(pp->last_srtp, out, olen);
+        pp->last_len = olen;
+    }
+}
+
+static void ev_set_limit(pair_t *pp, const char *sess, uint32_t ssrc,
+                         uint64_t num_left)
+{
+    srtp_t s = sess[0] == 's' ? pp->snd : pp->rcv;
+    srtp_stream_t st = srtp_get_stream(s, htonl(ssrc));
+    if (!st) {
+        fprintf(stderr, "gen_events: no stream %08x\n", ssrc);
+        exit(1);
+    }
+    st->session_keys[0].limit->num_left = num_left;
+    item_begin();
+    fprintf(g_out, "\"sess\": \"%s\", \"op\": \"set_limit\", "
+                   "\"ssrc\": %u, \"num_left\": %llu, \"events\": []}",
+            sess, ssrc, (unsigned long long)num_left);
+}
+
+static void gen_events_case(const char *name, void (*set)(srtp_crypto_policy_t *),
+                            int first)
+{
+    const uint32_t X = 0x5eedf00d;
+    srtp_policy_t ps, pr;
+    uint8_t keys[1][64], mkis[1][16];
+    memset(&ps, 0, sizeof ps);
+    set(&ps.rtp);
+    set(&ps.rtcp);
+    rfill(keys[0], 64);
+    ps.key = keys[0];
+    ps.ssrc.type = ssrc_specific;
+    ps.ssrc.value = X;
+    ps.window_size = 128;
+    pr = ps;
+    pair_t pp;
+    if (srtp_create(&pp.snd, &ps) || srtp_create(&pp.rcv, &pr))
+        exit(1);
+    fprintf(g_out, "%s    {\"name\": \"%s\", \"snd\": ", first ? "" : ",\n",
+            name);
+    emit_policy(&ps, keys, mkis, 1);
+    fputs(", \"rcv\": ", g_out);
+    emit_policy(&pr, keys, mkis, 1);
+    fputs(", \"ops\": [", g_out);
+    g_first_item = 1;
+    uint8_t rtp[300], sent[12][300];
+    size_t sent_len[12];
+    uint16_t seq = 0x2000;
+    /* sender: across the soft limit, then the hard limit (and past it) */
+    ev_set_limit(&pp, "snd", X, 0x10000 + 2);
+    for (int i = 0; i < 5; i++) {
+        size_t len = build_rtp(rtp, X, seq++, 0, 0, -1, 40 + i);
+        ev_op(&pp, "snd", "protect", rtp, len, len + 32);
+        memcpy(sent[i], pp.last_srtp, pp.last_len);
+        sent_len[i] = pp.last_len;
+    }
+    ev_set_limit(&pp, "snd", X, 2);
+    for (int i = 5; i < 9; i++) {
+        size_t len = build_rtp(rtp, X, seq++, 0, 0, -1, 40 + i);
+        ev_op(&pp, "snd", "protect", rtp, len, len + 32);
+        memcpy(sent[i], pp.last_srtp, pp.last_len);
+        sent_len[i] = pp.last_len;
+    }
+    /* receiver: a lowered limit, a tampered packet (AES-GCM counts it, the
+     * HMAC path does not), then the soft limit */
+    ev_op(&pp, "rcv", "unprotect", sent[0], sent_len[0], sent_len[0]);
+    ev_set_limit(&pp, "rcv", X, 0x10000 + 1);
+    {
+        uint8_t bad[300];
+        memcpy(bad, sent[1], sent_len[1]);
+        bad[sent_len[1] - 1] ^= 1;
+        ev_op(&pp, "rcv", "unprotect", bad, sent_len[1], sent_len[1]);
+    }
+    for (int i = 1; i < 5; i++)
+        ev_op(&pp, "rcv", "unprotect", sent[i], sent_len[i], sent_len[i]);
+    ev_set_limit(&pp, "rcv", X, 1);
+    ev_op(&pp, "rcv", "unprotect", sent[5], sent_len[5], sent_len[5]);
+    /* SSRC collision: the receiver's stream used to send, the sender's to
+     * receive (srtp.c:2607-2623, 3104-3121) */
+    {
+        size_t len = build_rtp(rtp, X, 0x3000, 0, 0, -1, 20);
+        ev_op(&pp, "rcv", "protect", rtp, len, len + 32);
+        ev_op(&pp, "snd", "unprotect", pp.last_srtp, pp.last_len,
+              pp.last_len);
+    }
+    fputs("\n    ]}", g_out);
+    srtp_dealloc(pp.snd);
+    srtp_dealloc(pp.rcv);
+}
+
+static void gen_events(void)
+{
+    srtp_install_event_handler(ev_handler);
+    fputs(",\n  \"events\": [\n", g_out);
+#ifndef REF_OSSL
+    gen_events_case("events_icm128_hmac80", srtp_crypto_policy_set_rtp_default,
+                    1);
+    gen_events_case("events_icm256_hmac32",
+                    srtp_crypto_policy_set_aes_cm_256_hmac_sha1_32, 0);
+#else
+    gen_events_case("events_gcm128_16",
+                    srtp_crypto_policy_set_aes_gcm_128_16_auth, 1);
+    gen_events_case("events_gcm256_8", set_gcm_256_8, 0);
+#endif
+    fputs("\n  ]", g_out);
+    srtp_install_event_handler(NULL);
+}
+
 static void kat_fail(const kat_t *k, const char *what)
 {
     fprintf(stderr, "reference build fails %s (%s): %s\n", k->name, k->cite,
@@ -871,6 +1030,7 @@ int main(int argc, char **argv)
 #endif
     fputs("\n  ]", g_out);
     gen_kats();
+    gen_events();
     fputs("\n}\n", g_out);
     fclose(g_out);
     srtp_shutdown();
