@@ -27,6 +27,11 @@ enum {
     SRTP_DEV_GCM = 2
 };
 
+/* srtp_dev_key_t.xflags: RFC 6904 header-extension encryption (the ICM key
+ * in slot xslot, IDs in xids) and RFC 9335 cryptex (srtp.c:135-305) */
+enum { SRTP_XF_XTN = 1, SRTP_XF_CRYPTEX = 2,
+       SRTP_XF_CONF = 4 /* the stream's RTP services include confidentiality */ };
+
 typedef struct srtp_dev_key {
     uint32_t rk[60];    /* AES round keys, little-endian words of the bytes */
     uint32_t salt[4];   /* ICM: 14-byte salt || 00 00; GCM: 12-byte salt   */
@@ -39,10 +44,12 @@ typedef struct srtp_dev_key {
     uint32_t mki_size;  /* bytes of MKI on the wire (0 if not used)          */
     uint32_t conf;      /* 1 = payload encrypted (sec_serv_conf)             */
     uint32_t ghash_slot;/* index into the GHASH table arena (GCM only)       */
-    uint32_t pad0;
+    uint32_t xslot;     /* slot of the header-extension ICM key (SRTP_XF_XTN) */
     uint32_t h[4];      /* GCM hash subkey E_K(0^128), big-endian words      */
     uint8_t mki[128];
-    uint32_t pad1[10];
+    uint32_t xids[8];   /* bitmap of the extension IDs to encrypt (0..255)  */
+    uint32_t xflags;    /* SRTP_XF_*                                         */
+    uint32_t pad1;
 } srtp_dev_key_t;
 
 /* per-packet work descriptor written by the pre-pass */
@@ -60,6 +67,18 @@ typedef struct srtp_dev_meta {
 /* kernel variant id: family*8 + rounds_code*2 + auth, rounds_code 0 null,
  * 1 AES-128, 2 AES-192, 3 AES-256 */
 #define SRTP_VARIANT(fam, rc, au) ((uint32_t)((fam) * 8 + (rc) * 2 + (au)))
+/* streams with header-extension encryption or cryptex: every packet goes to
+ * the byte-wise k_xrtp (any family / key size); meta.info bit 0 is then the
+ * caller's in-place flag (rtp == srtp in srtp_protect's terms) and bit 1
+ * (undo only) says the run being undone applied cryptex */
+#define SRTP_VARIANT_X 24u
+#define SRTP_XI_INPLACE 1u
+#define SRTP_XI_CRYPTEX 2u
+/* k_xrtp result byte (auth_ok[i]): bit 0 authenticated (unprotect) / done,
+ * bit 1 output written, bit 2 cryptex applied, bit 3 parse error of the
+ * header extension (srtp_process_header_encryption / srtp_cryptex_protect) */
+enum { SRTP_XR_OK = 1, SRTP_XR_WROTE = 2, SRTP_XR_CRYPTEX = 4,
+       SRTP_XR_PARSE = 8 };
 
 /* compact header summary produced by the device parse kernel */
 typedef struct srtp_dev_hdr {
@@ -67,6 +86,7 @@ typedef struct srtp_dev_hdr {
     uint32_t seq_len;   /* [15:0] seq, [31:16] reserved                      */
     uint32_t enc_start; /* header length incl. extension, or error code<<24 */
     uint32_t len;       /* packet length                                     */
+    uint32_t xinfo;     /* [15:0] extension profile, [19:16] CC, bit 20 X    */
 } srtp_dev_hdr_t;
 
 /* ---- thin FFI implemented in HIP (srtp_gpu.hip) ----------------------- */

@@ -52,6 +52,11 @@ DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
     }
 }
 
+// header-extension / cryptex packets (k_xrtp, below): undo of an unprotect
+DEV uint8_t xrtp_unprotect(const srtp_dev_key_t *keys, const srtp_dev_meta_t &m,
+                           const uint8_t *src, uint8_t *p, bool undo,
+                           const AesLds &T);
+
 __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
                                               const uint64_t *off,
                                               const srtp_dev_meta_t *meta,
@@ -68,10 +73,14 @@ __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
     if (SRTP_META_STATUS(m.info))
         return;
     const srtp_dev_key_t *key = keys + m.key;
-    if (!key->conf || key->family == SRTP_DEV_NULL)
-        return;
     const AesLds T = make_aes_lds(s_tab);
     uint8_t *p = arena + off[i];
+    if (SRTP_META_VARIANT(m.info) == SRTP_VARIANT_X) {
+        xrtp_unprotect(keys, m, p, p, true, T);
+        return;
+    }
+    if (!key->conf || key->family == SRTP_DEV_NULL)
+        return;
     if (key->rounds == 10)
         undo_one<10>(key, m, p, T);
     else if (key->rounds == 12)
@@ -86,22 +95,27 @@ __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
 // the RTP kernel's pieces: AES-ICM keystream over [8, P), the E|index trailer
 // at P, MKI, HMAC-SHA1 over [0, P + 4).
 
-// HMAC-SHA1 over msg[0, L) (hmac.c:157-229; no ROC suffix for SRTCP)
+// HMAC-SHA1 over msg[0, L) || tail[0, nt) (hmac.c:157-229; SRTCP has no
+// tail, SRTP's is the big-endian ROC)
 DEV void hmac_sha1_bytes(const srtp_dev_key_t *key, const uint8_t *msg,
-                         uint32_t L, uint32_t oh[5])
+                         uint32_t L, uint32_t oh[5],
+                         const uint8_t *tail = nullptr, uint32_t nt = 0)
 {
     uint32_t h[5];
     for (int k = 0; k < 5; k++)
         h[k] = key->ipad[k];
-    const uint32_t nb = (L + 1 + 8 + 63) / 64;   // data, 0x80, 64-bit length
-    const uint32_t bits = (64 + L) * 8;          // the ipad block counts
+    const uint32_t M = L + nt;
+    const uint32_t nb = (M + 1 + 8 + 63) / 64;   // data, 0x80, 64-bit length
+    const uint32_t bits = (64 + M) * 8;          // the ipad block counts
     for (uint32_t b = 0; b < nb; b++) {
         uint32_t w[16];
         for (int t = 0; t < 16; t++) {
             uint32_t v = 0;
             for (int u = 0; u < 4; u++) {
                 const uint32_t o = 64 * b + 4 * t + u;
-                const uint32_t c = o < L ? msg[o] : (o == L ? 0x80u : 0u);
+                const uint32_t c = o < L   ? msg[o]
+                                   : o < M ? tail[o - L]
+                                           : (o == M ? 0x80u : 0u);
                 v = (v << 8) | c;
             }
             w[t] = v;
@@ -510,6 +524,431 @@ __global__ __launch_bounds__(256) void k_raw(RawDev A)
         raw_gcm<14>(A, seal, T);
 }
 
+// ---------------------------------------------------------------------------
+// RFC 6904 header-extension encryption and RFC 9335 cryptex.  Streams with
+// either feature send every packet here (SRTP_VARIANT_X): one lane per
+// packet, byte-wise, any family and key size.  It follows srtp_protect
+// (srtp.c:2642-2818) / srtp_protect_aead (2163-2267) and srtp_unprotect
+// (2984-3106) / srtp_unprotect_aead (2360-2423) from the header copy on; the
+// host pre-pass did the rest (index, replay, key limit, cryptex_err and the
+// header-length parse errors).  These are uncommon per-stream options, so
+// this path is written for exactness, not rate.
+
+DEV void aes_rt(const srtp_dev_key_t *k, uint32_t x[4], const AesLds &T)
+{
+    GlobalKey rk{ k };
+    if (k->rounds == 10)
+        aes_block<10, false>(x[0], x[1], x[2], x[3], rk, T);
+    else if (k->rounds == 12)
+        aes_block<12, false>(x[0], x[1], x[2], x[3], rk, T);
+    else
+        aes_block<14, false>(x[0], x[1], x[2], x[3], rk, T);
+}
+
+// the keystream of one SRTP counter mode, consumed a byte at a time (the
+// reference's srtp_cipher_output / encrypt calls continue one stream)
+struct Kstream {
+    const srtp_dev_key_t *key;
+    uint32_t c[4];      // counter block, little-endian words
+    uint32_t ks[4];
+    uint32_t j, pos;    // next block number, bytes of ks used
+    bool gcm, null;
+
+    // AES-ICM, IV 0^4 || SSRC || ROC || SEQ || 0^2 xor the salt, 16-bit
+    // block counter in bytes 14..15 (srtp.c:2694-2707, aes_icm.c:236-282);
+    // the null cipher's keystream is zero
+    DEV void icm(const srtp_dev_key_t *k, const uint8_t *hdr, uint32_t roc)
+    {
+        key = k;
+        gcm = false;
+        null = k->family == SRTP_DEV_NULL;
+        const uint32_t seq = (uint32_t)hdr[2] << 8 | hdr[3];
+        c[0] = k->salt[0];
+        c[1] = k->salt[1] ^ ((uint32_t)hdr[8] | (uint32_t)hdr[9] << 8 |
+                             (uint32_t)hdr[10] << 16 | (uint32_t)hdr[11] << 24);
+        c[2] = k->salt[2] ^ bswap(roc);
+        c[3] = k->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
+        j = 0;
+        pos = 16;
+    }
+
+    // AES-GCM counter blocks IV || be32(2 + i), IV = salt ^ (00 00 || SSRC ||
+    // ROC || SEQ) (RFC 7714 8.1, srtp.c:1896-1950)
+    DEV void aead(const srtp_dev_key_t *k, const uint8_t *hdr, uint32_t roc)
+    {
+        key = k;
+        gcm = true;
+        null = false;
+        const uint8_t *salt = (const uint8_t *)k->salt;
+        uint8_t iv[12];
+        for (int u = 0; u < 12; u++)
+            iv[u] = salt[u];
+        for (int u = 0; u < 4; u++) {
+            iv[2 + u] ^= hdr[8 + u];
+            iv[6 + u] ^= (uint8_t)(roc >> (24 - 8 * u));
+        }
+        iv[10] ^= hdr[2];
+        iv[11] ^= hdr[3];
+        for (int w = 0; w < 3; w++)
+            c[w] = (uint32_t)iv[4 * w] | (uint32_t)iv[4 * w + 1] << 8 |
+                   (uint32_t)iv[4 * w + 2] << 16 | (uint32_t)iv[4 * w + 3] << 24;
+        c[3] = 0;
+        j = 2;
+        pos = 16;
+    }
+
+    DEV void block(uint32_t b, uint32_t out[4], const AesLds &T) const
+    {
+        out[0] = c[0];
+        out[1] = c[1];
+        out[2] = c[2];
+        out[3] = gcm ? bswap(b)
+                     : c[3] ^ (((b >> 8) & 0xffu) << 16) ^ ((b & 0xffu) << 24);
+        if (null)
+            out[0] = out[1] = out[2] = out[3] = 0;
+        else
+            aes_rt(key, out, T);
+    }
+
+    DEV uint8_t next(const AesLds &T)
+    {
+        if (pos == 16) {
+            block(j++, ks, T);
+            pos = 0;
+        }
+        const uint8_t b = (uint8_t)(ks[pos >> 2] >> (8 * (pos & 3)));
+        pos++;
+        return b;
+    }
+};
+
+// RTP header geometry: CSRC count, X bit, fixed + CSRC length, extension
+// end, and the enc_start of a packet without cryptex
+struct XGeo {
+    uint32_t cc, x, hl, xend;
+};
+
+DEV XGeo xgeo(const uint8_t *p)
+{
+    XGeo g;
+    g.cc = p[0] & 15u;
+    g.x = (p[0] >> 4) & 1u;
+    g.hl = 12 + 4 * g.cc;
+    g.xend = g.x ? g.hl + 4 + 4 * ((uint32_t)p[g.hl + 2] << 8 | p[g.hl + 3])
+                 : g.hl;
+    return g;
+}
+
+// the encrypted byte ranges in keystream order: cryptex takes the CSRCs,
+// the extension data and the payload (srtp.c:135-226, the in-place form
+// moves the extension header word out of the way; the not-in-place form
+// encrypts the CSRCs first), otherwise the payload after the header
+DEV uint32_t xsegs(const XGeo &g, bool crx, uint32_t L, uint32_t lo[3],
+                   uint32_t hi[3])
+{
+    if (!crx) {
+        lo[0] = g.xend;
+        hi[0] = L;
+        return 1;
+    }
+    lo[0] = 12;
+    hi[0] = g.hl;
+    lo[1] = g.hl + 4;
+    hi[1] = g.xend;
+    lo[2] = g.xend;
+    hi[2] = L;
+    return 3;
+}
+
+DEV bool xtn_selected(const srtp_dev_key_t *k, uint32_t id)
+{
+    return (k->xids[id >> 5] >> (id & 31u)) & 1u;   // srtp.c:1776-1797
+}
+
+// srtp_process_header_encryption (srtp.c:1802-1894): walk the RFC 8285
+// elements of the extension at p + xo (one-byte 0xBEDE or two-byte 0x100x
+// profile), consuming the extension keystream per element (header bytes
+// included); with `apply` XOR the data of the selected IDs.  Padding bytes
+// are skipped without keystream; a one-byte ID 15 ends the walk.  Element
+// header bytes are never encrypted, so the walk is the same both ways.
+// false = parse error.
+DEV bool xtn_walk(const srtp_dev_key_t *k, const srtp_dev_key_t *keys,
+                  uint8_t *p, uint32_t xo, uint32_t xend, uint32_t roc,
+                  bool apply, const AesLds &T)
+{
+    const uint32_t prof = (uint32_t)p[xo] << 8 | p[xo + 1];
+    const bool one = prof == 0xBEDEu;
+    if (!one && (prof & 0xfff0u) != 0x1000u)
+        return false;
+    Kstream K;
+    K.icm(keys + k->xslot, p, roc);
+    uint32_t d = xo + 4;
+    while (one ? d < xend : d + 1 < xend) {
+        uint32_t id, len;
+        const uint32_t hb = one ? 1u : 2u;
+        if (one) {
+            id = p[d] >> 4;
+            len = (p[d] & 15u) + 1;
+        } else {
+            id = p[d];
+            len = p[d + 1];
+        }
+        d += hb;
+        if (d + len > xend)
+            return false;
+        if (one && id == 15)
+            break;
+        if (apply) {
+            const bool sel = (one || len > 0) && xtn_selected(k, id);
+            for (uint32_t u = 0; u < hb; u++)
+                K.next(T);
+            for (uint32_t u = 0; u < len; u++) {
+                const uint8_t b = K.next(T);
+                if (sel)
+                    p[d + u] ^= b;
+            }
+        }
+        d += len;
+        while (d < xend && p[d] == 0)
+            d++;
+    }
+    return true;
+}
+
+// GHASH(aad || ciphertext || lengths) ^ E_K(J0) over the packet's AAD
+// ranges and encrypted ranges (which already hold ciphertext)
+DEV void xrtp_gcm_tag(const srtp_dev_key_t *k, const Kstream &K,
+                      const uint8_t *p, const XGeo &g, bool crx,
+                      const uint32_t lo[3], const uint32_t hi[3], uint32_t ns,
+                      uint8_t tag[16], const AesLds &T)
+{
+    Ghash G;
+    G.xh = G.xl = 0;
+    G.hh = (uint64_t)k->h[0] << 32 | k->h[1];
+    G.hl = (uint64_t)k->h[2] << 32 | k->h[3];
+    G.fill = 0;
+    // AAD: the header up to enc_start; with cryptex the fixed header and
+    // the extension header word (srtp.c:2234-2241, 2391-2398)
+    uint32_t alen;
+    if (crx) {
+        for (uint32_t u = 0; u < 12; u++)
+            G.put(p[u]);
+        for (uint32_t u = 0; u < 4; u++)
+            G.put(p[g.hl + u]);
+        alen = 16;
+    } else {
+        for (uint32_t u = 0; u < g.xend; u++)
+            G.put(p[u]);
+        alen = g.xend;
+    }
+    G.flush();
+    uint32_t clen = 0;
+    for (uint32_t s = 0; s < ns; s++) {
+        for (uint32_t u = lo[s]; u < hi[s]; u++)
+            G.put(p[u]);
+        clen += hi[s] - lo[s];
+    }
+    G.flush();
+    G.xh ^= (uint64_t)alen * 8;
+    G.xl ^= (uint64_t)clen * 8;
+    gf128_mul(G.xh, G.xl, G.hh, G.hl);
+    uint32_t e[4];
+    K.block(1, e, T);   // E_K(J0)
+    for (int u = 0; u < 16; u++) {
+        const uint64_t half = u < 8 ? G.xh : G.xl;
+        tag[u] = (uint8_t)(half >> (56 - 8 * (u & 7))) ^
+                 (uint8_t)(e[u >> 2] >> (8 * (u & 3)));
+    }
+}
+
+DEV void roc_be(uint32_t roc, uint8_t r[4])
+{
+    r[0] = (uint8_t)(roc >> 24);
+    r[1] = (uint8_t)(roc >> 16);
+    r[2] = (uint8_t)(roc >> 8);
+    r[3] = (uint8_t)roc;
+}
+
+DEV uint8_t xrtp_protect(const srtp_dev_key_t *keys, const srtp_dev_meta_t &m,
+                         const uint8_t *src, uint8_t *p, const AesLds &T)
+{
+    const srtp_dev_key_t *k = keys + m.key;
+    const uint32_t L = m.len;
+    if (src != p)
+        for (uint32_t u = 0; u < L; u++)
+            p[u] = src[u];
+    const XGeo g = xgeo(p);
+    const bool inplace = (m.info & SRTP_XI_INPLACE) != 0;
+    const bool crx = (k->xflags & SRTP_XF_CRYPTEX) &&
+                     (k->xflags & SRTP_XF_CONF) && g.x;
+    if (g.x && (k->xflags & SRTP_XF_XTN)) {
+        // not in place, cryptex encrypts the caller's plaintext extension
+        // (srtp.c:2766-2768, 2245-2246): only the walk's verdict remains
+        if (!xtn_walk(k, keys, p, g.hl, g.xend, m.roc, !(crx && !inplace), T))
+            return SRTP_XR_PARSE;
+    }
+    if (crx) {   // srtp_cryptex_protect (srtp.c:195-208)
+        const uint32_t prof = (uint32_t)p[g.hl] << 8 | p[g.hl + 1];
+        if (prof == 0xBEDEu) {
+            p[g.hl] = 0xC0;
+            p[g.hl + 1] = 0xDE;
+        } else if (prof == 0x1000u) {
+            p[g.hl] = 0xC2;
+            p[g.hl + 1] = 0xDE;
+        } else {
+            return SRTP_XR_PARSE;
+        }
+    }
+    uint32_t lo[3], hi[3];
+    const uint32_t ns = xsegs(g, crx, L, lo, hi);
+    const uint32_t mki = k->mki_size, TL = k->tag_len;
+    Kstream K;
+    if (k->family == SRTP_DEV_GCM) {
+        K.aead(k, p, m.roc);
+        for (uint32_t s = 0; s < ns; s++)
+            for (uint32_t u = lo[s]; u < hi[s]; u++)
+                p[u] ^= K.next(T);
+        uint8_t tag[16];
+        xrtp_gcm_tag(k, K, p, g, crx, lo, hi, ns, tag, T);
+        for (uint32_t u = 0; u < TL; u++)
+            p[L + u] = tag[u];
+        for (uint32_t u = 0; u < mki; u++)
+            p[L + TL + u] = k->mki[u];
+    } else {
+        if (k->conf && k->family == SRTP_DEV_ICM) {
+            K.icm(k, p, m.roc);
+            for (uint32_t s = 0; s < ns; s++)
+                for (uint32_t u = lo[s]; u < hi[s]; u++)
+                    p[u] ^= K.next(T);
+        }
+        for (uint32_t u = 0; u < mki; u++)
+            p[L + u] = k->mki[u];
+        if (k->auth) {   // HMAC over the packet, then the ROC (srtp.c:2785-2815)
+            uint8_t r[4];
+            roc_be(m.roc, r);
+            uint32_t oh[5];
+            hmac_sha1_bytes(k, p, L, oh, r, 4);
+            for (uint32_t u = 0; u < TL; u++)
+                p[L + mki + u] = (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3)));
+        }
+    }
+    return SRTP_XR_OK | SRTP_XR_WROTE | (crx ? SRTP_XR_CRYPTEX : 0);
+}
+
+// unprotect: verify on the input, then write the output.  `undo` re-applies
+// a run's transform to its output (XOR is its own inverse; the profile goes
+// back to the cryptex one) so a speculative run at a wrong index can be
+// taken back (k_undo).
+DEV uint8_t xrtp_unprotect(const srtp_dev_key_t *keys, const srtp_dev_meta_t &m,
+                           const uint8_t *src, uint8_t *p, bool undo,
+                           const AesLds &T)
+{
+    const srtp_dev_key_t *k = keys + m.key;
+    const uint32_t L = m.len;
+    const XGeo g = xgeo(src);
+    const bool inplace = (m.info & SRTP_XI_INPLACE) != 0;
+    const uint32_t prof = g.x ? ((uint32_t)src[g.hl] << 8 | src[g.hl + 1]) : 0;
+    // srtp_cryptex_unprotect_init (srtp.c:237-265): by the profile on the
+    // wire
+    const bool crx = undo ? (m.info & SRTP_XI_CRYPTEX) != 0
+                          : (k->xflags & SRTP_XF_CRYPTEX) && g.x &&
+                                (prof == 0xC0DEu || prof == 0xC2DEu);
+    const bool gcm = k->family == SRTP_DEV_GCM;
+    uint32_t lo[3], hi[3];
+    const uint32_t ns = xsegs(g, crx, L, lo, hi);
+    Kstream K;
+    if (gcm)
+        K.aead(k, src, m.roc);
+    else
+        K.icm(k, src, m.roc);
+    if (!undo) {
+        const uint32_t mki = k->mki_size, TL = k->tag_len;
+        uint32_t diff = 0;
+        if (gcm) {
+            uint8_t tag[16];
+            xrtp_gcm_tag(k, K, src, g, crx, lo, hi, ns, tag, T);
+            for (uint32_t u = 0; u < TL; u++)
+                diff |= tag[u] ^ src[L + u];
+        } else if (k->auth) {
+            uint8_t r[4];
+            roc_be(m.roc, r);
+            uint32_t oh[5];
+            hmac_sha1_bytes(k, src, L, oh, r, 4);
+            for (uint32_t u = 0; u < TL; u++)
+                diff |= src[L + mki + u] ^
+                        ((oh[u >> 2] >> (24 - 8 * (u & 3))) & 0xffu);
+        }
+        if (diff)
+            return 0;
+        // the extension walk runs on the still-cryptex profile and fails
+        // (srtp.c:3073-3080, 2409-2418)
+        if (g.x && (k->xflags & SRTP_XF_XTN) &&
+            (crx || !xtn_walk(k, keys, const_cast<uint8_t *>(src), g.hl,
+                              g.xend, m.roc, false, T)))
+            return SRTP_XR_OK | SRTP_XR_PARSE;
+        if (src != p)
+            for (uint32_t u = 0; u < L; u++)
+                p[u] = src[u];
+    }
+    if (g.x && (k->xflags & SRTP_XF_XTN) && !crx)
+        xtn_walk(k, keys, p, g.hl, g.xend, m.roc, true, T);
+    if (gcm || (k->conf && k->family == SRTP_DEV_ICM)) {
+        for (uint32_t s = 0; s < ns; s++)
+            for (uint32_t u = lo[s]; u < hi[s]; u++)
+                p[u] ^= K.next(T);
+    } else if (crx && !inplace && k->family != SRTP_DEV_NULL) {
+        // not in place, srtp_cryptex_unprotect decrypts the CSRCs whether
+        // or not the payload is encrypted (srtp.c:274-284)
+        for (uint32_t u = lo[0]; u < hi[0]; u++)
+            p[u] ^= K.next(T);
+    }
+    if (crx) {   // srtp_cryptex_unprotect_cleanup (srtp.c:290-305)
+        const uint32_t cur = (uint32_t)p[g.hl] << 8 | p[g.hl + 1];
+        if (!undo && cur == 0xC0DEu) {
+            p[g.hl] = 0xBE;
+            p[g.hl + 1] = 0xDE;
+        } else if (!undo && cur == 0xC2DEu) {
+            p[g.hl] = 0x10;
+            p[g.hl + 1] = 0x00;
+        } else if (undo && cur == 0xBEDEu) {
+            p[g.hl] = 0xC0;
+            p[g.hl + 1] = 0xDE;
+        } else if (undo && cur == 0x1000u) {
+            p[g.hl] = 0xC2;
+            p[g.hl + 1] = 0xDE;
+        }
+    }
+    return SRTP_XR_OK | SRTP_XR_WROTE | (crx ? SRTP_XR_CRYPTEX : 0);
+}
+
+__global__ __launch_bounds__(256) void k_xrtp(const uint8_t *in,
+                                              const uint64_t *in_off,
+                                              uint8_t *out,
+                                              const uint64_t *out_off,
+                                              const srtp_dev_meta_t *meta,
+                                              const srtp_dev_key_t *keys,
+                                              uint8_t *res,
+                                              const uint32_t *abort,
+                                              uint32_t n, int protect)
+{
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    load_aes_tables<false>(s_tab);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || (abort && *abort))
+        return;
+    const srtp_dev_meta_t m = meta[i];
+    if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != SRTP_VARIANT_X)
+        return;
+    const AesLds T = make_aes_lds(s_tab);
+    const uint8_t *src = in + in_off[i];
+    uint8_t *dst = out + out_off[i];
+    const uint8_t r = protect ? xrtp_protect(keys, m, src, dst, T)
+                              : xrtp_unprotect(keys, m, src, dst, false, T);
+    if (res)
+        res[i] = r;
+}
+
 }   // namespace
 
 // ===========================================================================
@@ -586,6 +1025,17 @@ static int run_dir(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     if (m & VBIT(SRTP_DEV_ICM, 3, 1)) rc |= launch_icm<14, true, PROT>(g, b, st);
     if (m & VBIT(SRTP_DEV_GCM, 1, 0)) rc |= launch_gcm<10, PROT>(g, b, st);
     if (m & VBIT(SRTP_DEV_GCM, 3, 0)) rc |= launch_gcm<14, PROT>(g, b, st);
+    if (m & (1u << SRTP_VARIANT_X)) {
+        // header-extension encryption / cryptex streams (k_xrtp)
+        const uint32_t n = (uint32_t)b->n;
+        hipLaunchKernelGGL(k_xrtp, dim3((n + 255) / 256), dim3(256), 0, st,
+                           b->in, b->in_off, b->out, b->out_off, b->meta,
+                           (const srtp_dev_key_t *)g->d_keys, b->auth_ok,
+                           b->abort, n, PROT ? 1 : 0);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess)
+            rc |= srtp_gpu_fail(e, "k_xrtp launch");
+    }
     return rc;
 }
 

@@ -103,11 +103,15 @@ typedef struct {
     uint32_t rslot;
     size_t rtag_len;
     int rgcm;               /* the RTCP cipher is AES-GCM (MKI offset)      */
+    /* RFC 6904 extension-header key (srtp.c:1385-1500): own device slot,
+     * ~0 without header-extension encryption */
+    uint32_t xslot;
 } hkey_t;
 
 typedef struct {
     int refs;
     size_t n;
+    int cryptex;   /* policy use_cryptex (RFC 9335)                          */
     hkey_t k[SRTP_MAX_NUM_MASTER_KEYS];
 } keyset_t;
 
@@ -760,6 +764,67 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         if (srtp_gpu_set_key(ctx->gpu, hk->rslot, &rk, NULL))
             return srtp_err_status_init_fail;
     }
+    /* RFC 6904 header-extension encryption and RFC 9335 cryptex
+     * (srtp.c:694-749, 1385-1500): every packet of such a stream goes to
+     * k_xrtp; the extension cipher is the RTP cipher's type, or AES-ICM of
+     * the same key size for AES-GCM */
+    hk->xslot = 0xffffffffu;
+    const int xtn = p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0;
+    if (xtn || p->use_cryptex) {
+        hk->variant = SRTP_VARIANT_X;
+        dk.xflags = (p->use_cryptex ? SRTP_XF_CRYPTEX : 0) |
+                    ((rtp->sec_serv & sec_serv_conf) ? SRTP_XF_CONF : 0);
+    }
+    if (xtn) {
+        srtp_dev_key_t xk;
+        memset(&xk, 0, sizeof xk);
+        for (size_t i = 0; i < p->enc_xtn_hdr_count; i++)
+            dk.xids[p->enc_xtn_hdr[i] >> 5] |= 1u << (p->enc_xtn_hdr[i] & 31);
+        dk.xflags |= SRTP_XF_XTN;
+        xk.family = SRTP_DEV_NULL;
+        if (hk->family != SRTP_DEV_NULL) {
+            uint8_t xkey[32], xsalt[16];
+            memset(xsalt, 0, sizeof xsalt);
+            if (hk->family == SRTP_DEV_GCM) {
+                /* a KDF of its own over the master key and the 12-byte
+                 * salt, zero padded (srtp.c:1393-1441); the ICM cipher then
+                 * reads 14 salt bytes, the last two being what the key
+                 * buffer holds there (srtp.c:1487) */
+                uint8_t tx[256];
+                memset(tx, 0, sizeof tx);
+                memcpy(tx, master, base + salt_len);
+                hc_aes_t xkdf;
+                hc_aes_init(&xkdf, tx, kdf_keylen - SRTP_SALT_LEN);
+                uint8_t xks[14];
+                memcpy(xks, tx + kdf_keylen - SRTP_SALT_LEN, 14);
+                kdf_gen(&xkdf, xks, 0x06, xkey, base);
+                kdf_gen(&xkdf, xks, 0x07, xsalt, salt_len);
+                xsalt[12] = tmp[base + 12];
+                xsalt[13] = tmp[base + 13];
+                memset(tx, 0, sizeof tx);
+            } else {
+                /* same cipher type: the main KDF, labels 6 and 7 */
+                kdf_gen(&kdf, kdf_salt, 0x06, xkey, base);
+                kdf_gen(&kdf, kdf_salt, 0x07, xsalt, 14);
+            }
+            hc_aes_t xa;
+            hc_aes_init(&xa, xkey, base);
+            memcpy(xk.rk, xa.rk, sizeof xk.rk);
+            xk.rounds = (uint32_t)xa.rounds;
+            xk.family = SRTP_DEV_ICM;
+            for (int i = 0; i < 4; i++)
+                xk.salt[i] = (uint32_t)xsalt[4 * i] |
+                             (uint32_t)xsalt[4 * i + 1] << 8 |
+                             (uint32_t)xsalt[4 * i + 2] << 16 |
+                             (uint32_t)xsalt[4 * i + 3] << 24;
+            memset(xkey, 0, sizeof xkey);
+        }
+        hk->xslot = alloc_slot(ctx);
+        xk.ghash_slot = hk->xslot;
+        dk.xslot = hk->xslot;
+        if (srtp_gpu_set_key(ctx->gpu, hk->xslot, &xk, NULL))
+            return srtp_err_status_init_fail;
+    }
     memset(tmp, 0, sizeof tmp);
     memset(ek, 0, sizeof ek);
     memset(ak, 0, sizeof ak);
@@ -777,6 +842,8 @@ static void keyset_release(srtp_t ctx, keyset_t *ks)
         release_slot(ctx, ks->k[i].slot);
         if (ks->k[i].rslot != 0xffffffffu)
             release_slot(ctx, ks->k[i].rslot);
+        if (ks->k[i].xslot != 0xffffffffu)
+            release_slot(ctx, ks->k[i].xslot);
     }
     memset(ks, 0, sizeof *ks);
     free(ks);
@@ -827,10 +894,6 @@ static srtp_err_status_t stream_new(srtp_t ctx, const srtp_policy_t *p,
         return st;
     if (!cipher_supported(&p->rtp) || !auth_supported(&p->rtp))
         return srtp_err_status_bad_param;
-    /* RFC 6904 header-extension encryption and RFC 9335 cryptex are not on
-     * the GPU path yet (DESIGN.md "Out of scope") */
-    if ((p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0) || p->use_cryptex)
-        return srtp_err_status_bad_param;
     if (p->window_size != 0 &&
         (p->window_size < 64 || p->window_size >= 0x8000))
         return srtp_err_status_bad_param; /* srtp.c:1670-1672 */
@@ -853,8 +916,9 @@ static srtp_err_status_t stream_new(srtp_t ctx, const srtp_policy_t *p,
         return srtp_err_status_alloc_fail;
     }
     ks->refs = 1;
+    ks->cryptex = p->use_cryptex;
     for (size_t i = 0; i < SRTP_MAX_NUM_MASTER_KEYS; i++)
-        ks->k[i].rslot = 0xffffffffu;
+        ks->k[i].rslot = ks->k[i].xslot = 0xffffffffu;
     s->keys = ks;
     if (p->key) {
         s->use_mki = false;
@@ -1164,6 +1228,9 @@ typedef struct {
     uint16_t err;
     uint32_t enc_start;
     uint32_t len;
+    uint16_t profile;  /* extension profile (X set)                          */
+    uint8_t cc, x;
+    uint8_t inplace;   /* the caller's output buffer is its input buffer    */
 } pkt_sum_t;
 
 static void summarize(const uint8_t *p, size_t len, pkt_sum_t *s)
@@ -1173,11 +1240,16 @@ static void summarize(const uint8_t *p, size_t len, pkt_sum_t *s)
     s->ssrc = 0;
     s->seq = 0;
     s->enc_start = 0;
+    s->profile = 0;
+    s->cc = s->x = 0;
+    s->inplace = 0;
     if (len < 12) {
         s->err = srtp_err_status_bad_param;
         return;
     }
     size_t h = 12 + 4 * (size_t)(p[0] & 0x0f);
+    s->cc = p[0] & 0x0f;
+    s->x = (p[0] >> 4) & 1;
     s->seq = (uint16_t)(p[2] << 8 | p[3]);
     s->ssrc = (uint32_t)p[8] << 24 | (uint32_t)p[9] << 16 |
               (uint32_t)p[10] << 8 | p[11];
@@ -1190,6 +1262,7 @@ static void summarize(const uint8_t *p, size_t len, pkt_sum_t *s)
             s->err = srtp_err_status_bad_param;
             return;
         }
+        s->profile = (uint16_t)(p[h] << 8 | p[h + 1]);
         h += ((size_t)(p[h + 2] << 8 | p[h + 3]) + 1) * 4;
         if (len < h) {
             s->err = srtp_err_status_bad_param;
@@ -1204,6 +1277,10 @@ static void from_dev_hdr(const srtp_dev_hdr_t *d, pkt_sum_t *s)
     s->ssrc = d->ssrc;
     s->seq = (uint16_t)(d->seq_len & 0xffff);
     s->len = d->len;
+    s->profile = (uint16_t)(d->xinfo & 0xffff);
+    s->cc = (uint8_t)((d->xinfo >> 16) & 15);
+    s->x = (uint8_t)((d->xinfo >> 20) & 1);
+    s->inplace = 0;
     if (d->enc_start >> 24) {
         s->err = (uint16_t)(d->enc_start >> 24);
         s->enc_start = 0;
@@ -1270,7 +1347,19 @@ static srtp_err_status_t pre_protect(srtp_t ctx, const pkt_sum_t *s,
     size_t tag_len = k->tag_len;
     if (cap < s->len + st->mki_size + tag_len)
         return srtp_err_status_buffer_small;
-    if (s->enc_start > s->len)
+    uint32_t es = s->enc_start;
+    const int xv = k->variant == SRTP_VARIANT_X;
+    if (xv && st->keys->cryptex && (st->rtp_services & sec_serv_conf)) {
+        /* srtp_cryptex_protect_init (srtp.c:163-193, 2151-2155) */
+        if (s->cc && !s->x)
+            return srtp_err_status_cryptex_err;
+        if (s->x) {
+            es = 12 + 4u * s->cc + 4 - (s->inplace ? 4u * s->cc : 0);
+            if (k->family == SRTP_DEV_GCM && !s->inplace && s->cc)
+                return srtp_err_status_cryptex_err;
+        }
+    }
+    if (es > s->len)
         return srtp_err_status_parse_err;
     uint64_t est;
     int64_t delta;
@@ -1287,12 +1376,13 @@ static srtp_err_status_t pre_protect(srtp_t ctx, const pkt_sum_t *s,
     }
     if (k->family == SRTP_DEV_ICM && (st->rtp_services & sec_serv_conf)) {
         /* aes_icm.c:317-322: at most 0xffff keystream blocks */
-        if ((s->len - s->enc_start + 15) / 16 > 0xffff)
+        if ((s->len - es + 15) / 16 > 0xffff)
             return srtp_err_status_cipher_fail;
     }
     meta->key = k->slot;
     meta->roc = (uint32_t)(est >> 16);
-    meta->info = s->enc_start | (k->variant << 24);
+    meta->info = (xv ? (s->inplace ? SRTP_XI_INPLACE : 0) : s->enc_start) |
+                 (k->variant << 24);
     meta->len = s->len;
     *out_len = s->len + tag_len + st->mki_size;
     return srtp_err_status_ok;
@@ -1308,6 +1398,7 @@ typedef struct {
     int auth;                   /* ... and authenticated                   */
     int failed;                 /* authentication failed at some index     */
     int dirty;                  /* output = input ^ keystream of `dm`      */
+    uint8_t xres;               /* k_xrtp result bits (SRTP_XR_*)          */
     hkey_t *key;                /* key of the last run                     */
     srtp_dev_meta_t dm;         /* meta of the last run                    */
 } upkt_t;
@@ -1444,17 +1535,27 @@ static srtp_err_status_t un_static(const srtp_stream_ctx_t *st,
     }
     *key = k;
     size_t tag_len = k->tag_len;
+    uint32_t es = s->enc_start;
+    const int xv = k->variant == SRTP_VARIANT_X;
+    if (xv && st->keys->cryptex && s->x &&
+        (s->profile == 0xC0DE || s->profile == 0xC2DE)) {
+        /* srtp_cryptex_unprotect_init (srtp.c:237-265, 2331-2335) */
+        es = 12 + 4u * s->cc + 4 - (s->inplace ? 4u * s->cc : 0);
+        if (k->family == SRTP_DEV_GCM && !s->inplace && s->cc)
+            return srtp_err_status_cryptex_err;
+    }
     if (s->len < tag_len + st->mki_size ||
-        s->enc_start > s->len - tag_len - st->mki_size)
+        es > s->len - tag_len - st->mki_size)
         return srtp_err_status_parse_err;
     if (k->family == SRTP_DEV_GCM) {
-        if (s->len - s->enc_start - st->mki_size < tag_len)
+        if (s->len - es - st->mki_size < tag_len)
             return srtp_err_status_cipher_fail;
     }
     if (cap < s->len - st->mki_size - tag_len)
         return srtp_err_status_buffer_small;
     meta->key = k->slot;
-    meta->info = s->enc_start | (k->variant << 24);
+    meta->info = (xv ? (s->inplace ? SRTP_XI_INPLACE : 0) : s->enc_start) |
+                 (k->variant << 24);
     meta->len = (uint32_t)(s->len - tag_len - st->mki_size);
     return srtp_err_status_ok;
 }
@@ -1516,7 +1617,8 @@ static int pre_unprotect(srtp_t ctx, provset_t *ps, const pkt_sum_t *s,
     const int known = u->gpu && u->est == est;
     int accept, run = 0;
     if (known) {
-        accept = u->auth; /* result already in hand at this index */
+        /* result already in hand at this index */
+        accept = u->auth && !(u->xres & SRTP_XR_PARSE);
     } else {
         run = 1;
         accept = mode == UNP_OPTIMISTIC && !u->failed;
@@ -1593,6 +1695,10 @@ static int post_unprotect(srtp_t ctx, const pkt_sum_t *s, upkt_t *u,
             return srtp_err_status_key_expired;
         }
     }
+    /* header-extension walk failed after authentication (srtp.c:3073-3080,
+     * 2409-2418): no index is added */
+    if (u->xres & SRTP_XR_PARSE)
+        return srtp_err_status_parse_err;
     if (kst->direction != DIR_RECEIVER) {
         if (kst->direction == DIR_UNKNOWN)
             kst->direction = DIR_RECEIVER;
@@ -1716,6 +1822,26 @@ static int memchr_nonzero(const size_t *v, size_t n)
     for (size_t i = 0; i < n; i++)
         if (v[i])
             return 1;
+    return 0;
+}
+
+/* k_xrtp verdicts of a protect batch: a header-extension parse error
+ * (srtp_process_header_encryption / srtp_cryptex_protect, srtp.c:2745-2762)
+ * comes after the index was taken.  Syncs `stream`. */
+static int xrtp_protect_results(srtp_t ctx, size_t n, srtp_err_status_t *status,
+                                void *stream)
+{
+    stage_t *sg = &ctx->st;
+    if (!(variants_of(sg->h_meta, n) & (1u << SRTP_VARIANT_X)))
+        return 0;
+    if (srtp_gpu_d2h(ctx->gpu, sg->h_auth, sg->d_auth, n, stream) ||
+        srtp_gpu_sync(ctx->gpu, stream))
+        return -1;
+    for (size_t i = 0; i < n; i++)
+        if (!status[i] &&
+            SRTP_META_VARIANT(sg->h_meta[i].info) == SRTP_VARIANT_X &&
+            (sg->h_auth[i] & SRTP_XR_PARSE))
+            status[i] = srtp_err_status_parse_err;
     return 0;
 }
 
@@ -1894,6 +2020,7 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
     for (size_t i = 0; i < n; i++) {
         pkt_sum_t s;
         summarize(rtp[i], rtp_len[i], &s);
+        s.inplace = rtp[i] == srtp[i];
         srtp_dev_meta_t *m = &sg->h_meta[i];
         memset(m, 0, sizeof *m);
         sg->h_off[i] = off;
@@ -1913,7 +2040,8 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
         run_gpu(ctx, 0, n, sg->d_arena, sg->d_off, sg->d_arena, sg->d_off,
                 sg->h_meta, HS(ctx)) ||
         srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, HS(ctx)) ||
-        srtp_gpu_sync(ctx->gpu, HS(ctx))) {
+        srtp_gpu_sync(ctx->gpu, HS(ctx)) ||
+        xrtp_protect_results(ctx, n, status, HS(ctx))) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         ret = srtp_err_status_fail;
     }
@@ -2044,10 +2172,19 @@ static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
                 if (SRTP_META_STATUS(sg->h_meta[i].info))
                     continue;
                 u[i].gpu = 1;
-                u[i].auth = sg->h_auth[i] != 0;
+                u[i].auth = (sg->h_auth[i] & 1) != 0;
                 u[i].failed |= !u[i].auth;
                 u[i].dirty = 1;
                 u[i].dm = sg->h_meta[i];
+                u[i].xres = 0;
+                if (SRTP_META_VARIANT(sg->h_meta[i].info) == SRTP_VARIANT_X) {
+                    /* k_xrtp writes only authenticated packets; an undo
+                     * needs to know whether cryptex was applied */
+                    u[i].xres = sg->h_auth[i];
+                    u[i].dirty = (sg->h_auth[i] & SRTP_XR_WROTE) != 0;
+                    if (sg->h_auth[i] & SRTP_XR_CRYPTEX)
+                        u[i].dm.info |= SRTP_XI_CRYPTEX;
+                }
             }
         }
         /* exact in-order post-pass; a packet whose estimate moved is re-run
@@ -2125,6 +2262,7 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
     size_t off = 0;
     for (size_t i = 0; i < n; i++) {
         summarize(srtp[i], srtp_len[i], &sum[i]);
+        sum[i].inplace = srtp[i] == rtp[i];
         /* MKI bytes: the stream decides its size; point at the packet and
          * let un_static() index from the end */
         mki[i] = NULL;
@@ -2216,6 +2354,9 @@ static srtp_err_status_t dev_headers(srtp_t ctx, const srtp_device_batch_t *b,
         return srtp_err_status_fail;
     for (size_t i = 0; i < b->n; i++) {
         from_dev_hdr(&sg->h_hdr[i], &sum[i]);
+        /* same arena: in place (an overlapping, different offset is not a
+         * supported layout) */
+        sum[i].inplace = b->in == b->out;
         cap[i] = caps[i];
     }
     return srtp_err_status_ok;
@@ -2279,7 +2420,9 @@ static int dev_build(srtp_t ctx)
         d->key = k->slot;
         d->variant = k->variant;
         d->flags = 0;
-        if (!st->use_mki && st->rdbx.pending_roc == 0 &&
+        /* header-extension encryption / cryptex streams: host pre-pass */
+        const int xs = k->variant == SRTP_VARIANT_X;
+        if (!st->use_mki && st->rdbx.pending_roc == 0 && !xs &&
             st->direction != DIR_RECEIVER) {
             d->flags |= SRTP_DS_ELIGIBLE;
             if (k->num_left < dt->num_left_min)
@@ -2291,7 +2434,7 @@ static int dev_build(srtp_t ctx)
             first = 0;
             dt->mask |= 1u << k->variant;
         }
-        if (!st->use_mki && st->rdbx.pending_roc == 0 &&
+        if (!st->use_mki && st->rdbx.pending_roc == 0 && !xs &&
             st->direction != DIR_SENDER) {
             d->flags |= SRTP_DS_RX_ELIGIBLE;
             if (k->num_left < dt->num_left_min)
@@ -2452,7 +2595,8 @@ srtp_err_status_t srtp_protect_device(srtp_t ctx, const srtp_device_batch_t *b)
             m->info = (uint32_t)(status[i] & 0xff) << 16;
     }
     if (run_gpu(ctx, 0, n, b->in, b->in_off, b->out, b->out_off,
-                ctx->st.h_meta, b->stream)) {
+                ctx->st.h_meta, b->stream) ||
+        xrtp_protect_results(ctx, n, status, b->stream)) {
         ret = srtp_err_status_fail;
         goto out;
     }

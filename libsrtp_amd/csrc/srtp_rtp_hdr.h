@@ -27,6 +27,7 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
     h.len = len;
     h.ssrc = 0;
     h.seq_len = 0;
+    h.xinfo = 0;
     uint32_t err = 0, es = 0;
     if ((off & 15) != 0) {
         err = 2;
@@ -37,6 +38,7 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
         h.ssrc = srtp_bswap32(*(const uint32_t *)(p + 8));
         h.seq_len = w0 & 0xffffu;
         es = 12 + 4 * ((w0 >> 24) & 0xfu);
+        h.xinfo = ((w0 >> 24) & 0xfu) << 16 | ((w0 >> 28) & 1u) << 20;
         if (len < es) {
             err = 2;
         } else if ((w0 >> 28) & 1) {
@@ -44,6 +46,7 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
                 err = 2;
             } else {
                 uint32_t xw = srtp_bswap32(*(const uint32_t *)(p + es));
+                h.xinfo |= xw >> 16;
                 es += ((xw & 0xffffu) + 1) * 4;
                 if (len < es)
                     err = 2;

@@ -223,6 +223,13 @@ class _PolicyHolder:
             kb = C.create_string_buffer(keys[0], max(64, len(keys[0])))
             self.keep.append(kb)
             p.key = C.cast(kb, C.c_void_p)
+        ids = d.get("enc_xtn_hdr") or []
+        if ids:
+            xb = (C.c_uint8 * len(ids))(*ids)
+            self.keep.append(xb)
+            p.enc_xtn_hdr = C.cast(xb, C.c_void_p)
+            p.enc_xtn_hdr_count = len(ids)
+        p.use_cryptex = bool(d.get("use_cryptex", 0))
         self.policy = p
 
 
@@ -282,19 +289,31 @@ class Session:
         return Status(self.L.srtp_update(self.h, C.byref(h.policy)))
 
     # -- single packet (srtp_protect / srtp_unprotect) ---------------------
-    def protect(self, rtp, cap=None, mki_index=0):
+    # inplace=True passes one buffer as both input and output, as the
+    # reference's in-place calls do (cryptex behaves differently then)
+    def protect(self, rtp, cap=None, mki_index=0, inplace=False):
         cap = len(rtp) + 144 if cap is None else cap
         out = C.create_string_buffer(max(cap, len(rtp), 1))
         n = C.c_size_t(cap)
-        st = self.L.srtp_protect(self.h, rtp, len(rtp), out, C.byref(n),
+        if inplace:
+            C.memmove(out, rtp, len(rtp))
+            src = out
+        else:
+            src = rtp
+        st = self.L.srtp_protect(self.h, src, len(rtp), out, C.byref(n),
                                  mki_index)
         return Status(st), (out.raw[:n.value] if st == 0 else None)
 
-    def unprotect(self, srtp, cap=None):
+    def unprotect(self, srtp, cap=None, inplace=False):
         cap = len(srtp) if cap is None else cap
         out = C.create_string_buffer(max(cap, len(srtp), 1))
         n = C.c_size_t(cap)
-        st = self.L.srtp_unprotect(self.h, srtp, len(srtp), out, C.byref(n))
+        if inplace:
+            C.memmove(out, srtp, len(srtp))
+            src = out
+        else:
+            src = srtp
+        st = self.L.srtp_unprotect(self.h, src, len(srtp), out, C.byref(n))
         return Status(st), (out.raw[:n.value] if st == 0 else None)
 
     # -- SRTCP (srtp_protect_rtcp / srtp_unprotect_rtcp) -------------------
@@ -316,12 +335,16 @@ class Session:
 
     # -- batch over host buffers -------------------------------------------
     def protect_batch(self, pkts, caps=None, mki=None,
-                      fn="srtp_protect_batch"):
+                      fn="srtp_protect_batch", inplace=False):
         n = len(pkts)
         caps = [len(p) + 148 for p in pkts] if caps is None else caps
-        ins = [C.create_string_buffer(p, max(1, len(p))) for p in pkts]
-        outs = [C.create_string_buffer(max(1, c, len(p)))
-                for c, p in zip(caps, pkts)]
+        if inplace:   # rtp[i] == srtp[i]
+            ins = outs = [C.create_string_buffer(p, max(1, c, len(p)))
+                          for c, p in zip(caps, pkts)]
+        else:
+            ins = [C.create_string_buffer(p, max(1, len(p))) for p in pkts]
+            outs = [C.create_string_buffer(max(1, c, len(p)))
+                    for c, p in zip(caps, pkts)]
         inp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in ins])
         outp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in outs])
         ilen = (C.c_size_t * n)(*[len(p) for p in pkts])
@@ -335,12 +358,17 @@ class Session:
                 [outs[i].raw[:olen[i]] if st[i] == 0 else None
                  for i in range(n)])
 
-    def unprotect_batch(self, pkts, caps=None, fn="srtp_unprotect_batch"):
+    def unprotect_batch(self, pkts, caps=None, fn="srtp_unprotect_batch",
+                        inplace=False):
         n = len(pkts)
         caps = [len(p) for p in pkts] if caps is None else caps
-        ins = [C.create_string_buffer(p, max(1, len(p))) for p in pkts]
-        outs = [C.create_string_buffer(max(1, c, len(p)))
-                for c, p in zip(caps, pkts)]
+        if inplace:   # srtp[i] == rtp[i]
+            ins = outs = [C.create_string_buffer(p, max(1, c, len(p)))
+                          for c, p in zip(caps, pkts)]
+        else:
+            ins = [C.create_string_buffer(p, max(1, len(p))) for p in pkts]
+            outs = [C.create_string_buffer(max(1, c, len(p)))
+                    for c, p in zip(caps, pkts)]
         inp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in ins])
         outp = (C.c_void_p * n)(*[C.cast(b, C.c_void_p) for b in outs])
         ilen = (C.c_size_t * n)(*[len(p) for p in pkts])

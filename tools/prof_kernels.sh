@@ -9,7 +9,7 @@ args=${*:-"--steps 3 --warmup 1 --no-cpu-baseline --traffic off"}
 export TMPDIR=/tmp
 mkdir -p "$out"
 echo "[prof] kernel trace"
-timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$out/kt" -o kt \
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o kt \
     -- python3 bench.py $args > "$out/kt.log" 2>&1 || { tail -5 "$out/kt.log"; exit 1; }
 python3 tools/pmc_reduce.py "$out/kt"
 passes=(
