@@ -86,8 +86,33 @@ typedef struct srtp_dev_hdr {
     uint32_t seq_len;   /* [15:0] seq, [31:16] reserved                      */
     uint32_t enc_start; /* header length incl. extension, or error code<<24 */
     uint32_t len;       /* packet length                                     */
-    uint32_t xinfo;     /* [15:0] extension profile, [19:16] CC, bit 20 X    */
 } srtp_dev_hdr_t;
+
+/* session-key derivation job for k_kdf (srtp_gpu_kdf): the SRTP KDF
+ * (srtp.c:1070-1142: AES-ICM PRF keyed by the master key, offset = master
+ * salt, label in byte 7) for one session key, then the device key record
+ * (AES schedule, salt, HMAC midstates, GCM H and GHASH table).  The host
+ * fills every field of `key` but rk / salt / ipad / opad / h. */
+enum {
+    SRTP_KDF_HMAC = 1,      /* ipad / opad from the auth key               */
+    SRTP_KDF_GCM_H = 2,     /* h = E_K(0^128)                              */
+    SRTP_KDF_GHASH = 4,     /* Shoup table of h into ghash slot            */
+    SRTP_KDF_SALT_TAIL = 8  /* salt bytes salt_len.. from salt_tail        */
+};
+
+typedef struct srtp_kdf_job {
+    srtp_dev_key_t key;
+    uint8_t kdf_key[32];    /* the PRF's AES key                            */
+    uint8_t kdf_salt[16];   /* its 14-byte offset                           */
+    uint8_t salt_tail[2];
+    uint8_t lab_enc, lab_salt, lab_auth, pad[3];
+    uint32_t kdf_len;       /* 16 / 24 / 32                                 */
+    uint32_t enc_len;       /* 0 (no AES key) / 16 / 24 / 32                */
+    uint32_t salt_len;      /* bytes of PRF salt output: 0 / 12 / 14        */
+    uint32_t auth_len;      /* bytes of PRF auth-key output (0..20)         */
+    uint32_t flags;         /* SRTP_KDF_*                                   */
+    uint32_t slot;          /* destination key slot                         */
+} srtp_kdf_job_t;
 
 /* ---- thin FFI implemented in HIP (srtp_gpu.hip) ----------------------- */
 
@@ -101,6 +126,10 @@ const char *srtp_gpu_last_error(void);
 /* key table (device copy of srtp_dev_key_t, grown on demand) */
 int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
                      const uint32_t *ghash_tab /* 1024 words or NULL */);
+
+/* derive n session keys on the GPU (k_kdf) straight into the key table;
+ * synchronous */
+int srtp_gpu_kdf(srtp_gpu_t *g, const srtp_kdf_job_t *jobs, size_t n);
 
 /* One pass over a batch in device memory.  Packets whose meta status is
  * non-zero are skipped.  For unprotect, auth_ok[i] receives 1 when the tag
@@ -138,10 +167,11 @@ int srtp_gpu_rtcp(srtp_gpu_t *g, int op, size_t n, uint8_t *arena,
                   const uint64_t *off, const srtp_dev_meta_t *meta,
                   uint8_t *auth_ok, void *stream);
 
-/* device header parse for the device-resident API */
+/* device header parse for the device-resident API; xinfo_out[i] (may be
+ * NULL): [15:0] extension profile, [19:16] CC, bit 20 X (cryptex checks) */
 int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
                    const uint64_t *in_off, const uint32_t *in_len,
-                   srtp_dev_hdr_t *hdr_out, void *stream);
+                   srtp_dev_hdr_t *hdr_out, uint32_t *xinfo_out, void *stream);
 
 /* ---- device pre-pass (DESIGN.md "Device pre-pass") --------------------
  * A device mirror of the session's streams lets srtp_protect_device and

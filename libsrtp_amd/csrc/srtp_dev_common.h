@@ -571,7 +571,12 @@ struct GhTab {
 template <>
 DEV u32x4 GhTab<true>::get(uint32_t w, int k) const
 {
-    // byte k of BE word w (k = 0 is the most significant byte)
+    // byte k of BE word w (k = 0 is the most significant byte) at address
+    // bits 15:8; byte 2 is there already: one full-rate v_bitop3 instead of
+    // the half-rate v_perm
+    if (k == 2)
+        return *(const u32x4 *)(lds + __builtin_amdgcn_bitop3_b32(
+                                          w, 0x0000ff00u, lane16, 0xEA));
     uint32_t sel = 0x0c020000u | ((4u + 3u - (uint32_t)k) << 8);
     uint32_t a = __builtin_amdgcn_perm(w, lane16, sel);
     return *(const u32x4 *)(lds + a);
@@ -584,22 +589,35 @@ DEV u32x4 GhTab<false>::get(uint32_t w, int k) const
     return g[idx];
 }
 
+// Z = X * H by Horner over the bytes of X, last byte first (Shoup's 8-bit
+// table M[b] = b * H).  Each step multiplies Z by x^8: the byte leaving Z
+// (coefficients x^128..x^135) would be reduced at once by
+// x^128 = 1 + x + x^2 + x^7; here it is shifted into a fifth word o
+// instead, and every 4 steps the 32 collected coefficients x^128..x^159
+// (o bit j <-> x^(159-j)) are folded back in one go:
+//   word 0 ^= o ^ o>>1 ^ o>>2 ^ o>>7,  word 1 ^= o<<31 ^ o<<30 ^ o<<25
+// (6 shifts per 4 steps instead of 4 per step: the shifts are half-rate
+// VALU on gfx950, tools/valu_rate.hip).
 template <bool LDSM>
 DEV void ghash_mul(uint32_t x[4], const GhTab<LDSM> &T)
 {
-    // Z = X * H by Horner over the bytes, last byte first
     u32x4 z = T.get(x[3], 3);
+    uint32_t o = 0;
 #pragma unroll
     for (int k = 14; k >= 0; k--) {
-        uint32_t r = z.w & 0xffu;
-        uint32_t red = xor3(r << 24, r << 23, r << 22) ^ (r << 17);
         u32x4 mv = T.get(x[k >> 2], k & 3);
+        o = __builtin_amdgcn_alignbit(z.w, o, 8);
         u32x4 nz;
         nz.w = __builtin_amdgcn_alignbit(z.z, z.w, 8) ^ mv.w;
         nz.z = __builtin_amdgcn_alignbit(z.y, z.z, 8) ^ mv.z;
         nz.y = __builtin_amdgcn_alignbit(z.x, z.y, 8) ^ mv.y;
-        nz.x = xor3(z.x >> 8, red, mv.x);
+        nz.x = (z.x >> 8) ^ mv.x;
         z = nz;
+        if (k % 4 == 3 || k == 0) {
+            z.x = xor3(xor3(z.x, o, o >> 1), o >> 2, o >> 7);
+            z.y = xor3(z.y, o << 31, o << 30) ^ (o << 25);
+            o = 0;
+        }
     }
     x[0] = z.x;
     x[1] = z.y;

@@ -382,13 +382,17 @@ __global__ __launch_bounds__(256) void k_rtcp(uint8_t *arena,
 // header parse for the device-resident API (srtp_validate_rtp_header,
 // srtp.c:307-336; header length 96-125)
 __global__ void k_parse(const uint8_t *in, const uint64_t *in_off,
-                        const uint32_t *in_len, srtp_dev_hdr_t *hdr, uint32_t n)
+                        const uint32_t *in_len, srtp_dev_hdr_t *hdr,
+                        uint32_t *xinfo, uint32_t n)
 {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
     const uint64_t off = in_off[i];
-    hdr[i] = srtp_parse_rtp(in + off, off, in_len[i]);
+    const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
+    hdr[i] = h;
+    if (xinfo)
+        xinfo[i] = srtp_rtp_xinfo(in + off, h);
 }
 
 // ---------------------------------------------------------------------------
@@ -949,6 +953,202 @@ __global__ __launch_bounds__(256) void k_xrtp(const uint8_t *in,
         res[i] = r;
 }
 
+// ---------------------------------------------------------------------------
+// Session-key derivation for many keys at once (srtp_gpu_kdf): one lane per
+// session key.  The SRTP KDF (srtp.c:1070-1142) is AES-ICM keyed by the
+// master key with the master salt as offset and the label in byte 7;
+// srtp_stream_init_keys (srtp.c:1233-1607) draws the cipher key, salt and
+// HMAC key from it, and the cipher / auth init turn them into the AES
+// schedule (aes.c key expansion, FIPS-197 5.2), the HMAC ipad / opad SHA-1
+// midstates (hmac.c:76-120) and, for AES-GCM, H = E_K(0) and the GHASH
+// table.  The host decides every policy question (labels, lengths, which
+// records) and the GPU does the arithmetic: a mass (re)key of 64k streams
+// is one launch instead of 64k host derivations and uploads.
+
+DEV uint32_t kdf_subword(uint32_t t, const uint32_t *sb)
+{
+    return sb[t & 0xffu] | sb[(t >> 8) & 0xffu] << 8 |
+           sb[(t >> 16) & 0xffu] << 16 | sb[t >> 24] << 24;
+}
+
+template <int NR>
+struct ArrKey {
+    uint32_t rk[4 * (NR + 1)];
+    DEV uint32_t operator()(int i) const { return rk[i]; }
+};
+
+// AES key expansion: little-endian words of the key bytes (the layout of
+// srtp_dev_key_t.rk), RotWord / SubWord / Rcon on those
+template <int NR>
+DEV void kdf_expand(const uint8_t *key, ArrKey<NR> &K, const uint32_t *sb)
+{
+    constexpr int NK = NR - 6, NW = 4 * (NR + 1);
+#pragma unroll
+    for (int i = 0; i < NK; i++)
+        K.rk[i] = (uint32_t)key[4 * i] | (uint32_t)key[4 * i + 1] << 8 |
+                  (uint32_t)key[4 * i + 2] << 16 | (uint32_t)key[4 * i + 3] << 24;
+    uint32_t rc = 1;
+#pragma unroll
+    for (int i = NK; i < NW; i++) {
+        uint32_t t = K.rk[i - 1];
+        if (i % NK == 0) {
+            t = kdf_subword((t >> 8) | (t << 24), sb) ^ rc;
+            rc = ((rc << 1) ^ ((rc >> 7) * 0x1bu)) & 0xffu;
+        } else if (NK > 6 && i % NK == 4) {
+            t = kdf_subword(t, sb);
+        }
+        K.rk[i] = K.rk[i - NK] ^ t;
+    }
+}
+
+// `len` bytes of PRF output for `label` (srtp.c:1104-1142): counter block =
+// offset ^ (label at byte 7), 16-bit block counter in bytes 14..15
+template <int NR>
+DEV void kdf_prf(const ArrKey<NR> &K, const uint8_t *salt, uint32_t label,
+                 uint8_t *out, uint32_t len, const AesLds &T)
+{
+    for (uint32_t j = 0; 16 * j < len; j++) {
+        uint8_t c[16];
+        for (int u = 0; u < 14; u++)
+            c[u] = salt[u];
+        c[7] ^= (uint8_t)label;
+        c[14] = (uint8_t)(j >> 8);
+        c[15] = (uint8_t)j;
+        uint32_t x[4];
+        for (int w = 0; w < 4; w++)
+            x[w] = (uint32_t)c[4 * w] | (uint32_t)c[4 * w + 1] << 8 |
+                   (uint32_t)c[4 * w + 2] << 16 | (uint32_t)c[4 * w + 3] << 24;
+        aes_block<NR, false>(x[0], x[1], x[2], x[3], K, T);
+        for (uint32_t b = 0; b < 16 && 16 * j + b < len; b++)
+            out[16 * j + b] = (uint8_t)(x[b >> 2] >> (8 * (b & 3)));
+    }
+}
+
+// the cipher half of the record: schedule of the derived key, H, GHASH
+template <int NR>
+DEV void kdf_cipher(const srtp_kdf_job_t &J, const uint8_t *ek,
+                    srtp_dev_key_t *o, uint32_t *ghash, const uint32_t *sb,
+                    const AesLds &T)
+{
+    ArrKey<NR> K;
+    kdf_expand<NR>(ek, K, sb);
+#pragma unroll
+    for (int i = 0; i < 4 * (NR + 1); i++)
+        o->rk[i] = K.rk[i];
+    if (!(J.flags & (SRTP_KDF_GCM_H | SRTP_KDF_GHASH)))
+        return;
+    uint32_t x[4] = { 0, 0, 0, 0 };
+    aes_block<NR, false>(x[0], x[1], x[2], x[3], K, T);
+    uint32_t v[4];   // H as big-endian words
+    for (int w = 0; w < 4; w++) {
+        v[w] = bswap(x[w]);
+        o->h[w] = v[w];
+    }
+    if (!(J.flags & SRTP_KDF_GHASH))
+        return;
+    // Shoup's table M[b] = b * H: powers by halving (v * x = v >> 1, ^ 0xe1
+    // on carry), then sums (host_crypto.c hc_ghash_table, same layout)
+    uint32_t *tab = ghash + 1024 * (size_t)J.key.ghash_slot;
+    for (int w = 0; w < 4; w++)
+        tab[w] = 0;
+    for (uint32_t bit = 0x80; bit; bit >>= 1) {
+        for (int w = 0; w < 4; w++)
+            tab[4 * bit + w] = v[w];
+        const uint32_t lsb = v[3] & 1u;
+        v[3] = (v[3] >> 1) | (v[2] << 31);
+        v[2] = (v[2] >> 1) | (v[1] << 31);
+        v[1] = (v[1] >> 1) | (v[0] << 31);
+        v[0] = (v[0] >> 1) ^ ((0u - lsb) & 0xe1000000u);
+    }
+    for (uint32_t b = 1; b < 256; b++) {
+        const uint32_t low = b & (0u - b);
+        if (b == low)
+            continue;
+        for (int w = 0; w < 4; w++)
+            tab[4 * b + w] = tab[4 * low + w] ^ tab[4 * (b ^ low) + w];
+    }
+}
+
+template <int NRK>
+DEV void kdf_one(const srtp_kdf_job_t &J, srtp_dev_key_t *keys,
+                 uint32_t *ghash, const uint32_t *sb, const AesLds &T)
+{
+    ArrKey<NRK> P;
+    kdf_expand<NRK>(J.kdf_key, P, sb);
+    uint8_t ek[32], sa[16], ak[20];
+    for (int u = 0; u < 16; u++)
+        sa[u] = 0;
+    kdf_prf<NRK>(P, J.kdf_salt, J.lab_enc, ek, J.enc_len, T);
+    kdf_prf<NRK>(P, J.kdf_salt, J.lab_salt, sa, J.salt_len, T);
+    kdf_prf<NRK>(P, J.kdf_salt, J.lab_auth, ak, J.auth_len, T);
+    if (J.flags & SRTP_KDF_SALT_TAIL) {
+        sa[J.salt_len] = J.salt_tail[0];
+        sa[J.salt_len + 1] = J.salt_tail[1];
+    }
+    srtp_dev_key_t *o = keys + J.slot;
+    // the host's fields, then the derived ones
+    const uint32_t *src = (const uint32_t *)&J.key;
+    uint32_t *dst = (uint32_t *)o;
+    for (uint32_t w = 0; w < sizeof(srtp_dev_key_t) / 4; w++)
+        dst[w] = src[w];
+    for (int w = 0; w < 4; w++)
+        o->salt[w] = (uint32_t)sa[4 * w] | (uint32_t)sa[4 * w + 1] << 8 |
+                     (uint32_t)sa[4 * w + 2] << 16 | (uint32_t)sa[4 * w + 3] << 24;
+    if (J.enc_len == 16)
+        kdf_cipher<10>(J, ek, o, ghash, sb, T);
+    else if (J.enc_len == 24)
+        kdf_cipher<12>(J, ek, o, ghash, sb, T);
+    else if (J.enc_len == 32)
+        kdf_cipher<14>(J, ek, o, ghash, sb, T);
+    if (J.flags & SRTP_KDF_HMAC) {
+        // SHA-1 midstates of (K ^ ipad) and (K ^ opad), K zero padded
+        for (int pass = 0; pass < 2; pass++) {
+            const uint32_t pad = pass ? 0x5c5c5c5cu : 0x36363636u;
+            uint32_t w[16];
+            for (int t = 0; t < 16; t++) {
+                uint32_t v = 0;
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t b = 4 * t + u;
+                    v = (v << 8) | (b < J.auth_len ? ak[b] : 0u);
+                }
+                w[t] = v ^ pad;
+            }
+            uint32_t h[5] = { 0x67452301u, 0xefcdab89u, 0x98badcfeu,
+                              0x10325476u, 0xc3d2e1f0u };
+            sha1_compress(h, w);   // adds the chaining value itself
+            for (int k = 0; k < 5; k++) {
+                if (pass)
+                    o->opad[k] = h[k];
+                else
+                    o->ipad[k] = h[k];
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_kdf(const srtp_kdf_job_t *jobs,
+                                             uint32_t n, srtp_dev_key_t *keys,
+                                             uint32_t *ghash)
+{
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    __shared__ uint32_t s_sb[256];
+    for (int x = threadIdx.x; x < 256; x += blockDim.x)
+        s_sb[x] = (aes_t0((uint32_t)x) >> 8) & 0xffu;   // S[x]
+    load_aes_tables<false>(s_tab);
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const AesLds T = make_aes_lds(s_tab);
+    const srtp_kdf_job_t &J = jobs[i];
+    if (J.kdf_len == 16)
+        kdf_one<10>(J, keys, ghash, s_sb, T);
+    else if (J.kdf_len == 24)
+        kdf_one<12>(J, keys, ghash, s_sb, T);
+    else
+        kdf_one<14>(J, keys, ghash, s_sb, T);
+}
+
 }   // namespace
 
 // ===========================================================================
@@ -1138,6 +1338,44 @@ int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
     return 0;
 }
 
+int srtp_gpu_kdf(srtp_gpu_t *g, const srtp_kdf_job_t *jobs, size_t n)
+{
+    if (!n)
+        return 0;
+    uint32_t kmax = 0, gmax = 0;
+    int any_gh = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (jobs[i].slot + 1 > kmax)
+            kmax = jobs[i].slot + 1;
+        if (jobs[i].flags & SRTP_KDF_GHASH) {
+            any_gh = 1;
+            if (jobs[i].key.ghash_slot + 1 > gmax)
+                gmax = jobs[i].key.ghash_slot + 1;
+        }
+    }
+    if (grow((void **)&g->d_keys, &g->key_cap, kmax, sizeof(srtp_dev_key_t)))
+        return -1;
+    if (any_gh && grow((void **)&g->d_ghash, &g->ghash_cap, gmax,
+                       1024 * sizeof(uint32_t)))
+        return -1;
+    srtp_kdf_job_t *d = NULL;
+    HIPCHK(hipMalloc((void **)&d, n * sizeof *d));
+    hipError_t e = hipMemcpyAsync(d, jobs, n * sizeof *d,
+                                  hipMemcpyHostToDevice, g->stream);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_kdf, dim3((unsigned)((n + 255) / 256)), dim3(256),
+                           0, g->stream, d, (uint32_t)n, g->d_keys,
+                           (uint32_t *)g->d_ghash);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(g->stream);
+    (void)hipFree(d);
+    if (e != hipSuccess)
+        return srtp_gpu_fail(e, "k_kdf");
+    return 0;
+}
+
 int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b)
 {
     if (b->n == 0)
@@ -1183,13 +1421,14 @@ int srtp_gpu_rtcp(srtp_gpu_t *g, int op, size_t n, uint8_t *arena,
 
 int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
                    const uint64_t *in_off, const uint32_t *in_len,
-                   srtp_dev_hdr_t *hdr_out, void *stream)
+                   srtp_dev_hdr_t *hdr_out, uint32_t *xinfo_out, void *stream)
 {
     if (!n)
         return 0;
     hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     hipLaunchKernelGGL(k_parse, dim3((unsigned)((n + 255) / 256)), dim3(256),
-                       0, st, in, in_off, in_len, hdr_out, (uint32_t)n);
+                       0, st, in, in_off, in_len, hdr_out, xinfo_out,
+                       (uint32_t)n);
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -138,6 +138,7 @@ struct srtp_stream_ctx_t_ {
     uint64_t spec_epoch;
     rdbx_t spec;
     uint32_t dev_sid;   /* id in the device stream table (dev_build) */
+    size_t lpos;        /* index in ctx->list */
     /* SRTCP replay database (crypto/replay/rdb.c): 31-bit index window */
     uint32_t rtcp_start;
     uint32_t rtcp_bm[4];
@@ -158,6 +159,7 @@ typedef struct {
     srtp_dev_meta_t *h_meta, *d_meta;
     uint8_t *h_auth, *d_auth;
     srtp_dev_hdr_t *h_hdr, *d_hdr;
+    uint32_t *h_xinfo, *d_xinfo; /* CC / X / profile (k_parse) */
     /* host-buffer batches on the device pre-pass: lengths in, capacities
      * in / lengths out, statuses out */
     uint32_t *h_len, *d_len, *h_cap, *d_cap;
@@ -203,6 +205,13 @@ struct srtp_ctx_t_ {
     int timing;
     double last_ms;
     devtab_t dt;
+    /* queued GPU key derivations (kq_flush); SRTP_MI355X_HOST_KDF=1 derives
+     * on the host instead */
+    srtp_kdf_job_t *kq;
+    size_t kq_n, kq_cap;
+    uint32_t *rel;          /* slots released while jobs were queued */
+    size_t n_rel, rel_cap;
+    int host_kdf;
 };
 
 static void dev_pull(srtp_t ctx);
@@ -280,6 +289,7 @@ static int list_insert(srtp_t ctx, srtp_stream_ctx_t *s)
         ctx->list = (srtp_stream_ctx_t **)p;
         ctx->cap = nc;
     }
+    s->lpos = ctx->n;
     ctx->list[ctx->n++] = s;
     if (2 * (ctx->map.used + 1) > ctx->map.cap)
         return map_rebuild(ctx, ctx->map.cap ? 2 * ctx->map.cap : 64);
@@ -298,14 +308,29 @@ static int list_insert(srtp_t ctx, srtp_stream_ctx_t *s)
 
 static void list_remove(srtp_t ctx, srtp_stream_ctx_t *s)
 {
-    for (size_t i = 0; i < ctx->n; i++)
-        if (ctx->list[i] == s) {
-            memmove(&ctx->list[i], &ctx->list[i + 1],
-                    (ctx->n - i - 1) * sizeof(void *));
-            ctx->n--;
+    size_t i = s->lpos;
+    if (i < ctx->n && ctx->list[i] == s) {
+        memmove(&ctx->list[i], &ctx->list[i + 1],
+                (ctx->n - i - 1) * sizeof(void *));
+        ctx->n--;
+        for (; i < ctx->n; i++)
+            ctx->list[i]->lpos = i;
+    }
+    map_rebuild(ctx, ctx->map.cap ? ctx->map.cap : 64);
+}
+
+/* the stream `ns` takes old's place in the list and the SSRC map */
+static void list_replace(srtp_t ctx, srtp_stream_ctx_t *old,
+                         srtp_stream_ctx_t *ns)
+{
+    ns->lpos = old->lpos;
+    ctx->list[old->lpos] = ns;
+    for (size_t h = map_hash(old->ssrc, ctx->map.cap); ctx->map.vals[h];
+         h = (h + 1) & (ctx->map.cap - 1))
+        if (ctx->map.vals[h] == old) {
+            ctx->map.vals[h] = ns;
             break;
         }
-    map_rebuild(ctx, ctx->map.cap ? ctx->map.cap : 64);
 }
 
 /* ------------------------------------------------------------------------
@@ -561,7 +586,12 @@ static uint32_t alloc_slot(srtp_t ctx)
     return ctx->next_slot++;
 }
 
-static void release_slot(srtp_t ctx, uint32_t slot)
+/* Pending session-key derivations for the GPU (k_kdf, srtp_gpu_kdf): a
+ * stream's keys are queued by init_key and derived in one launch when the
+ * public call that created them returns (srtp_create with 64k policies is
+ * one launch, not 64k host derivations and uploads).  A slot is never
+ * released, reused or read by a kernel with its job still queued. */
+static void free_slot_now(srtp_t ctx, uint32_t slot)
 {
     if (ctx->n_free == ctx->free_cap) {
         size_t nc = ctx->free_cap ? 2 * ctx->free_cap : 16;
@@ -574,6 +604,144 @@ static void release_slot(srtp_t ctx, uint32_t slot)
     ctx->free_slots[ctx->n_free++] = slot;
 }
 
+static int kq_flush(srtp_t ctx)
+{
+    int rc = 0;
+    if (ctx->kq_n) {
+        rc = srtp_gpu_kdf(ctx->gpu, ctx->kq, ctx->kq_n);
+        ctx->kq_n = 0;
+        if (rc)
+            log_msg(srtp_log_level_error, srtp_gpu_last_error());
+    }
+    /* slots released while jobs were queued become reusable now */
+    for (size_t i = 0; i < ctx->n_rel; i++)
+        free_slot_now(ctx, ctx->rel[i]);
+    ctx->n_rel = 0;
+    return rc;
+}
+
+static srtp_kdf_job_t *kq_push(srtp_t ctx)
+{
+    if (ctx->kq_n == ctx->kq_cap) {
+        size_t nc = ctx->kq_cap ? 2 * ctx->kq_cap : 64;
+        srtp_kdf_job_t *q =
+            (srtp_kdf_job_t *)realloc(ctx->kq, nc * sizeof(srtp_kdf_job_t));
+        if (!q)
+            return NULL;
+        ctx->kq = q;
+        ctx->kq_cap = nc;
+    }
+    srtp_kdf_job_t *j = &ctx->kq[ctx->kq_n++];
+    memset(j, 0, sizeof *j);
+    return j;
+}
+
+static void release_slot(srtp_t ctx, uint32_t slot)
+{
+    if (!ctx->kq_n) {
+        free_slot_now(ctx, slot);
+        return;
+    }
+    /* a queued job may still write this slot: reuse it after the flush */
+    if (ctx->n_rel == ctx->rel_cap) {
+        size_t nc = ctx->rel_cap ? 2 * ctx->rel_cap : 16;
+        uint32_t *p = (uint32_t *)realloc(ctx->rel, nc * 4);
+        if (!p)
+            return;
+        ctx->rel = p;
+        ctx->rel_cap = nc;
+    }
+    ctx->rel[ctx->n_rel++] = slot;
+}
+
+/* one device key record: on the host (SRTP_MI355X_HOST_KDF=1) or queued for
+ * k_kdf.  `kk` / `ks`: the PRF's AES key (kdf_len bytes) and 14-byte offset;
+ * labels and output lengths as srtp_stream_init_keys draws them. */
+typedef struct {
+    const uint8_t *kk, *ks;
+    size_t kdf_len;
+    uint8_t lab_enc, lab_salt, lab_auth;
+    size_t enc_len, salt_len, auth_len;
+    int hmac, gcm_h, ghash;
+    int tail;                 /* salt bytes salt_len, salt_len + 1 from tail */
+    uint8_t tail_b[2];
+} kspec_t;
+
+static int put_key(srtp_t ctx, uint32_t slot, srtp_dev_key_t *dk,
+                   const kspec_t *q)
+{
+    if (!ctx->host_kdf) {
+        srtp_kdf_job_t *j = kq_push(ctx);
+        if (!j)
+            return -1;
+        j->key = *dk;
+        memcpy(j->kdf_key, q->kk, q->kdf_len);
+        memcpy(j->kdf_salt, q->ks, 14);
+        j->kdf_len = (uint32_t)q->kdf_len;
+        j->lab_enc = q->lab_enc;
+        j->lab_salt = q->lab_salt;
+        j->lab_auth = q->lab_auth;
+        j->enc_len = (uint32_t)q->enc_len;
+        j->salt_len = (uint32_t)q->salt_len;
+        j->auth_len = (uint32_t)q->auth_len;
+        j->flags = (q->hmac ? SRTP_KDF_HMAC : 0) |
+                   (q->gcm_h ? SRTP_KDF_GCM_H : 0) |
+                   (q->ghash ? SRTP_KDF_GHASH : 0) |
+                   (q->tail ? SRTP_KDF_SALT_TAIL : 0);
+        j->salt_tail[0] = q->tail_b[0];
+        j->salt_tail[1] = q->tail_b[1];
+        j->slot = slot;
+        return 0;
+    }
+    hc_aes_t kdf;
+    hc_aes_init(&kdf, q->kk, q->kdf_len);
+    uint8_t ek[32], sa[16], ak[20];
+    memset(sa, 0, sizeof sa);
+    kdf_gen(&kdf, q->ks, q->lab_enc, ek, q->enc_len);
+    kdf_gen(&kdf, q->ks, q->lab_salt, sa, q->salt_len);
+    kdf_gen(&kdf, q->ks, q->lab_auth, ak, q->auth_len);
+    if (q->tail) {
+        sa[q->salt_len] = q->tail_b[0];
+        sa[q->salt_len + 1] = q->tail_b[1];
+    }
+    for (int i = 0; i < 4; i++)
+        dk->salt[i] = (uint32_t)sa[4 * i] | (uint32_t)sa[4 * i + 1] << 8 |
+                      (uint32_t)sa[4 * i + 2] << 16 | (uint32_t)sa[4 * i + 3] << 24;
+    uint32_t gbuf[1024];
+    uint32_t *gtab = NULL;
+    if (q->enc_len) {
+        hc_aes_t ca;
+        hc_aes_init(&ca, ek, q->enc_len);
+        memcpy(dk->rk, ca.rk, sizeof dk->rk);
+        if (q->gcm_h || q->ghash) {
+            uint8_t z[16] = { 0 }, h[16];
+            hc_aes_block(&ca, z, h);
+            for (int i = 0; i < 4; i++)
+                dk->h[i] = (uint32_t)h[4 * i] << 24 | (uint32_t)h[4 * i + 1] << 16 |
+                           (uint32_t)h[4 * i + 2] << 8 | h[4 * i + 3];
+            if (q->ghash) {
+                hc_ghash_table(h, gbuf);
+                gtab = gbuf;
+            }
+        }
+    }
+    if (q->hmac) {
+        uint8_t pad[64];
+        for (int i = 0; i < 64; i++)
+            pad[i] = (uint8_t)((i < (int)q->auth_len ? ak[i] : 0) ^ 0x36);
+        hc_sha1_midstate(pad, dk->ipad);
+        for (int i = 0; i < 64; i++)
+            pad[i] = (uint8_t)((i < (int)q->auth_len ? ak[i] : 0) ^ 0x5c);
+        hc_sha1_midstate(pad, dk->opad);
+    }
+    memset(ek, 0, sizeof ek);
+    memset(ak, 0, sizeof ak);
+    return srtp_gpu_set_key(ctx->gpu, slot, dk, gtab);
+}
+
+/* srtp_stream_init_keys (srtp.c:1233-1607) for one master key: the host
+ * settles every policy question and the record layout; the derivations run
+ * in put_key */
 static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
                                   const srtp_policy_t *p, const uint8_t *master,
                                   const uint8_t *mki_id, size_t mki_size)
@@ -604,22 +772,16 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         kdf_keylen += 2; /* srtp.c:1309-1312 */
     if (kdf_keylen != 30 && kdf_keylen != 38 && kdf_keylen != 46)
         return srtp_err_status_init_fail;
+    if (base != 0 && base != 16 && base != 24 && base != 32)
+        return srtp_err_status_init_fail;
 
+    /* the PRF: AES keyed by the zero-padded master key, offset = the 14
+     * bytes after it (srtp.c:1322-1340) */
     uint8_t tmp[256];
     memset(tmp, 0, sizeof tmp);
     memcpy(tmp, master, input_keylen);
-    hc_aes_t kdf;
-    hc_aes_init(&kdf, tmp, kdf_keylen - SRTP_SALT_LEN);
-    uint8_t kdf_salt[14];
-    memcpy(kdf_salt, tmp + kdf_keylen - SRTP_SALT_LEN, 14);
-
-    uint8_t ek[32], salt[64], ak[20];
-    memset(salt, 0, sizeof salt);
-    kdf_gen(&kdf, kdf_salt, 0x00, ek, base);
-    if (salt_len > 0)
-        kdf_gen(&kdf, kdf_salt, 0x02, salt, salt_len);
-    size_t auth_key_len = rtp->auth_type == SRTP_HMAC_SHA1 ? rtp->auth_key_len : 0;
-    kdf_gen(&kdf, kdf_salt, 0x01, ak, auth_key_len);
+    const size_t kdf_len = kdf_keylen - SRTP_SALT_LEN;
+    const uint8_t *kdf_salt = tmp + kdf_len;
 
     srtp_dev_key_t dk;
     memset(&dk, 0, sizeof dk);
@@ -636,28 +798,16 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
     dk.conf = (rtp->sec_serv & sec_serv_conf) ? 1 : 0;
 
     int rc_code = 0;
-    uint32_t *gtab = NULL;
-    uint32_t gbuf[1024];
     if (rtp->cipher_type == SRTP_NULL_CIPHER) {
         hk->family = SRTP_DEV_NULL;
         hk->rounds = 0;
         dk.conf = 0;
     } else {
-        hc_aes_t ca;
-        hc_aes_init(&ca, ek, base);
-        memcpy(dk.rk, ca.rk, sizeof dk.rk);
-        hk->rounds = (uint32_t)ca.rounds;
-        rc_code = (ca.rounds - 8) / 2;
+        hk->rounds = (uint32_t)(base / 4 + 6);
+        rc_code = ((int)hk->rounds - 8) / 2;
         if (rtp->cipher_type == SRTP_AES_GCM_128 ||
             rtp->cipher_type == SRTP_AES_GCM_256) {
             hk->family = SRTP_DEV_GCM;
-            uint8_t z[16] = { 0 }, h[16];
-            hc_aes_block(&ca, z, h);
-            for (int i = 0; i < 4; i++)
-                dk.h[i] = (uint32_t)h[4 * i] << 24 | (uint32_t)h[4 * i + 1] << 16 |
-                          (uint32_t)h[4 * i + 2] << 8 | h[4 * i + 3];
-            hc_ghash_table(h, gbuf);
-            gtab = gbuf;
             dk.conf = 1; /* AEAD always encrypts (srtp.c:2088-2098) */
         } else {
             hk->family = SRTP_DEV_ICM;
@@ -665,34 +815,94 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
     }
     dk.rounds = hk->rounds;
     dk.family = hk->family;
-    /* salt as little-endian words; bytes past the salt are zero */
-    uint8_t sb[16];
-    memset(sb, 0, sizeof sb);
-    if (hk->family == SRTP_DEV_ICM)
-        memcpy(sb, salt, 14);
-    else if (hk->family == SRTP_DEV_GCM)
-        memcpy(sb, salt, 12);
-    for (int i = 0; i < 4; i++)
-        dk.salt[i] = (uint32_t)sb[4 * i] | (uint32_t)sb[4 * i + 1] << 8 |
-                     (uint32_t)sb[4 * i + 2] << 16 | (uint32_t)sb[4 * i + 3] << 24;
     int auth_on = rtp->auth_type == SRTP_HMAC_SHA1 &&
                   (rtp->sec_serv & sec_serv_auth) && hk->family != SRTP_DEV_GCM;
     dk.auth = (uint32_t)auth_on;
-    if (rtp->auth_type == SRTP_HMAC_SHA1) {
-        uint8_t pad[64];
-        for (int i = 0; i < 64; i++)
-            pad[i] = (uint8_t)((i < (int)auth_key_len ? ak[i] : 0) ^ 0x36);
-        hc_sha1_midstate(pad, dk.ipad);
-        for (int i = 0; i < 64; i++)
-            pad[i] = (uint8_t)((i < (int)auth_key_len ? ak[i] : 0) ^ 0x5c);
-        hc_sha1_midstate(pad, dk.opad);
-    }
     hk->variant = hk->family == SRTP_DEV_GCM
                       ? SRTP_VARIANT(SRTP_DEV_GCM, rc_code, 0)
                       : SRTP_VARIANT(hk->family, hk->family ? rc_code : 0,
                                      auth_on);
     hk->slot = alloc_slot(ctx);
     dk.ghash_slot = hk->slot;
+
+    /* RFC 6904 header-extension encryption and RFC 9335 cryptex
+     * (srtp.c:694-749, 1385-1500): every packet of such a stream goes to
+     * k_xrtp; the extension cipher is the RTP cipher's type, or AES-ICM of
+     * the same size for AES-GCM */
+    hk->xslot = 0xffffffffu;
+    const int xtn = p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0;
+    if (xtn || p->use_cryptex) {
+        hk->variant = SRTP_VARIANT_X;
+        dk.xflags = (p->use_cryptex ? SRTP_XF_CRYPTEX : 0) |
+                    ((rtp->sec_serv & sec_serv_conf) ? SRTP_XF_CONF : 0);
+    }
+    if (xtn) {
+        for (size_t i = 0; i < p->enc_xtn_hdr_count; i++)
+            dk.xids[p->enc_xtn_hdr[i] >> 5] |= 1u << (p->enc_xtn_hdr[i] & 31);
+        dk.xflags |= SRTP_XF_XTN;
+        hk->xslot = alloc_slot(ctx);
+        dk.xslot = hk->xslot;
+        srtp_dev_key_t xk;
+        memset(&xk, 0, sizeof xk);
+        xk.family = SRTP_DEV_NULL;
+        xk.ghash_slot = hk->xslot;
+        uint8_t tx[256];
+        memset(tx, 0, sizeof tx);
+        kspec_t q;
+        memset(&q, 0, sizeof q);
+        q.kk = tmp;
+        q.ks = kdf_salt;
+        q.kdf_len = kdf_len;
+        q.lab_enc = 0x06; /* label_rtp_header_encryption */
+        q.lab_salt = 0x07; /* label_rtp_header_salt */
+        if (hk->family != SRTP_DEV_NULL) {
+            xk.family = SRTP_DEV_ICM;
+            xk.rounds = hk->rounds;
+            q.enc_len = base;
+            q.salt_len = 14;
+            if (hk->family == SRTP_DEV_GCM) {
+                /* a PRF of its own over the master key and the 12-byte
+                 * salt, zero padded (srtp.c:1393-1441); the ICM cipher then
+                 * reads 14 salt bytes, the last two being what the key
+                 * buffer holds there (srtp.c:1487) */
+                memcpy(tx, master, base + salt_len);
+                q.kk = tx;
+                q.ks = tx + kdf_len;
+                q.salt_len = salt_len;
+                q.tail = 1;
+                q.tail_b[0] = tmp[base + 12];
+                q.tail_b[1] = tmp[base + 13];
+            }
+        }
+        int bad = put_key(ctx, hk->xslot, &xk, &q);
+        memset(tx, 0, sizeof tx);
+        if (bad)
+            return srtp_err_status_init_fail;
+    }
+
+    /* the RTP record: labels 0 (cipher key), 2 (salt), 1 (auth key) */
+    {
+        kspec_t q;
+        memset(&q, 0, sizeof q);
+        q.kk = tmp;
+        q.ks = kdf_salt;
+        q.kdf_len = kdf_len;
+        q.lab_enc = 0x00;
+        q.lab_salt = 0x02;
+        q.lab_auth = 0x01;
+        q.enc_len = hk->family == SRTP_DEV_NULL ? 0 : base;
+        /* the record keeps 14 salt bytes for ICM, 12 for GCM (the rest of
+         * the PRF's salt output is not used) */
+        q.salt_len = hk->family == SRTP_DEV_ICM ? 14
+                     : hk->family == SRTP_DEV_GCM ? 12 : 0;
+        q.hmac = rtp->auth_type == SRTP_HMAC_SHA1;
+        q.auth_len = q.hmac ? rtp->auth_key_len : 0;
+        q.ghash = hk->family == SRTP_DEV_GCM;
+        q.gcm_h = q.ghash;
+        srtp_dev_key_t rk = dk;
+        if (put_key(ctx, hk->slot, &rk, &q))
+            return srtp_err_status_init_fail;
+    }
 
     /* SRTCP key: srtp.c:1527-1600 (labels 3 encryption, 5 salt, 4 auth).
      * AEAD RTCP stays off the GPU path (srtp_protect_rtcp reports
@@ -713,123 +923,42 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         srtp_dev_key_t rk;
         memset(&rk, 0, sizeof rk);
         size_t rbase = base_key_length(rtcp->cipher_type, rtcp_keylen);
-        size_t rsalt_len = rtcp->cipher_type == SRTP_NULL_CIPHER
-                               ? 0 : rtcp_keylen - rbase; /* 14 ICM, 12 GCM */
-        uint8_t rek[32], rsalt[16], rak[20];
-        memset(rsalt, 0, sizeof rsalt);
         memcpy(rk.mki, hk->mki, sizeof rk.mki);
         rk.mki_size = (uint32_t)mki_size;
         rk.tag_len = (uint32_t)rtcp->auth_tag_len;
+        kspec_t q;
+        memset(&q, 0, sizeof q);
+        q.kk = tmp;
+        q.ks = kdf_salt;
+        q.kdf_len = kdf_len;
+        q.lab_enc = 0x03;
+        q.lab_salt = 0x05;
+        q.lab_auth = 0x04;
         if (rtcp->cipher_type == SRTP_NULL_CIPHER) {
             rk.family = SRTP_DEV_NULL;
         } else {
-            kdf_gen(&kdf, kdf_salt, 0x03, rek, rbase);
-            if (rsalt_len > 0)
-                kdf_gen(&kdf, kdf_salt, 0x05, rsalt, rsalt_len);
-            hc_aes_t ca;
-            hc_aes_init(&ca, rek, rbase);
-            memcpy(rk.rk, ca.rk, sizeof rk.rk);
-            rk.rounds = (uint32_t)ca.rounds;
+            if (rbase != 16 && rbase != 24 && rbase != 32)
+                return srtp_err_status_init_fail;
+            q.enc_len = rbase;
+            q.salt_len = rtcp_keylen - rbase; /* 14 ICM, 12 GCM */
+            if (q.salt_len > 14)
+                q.salt_len = 14;
+            rk.rounds = (uint32_t)(rbase / 4 + 6);
             rk.family = rtcp_gcm ? SRTP_DEV_GCM : SRTP_DEV_ICM;
             rk.conf = 1;
-            if (rtcp_gcm) {
-                uint8_t z[16] = { 0 }, h[16];
-                hc_aes_block(&ca, z, h);
-                for (int i = 0; i < 4; i++)
-                    rk.h[i] = (uint32_t)h[4 * i] << 24 |
-                              (uint32_t)h[4 * i + 1] << 16 |
-                              (uint32_t)h[4 * i + 2] << 8 | h[4 * i + 3];
-            }
+            q.gcm_h = rtcp_gcm;
         }
-        for (int i = 0; i < 4; i++)
-            rk.salt[i] = (uint32_t)rsalt[4 * i] | (uint32_t)rsalt[4 * i + 1] << 8 |
-                         (uint32_t)rsalt[4 * i + 2] << 16 |
-                         (uint32_t)rsalt[4 * i + 3] << 24;
         if (rtcp->auth_type == SRTP_HMAC_SHA1 && !rtcp_gcm) {
-            size_t rakl = rtcp->auth_key_len;
-            kdf_gen(&kdf, kdf_salt, 0x04, rak, rakl);
-            uint8_t pad[64];
-            for (int i = 0; i < 64; i++)
-                pad[i] = (uint8_t)((i < (int)rakl ? rak[i] : 0) ^ 0x36);
-            hc_sha1_midstate(pad, rk.ipad);
-            for (int i = 0; i < 64; i++)
-                pad[i] = (uint8_t)((i < (int)rakl ? rak[i] : 0) ^ 0x5c);
-            hc_sha1_midstate(pad, rk.opad);
+            q.hmac = 1;
+            q.auth_len = rtcp->auth_key_len;
             rk.auth = 1;
         }
         hk->rslot = alloc_slot(ctx);
         rk.ghash_slot = hk->rslot;
-        memset(rek, 0, sizeof rek);
-        memset(rak, 0, sizeof rak);
-        if (srtp_gpu_set_key(ctx->gpu, hk->rslot, &rk, NULL))
-            return srtp_err_status_init_fail;
-    }
-    /* RFC 6904 header-extension encryption and RFC 9335 cryptex
-     * (srtp.c:694-749, 1385-1500): every packet of such a stream goes to
-     * k_xrtp; the extension cipher is the RTP cipher's type, or AES-ICM of
-     * the same key size for AES-GCM */
-    hk->xslot = 0xffffffffu;
-    const int xtn = p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0;
-    if (xtn || p->use_cryptex) {
-        hk->variant = SRTP_VARIANT_X;
-        dk.xflags = (p->use_cryptex ? SRTP_XF_CRYPTEX : 0) |
-                    ((rtp->sec_serv & sec_serv_conf) ? SRTP_XF_CONF : 0);
-    }
-    if (xtn) {
-        srtp_dev_key_t xk;
-        memset(&xk, 0, sizeof xk);
-        for (size_t i = 0; i < p->enc_xtn_hdr_count; i++)
-            dk.xids[p->enc_xtn_hdr[i] >> 5] |= 1u << (p->enc_xtn_hdr[i] & 31);
-        dk.xflags |= SRTP_XF_XTN;
-        xk.family = SRTP_DEV_NULL;
-        if (hk->family != SRTP_DEV_NULL) {
-            uint8_t xkey[32], xsalt[16];
-            memset(xsalt, 0, sizeof xsalt);
-            if (hk->family == SRTP_DEV_GCM) {
-                /* a KDF of its own over the master key and the 12-byte
-                 * salt, zero padded (srtp.c:1393-1441); the ICM cipher then
-                 * reads 14 salt bytes, the last two being what the key
-                 * buffer holds there (srtp.c:1487) */
-                uint8_t tx[256];
-                memset(tx, 0, sizeof tx);
-                memcpy(tx, master, base + salt_len);
-                hc_aes_t xkdf;
-                hc_aes_init(&xkdf, tx, kdf_keylen - SRTP_SALT_LEN);
-                uint8_t xks[14];
-                memcpy(xks, tx + kdf_keylen - SRTP_SALT_LEN, 14);
-                kdf_gen(&xkdf, xks, 0x06, xkey, base);
-                kdf_gen(&xkdf, xks, 0x07, xsalt, salt_len);
-                xsalt[12] = tmp[base + 12];
-                xsalt[13] = tmp[base + 13];
-                memset(tx, 0, sizeof tx);
-            } else {
-                /* same cipher type: the main KDF, labels 6 and 7 */
-                kdf_gen(&kdf, kdf_salt, 0x06, xkey, base);
-                kdf_gen(&kdf, kdf_salt, 0x07, xsalt, 14);
-            }
-            hc_aes_t xa;
-            hc_aes_init(&xa, xkey, base);
-            memcpy(xk.rk, xa.rk, sizeof xk.rk);
-            xk.rounds = (uint32_t)xa.rounds;
-            xk.family = SRTP_DEV_ICM;
-            for (int i = 0; i < 4; i++)
-                xk.salt[i] = (uint32_t)xsalt[4 * i] |
-                             (uint32_t)xsalt[4 * i + 1] << 8 |
-                             (uint32_t)xsalt[4 * i + 2] << 16 |
-                             (uint32_t)xsalt[4 * i + 3] << 24;
-            memset(xkey, 0, sizeof xkey);
-        }
-        hk->xslot = alloc_slot(ctx);
-        xk.ghash_slot = hk->xslot;
-        dk.xslot = hk->xslot;
-        if (srtp_gpu_set_key(ctx->gpu, hk->xslot, &xk, NULL))
+        if (put_key(ctx, hk->rslot, &rk, &q))
             return srtp_err_status_init_fail;
     }
     memset(tmp, 0, sizeof tmp);
-    memset(ek, 0, sizeof ek);
-    memset(ak, 0, sizeof ak);
-    if (srtp_gpu_set_key(ctx->gpu, hk->slot, &dk, gtab))
-        return srtp_err_status_init_fail;
     ctx->variant_mask |= 1u << hk->variant;
     return srtp_err_status_ok;
 }
@@ -1015,15 +1144,23 @@ static srtp_err_status_t add_stream(srtp_t ctx, const srtp_policy_t *p)
     }
 }
 
-srtp_err_status_t srtp_stream_add(srtp_t ctx, const srtp_policy_t *p)
+static srtp_err_status_t stream_add_queued(srtp_t ctx, const srtp_policy_t *p)
 {
-    if (!ctx)
-        return srtp_err_status_bad_param;
     dev_pull(ctx);
     srtp_err_status_t st = valid_policy(p);
     if (st)
         return st;
     return add_stream(ctx, p);
+}
+
+srtp_err_status_t srtp_stream_add(srtp_t ctx, const srtp_policy_t *p)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st = stream_add_queued(ctx, p);
+    if (kq_flush(ctx) && !st)
+        st = srtp_err_status_init_fail;
+    return st;
 }
 
 srtp_err_status_t srtp_create(srtp_t *session, const srtp_policy_t *policy)
@@ -1043,14 +1180,24 @@ srtp_err_status_t srtp_create(srtp_t *session, const srtp_policy_t *policy)
         return srtp_err_status_init_fail;
     }
     map_rebuild(ctx, 64);
+    {
+        const char *e = getenv("SRTP_MI355X_HOST_KDF");
+        ctx->host_kdf = e && e[0] == '1';
+    }
     *session = ctx;
+    /* every stream's session keys are derived in one k_kdf launch */
     for (const srtp_policy_t *p = policy; p; p = p->next) {
-        srtp_err_status_t st = srtp_stream_add(ctx, p);
+        srtp_err_status_t st = stream_add_queued(ctx, p);
         if (st) {
             srtp_dealloc(ctx);
             *session = NULL;
             return st;
         }
+    }
+    if (kq_flush(ctx)) {
+        srtp_dealloc(ctx);
+        *session = NULL;
+        return srtp_err_status_init_fail;
     }
     return srtp_err_status_ok;
 }
@@ -1067,6 +1214,8 @@ static void stage_free(stage_t *st)
     srtp_gpu_free(st->d_auth);
     srtp_gpu_host_free(st->h_hdr);
     srtp_gpu_free(st->d_hdr);
+    srtp_gpu_host_free(st->h_xinfo);
+    srtp_gpu_free(st->d_xinfo);
     srtp_gpu_host_free(st->h_len);
     srtp_gpu_free(st->d_len);
     srtp_gpu_host_free(st->h_cap);
@@ -1080,6 +1229,7 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    ctx->kq_n = 0; /* keys about to be freed need no derivation */
     for (size_t i = 0; i < ctx->n; i++)
         stream_free(ctx, ctx->list[i]);
     stream_free(ctx, ctx->templ);
@@ -1091,6 +1241,8 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
     free(ctx->dt.sv);
     free(ctx->dt.hs);
     free(ctx->dt.hwin);
+    free(ctx->kq);
+    free(ctx->rel);
     srtp_gpu_close(ctx->gpu);
     free(ctx);
     return srtp_err_status_ok;
@@ -1129,21 +1281,18 @@ static srtp_err_status_t update_specific(srtp_t ctx, const srtp_policy_t *p)
         return srtp_err_status_bad_param;
     /* the extended sequence number and the SRTCP replay database survive
      * the update (srtp.c:3594-3614: old_index, old_rtcp_rdb) */
-    uint64_t old_index = s->rdbx.index;
-    uint32_t old_rtcp_start = s->rtcp_start, old_rtcp_bm[4];
-    memcpy(old_rtcp_bm, s->rtcp_bm, sizeof old_rtcp_bm);
-    srtp_err_status_t st = srtp_stream_remove(ctx, p->ssrc.value);
+    /* the reference removes the stream and adds a new one; here the new
+     * stream takes the old one's place (the list order is not observable),
+     * so a rekey of n streams is O(n) and its keys derive in one launch */
+    srtp_stream_ctx_t *ns;
+    srtp_err_status_t st = stream_new(ctx, p, &ns);
     if (st)
         return st;
-    st = srtp_stream_add(ctx, p);
-    if (st)
-        return st;
-    s = map_get(ctx, p->ssrc.value);
-    if (!s)
-        return srtp_err_status_fail;
-    s->rdbx.index = old_index;
-    s->rtcp_start = old_rtcp_start;
-    memcpy(s->rtcp_bm, old_rtcp_bm, sizeof old_rtcp_bm);
+    ns->rdbx.index = s->rdbx.index;
+    ns->rtcp_start = s->rtcp_start;
+    memcpy(ns->rtcp_bm, s->rtcp_bm, sizeof ns->rtcp_bm);
+    list_replace(ctx, s, ns);
+    stream_free(ctx, s);
     return srtp_err_status_ok;
 }
 
@@ -1176,6 +1325,7 @@ static srtp_err_status_t update_template(srtp_t ctx, const srtp_policy_t *p)
         c->rdbx.index = s->rdbx.index;
         c->rtcp_start = s->rtcp_start;
         memcpy(c->rtcp_bm, s->rtcp_bm, sizeof c->rtcp_bm);
+        c->lpos = i;
         ctx->list[i] = c;
         stream_free(ctx, s);
     }
@@ -1185,10 +1335,9 @@ static srtp_err_status_t update_template(srtp_t ctx, const srtp_policy_t *p)
     return srtp_err_status_ok;
 }
 
-srtp_err_status_t srtp_stream_update(srtp_t ctx, const srtp_policy_t *p)
+static srtp_err_status_t stream_update_queued(srtp_t ctx,
+                                              const srtp_policy_t *p)
 {
-    if (!ctx)
-        return srtp_err_status_bad_param;
     dev_pull(ctx);
     srtp_err_status_t st = valid_policy(p);
     if (st)
@@ -1204,6 +1353,17 @@ srtp_err_status_t srtp_stream_update(srtp_t ctx, const srtp_policy_t *p)
     }
 }
 
+srtp_err_status_t srtp_stream_update(srtp_t ctx, const srtp_policy_t *p)
+{
+    if (!ctx)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st = stream_update_queued(ctx, p);
+    if (kq_flush(ctx) && !st)
+        st = srtp_err_status_init_fail;
+    return st;
+}
+
+/* a rekey of every stream in the list: one k_kdf launch */
 srtp_err_status_t srtp_update(srtp_t ctx, const srtp_policy_t *p)
 {
     if (!ctx)
@@ -1211,12 +1371,11 @@ srtp_err_status_t srtp_update(srtp_t ctx, const srtp_policy_t *p)
     srtp_err_status_t st = valid_policy(p);
     if (st)
         return st;
-    for (; p; p = p->next) {
-        st = srtp_stream_update(ctx, p);
-        if (st)
-            return st;
-    }
-    return srtp_err_status_ok;
+    for (; p && !st; p = p->next)
+        st = stream_update_queued(ctx, p);
+    if (kq_flush(ctx) && !st)
+        st = srtp_err_status_init_fail;
+    return st;
 }
 
 /* ------------------------------------------------------------------------
@@ -1272,14 +1431,14 @@ static void summarize(const uint8_t *p, size_t len, pkt_sum_t *s)
     s->enc_start = (uint32_t)h;
 }
 
-static void from_dev_hdr(const srtp_dev_hdr_t *d, pkt_sum_t *s)
+static void from_dev_hdr(const srtp_dev_hdr_t *d, uint32_t xinfo, pkt_sum_t *s)
 {
     s->ssrc = d->ssrc;
     s->seq = (uint16_t)(d->seq_len & 0xffff);
     s->len = d->len;
-    s->profile = (uint16_t)(d->xinfo & 0xffff);
-    s->cc = (uint8_t)((d->xinfo >> 16) & 15);
-    s->x = (uint8_t)((d->xinfo >> 20) & 1);
+    s->profile = (uint16_t)(xinfo & 0xffff);
+    s->cc = (uint8_t)((xinfo >> 16) & 15);
+    s->x = (uint8_t)((xinfo >> 20) & 1);
     s->inplace = 0;
     if (d->enc_start >> 24) {
         s->err = (uint16_t)(d->enc_start >> 24);
@@ -1752,6 +1911,7 @@ static int stage_reserve(srtp_t ctx, size_t n, size_t arena)
         REALLOC_PAIR(h_meta, d_meta, srtp_dev_meta_t)
         REALLOC_PAIR(h_auth, d_auth, uint8_t)
         REALLOC_PAIR(h_hdr, d_hdr, srtp_dev_hdr_t)
+        REALLOC_PAIR(h_xinfo, d_xinfo, uint32_t)
         REALLOC_PAIR(h_len, d_len, uint32_t)
         REALLOC_PAIR(h_cap, d_cap, uint32_t)
         REALLOC_PAIR(h_st, d_st, int32_t)
@@ -2340,9 +2500,10 @@ static srtp_err_status_t dev_headers(srtp_t ctx, const srtp_device_batch_t *b,
     if (stage_reserve(ctx, b->n, 0))
         return srtp_err_status_alloc_fail;
     if (srtp_gpu_parse(ctx->gpu, b->n, b->in, b->in_off, b->in_len, sg->d_hdr,
-                       b->stream) ||
+                       sg->d_xinfo, b->stream) ||
         srtp_gpu_d2h(ctx->gpu, sg->h_hdr, sg->d_hdr, b->n * sizeof *sg->h_hdr,
-                     b->stream))
+                     b->stream) ||
+        srtp_gpu_d2h(ctx->gpu, sg->h_xinfo, sg->d_xinfo, b->n * 4, b->stream))
         return srtp_err_status_fail;
     /* capacities: the caller's out_len array */
     uint32_t *caps = (uint32_t *)sg->h_arena;
@@ -2353,7 +2514,7 @@ static srtp_err_status_t dev_headers(srtp_t ctx, const srtp_device_batch_t *b,
         srtp_gpu_sync(ctx->gpu, b->stream))
         return srtp_err_status_fail;
     for (size_t i = 0; i < b->n; i++) {
-        from_dev_hdr(&sg->h_hdr[i], &sum[i]);
+        from_dev_hdr(&sg->h_hdr[i], sg->h_xinfo[i], &sum[i]);
         /* same arena: in place (an overlapping, different offset is not a
          * supported layout) */
         sum[i].inplace = b->in == b->out;

@@ -27,7 +27,6 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
     h.len = len;
     h.ssrc = 0;
     h.seq_len = 0;
-    h.xinfo = 0;
     uint32_t err = 0, es = 0;
     if ((off & 15) != 0) {
         err = 2;
@@ -38,7 +37,6 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
         h.ssrc = srtp_bswap32(*(const uint32_t *)(p + 8));
         h.seq_len = w0 & 0xffffu;
         es = 12 + 4 * ((w0 >> 24) & 0xfu);
-        h.xinfo = ((w0 >> 24) & 0xfu) << 16 | ((w0 >> 28) & 1u) << 20;
         if (len < es) {
             err = 2;
         } else if ((w0 >> 28) & 1) {
@@ -46,7 +44,6 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
                 err = 2;
             } else {
                 uint32_t xw = srtp_bswap32(*(const uint32_t *)(p + es));
-                h.xinfo |= xw >> 16;
                 es += ((xw & 0xffffu) + 1) * 4;
                 if (len < es)
                     err = 2;
@@ -55,6 +52,21 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
     }
     h.enc_start = err ? (err << 24) : es;
     return h;
+}
+
+// CSRC count, X bit and extension profile of a header srtp_parse_rtp
+// accepted: [15:0] profile, [19:16] CC, bit 20 X
+__device__ __forceinline__ uint32_t srtp_rtp_xinfo(const uint8_t *p,
+                                                   const srtp_dev_hdr_t &h)
+{
+    if (h.enc_start >> 24)
+        return 0;
+    const uint32_t w0 = srtp_bswap32(*(const uint32_t *)p);
+    const uint32_t cc = (w0 >> 24) & 0xfu, x = (w0 >> 28) & 1u;
+    uint32_t v = cc << 16 | x << 20;
+    if (x)
+        v |= srtp_bswap32(*(const uint32_t *)(p + 12 + 4 * cc)) >> 16;
+    return v;
 }
 
 #endif

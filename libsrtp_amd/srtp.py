@@ -288,6 +288,13 @@ class Session:
         h = _PolicyHolder(policy)
         return Status(self.L.srtp_update(self.h, C.byref(h.policy)))
 
+    def update_all(self, policies):
+        """srtp_update with a linked list of policies (one rekey call)"""
+        holders = [_PolicyHolder(p) for p in policies]
+        for a, b in zip(holders, holders[1:]):
+            a.policy.next = C.pointer(b.policy)
+        return Status(self.L.srtp_update(self.h, C.byref(holders[0].policy)))
+
     # -- single packet (srtp_protect / srtp_unprotect) ---------------------
     # inplace=True passes one buffer as both input and output, as the
     # reference's in-place calls do (cryptex behaves differently then)

@@ -319,14 +319,19 @@ def test_device_api_vs_oracle(name):
             assert host2[offs2[i]:offs2[i] + olen2[i]] == ref, i
 
 
-def test_large_uniform_batch_roundtrip():
-    """64k x 1400 B through the device API (the bench shape, scaled down):
-    protect -> unprotect must restore every packet; a sample is compared
-    byte-for-byte with the oracle."""
+@pytest.mark.parametrize("name,n,trailer", [
+    ("icm128_hmac80", 65536, 10),
+    ("icm128_hmac80", 1 << 20, 10),   # configs[1] at its own size
+    ("gcm256_16", 65536, 16),         # configs[2]'s cipher, uniform key
+])
+def test_large_uniform_batch_roundtrip(name, n, trailer):
+    """n x 1400 B through the device API (the bench shape): protect ->
+    unprotect must restore every packet; a prefix is compared byte-for-byte
+    with the oracle."""
     _gpu()
     import torch
-    n, payload = 65536, 1400
-    pol = policy("icm128_hmac80")
+    payload = 1400
+    pol = policy(name)
     g = torch.Generator().manual_seed(5)
     body = torch.randint(0, 256, (n, payload), dtype=torch.uint8, generator=g)
     slot = (12 + payload + 160 + 15) & ~15
@@ -340,7 +345,8 @@ def test_large_uniform_batch_roundtrip():
     arena = torch.zeros((n, slot), dtype=torch.uint8)
     arena[:, :12] = hdr
     arena[:, 12:12 + payload] = body
-    orig = arena.clone()
+    del body
+    orig = arena
     d = arena.reshape(-1).cuda()
     off = (torch.arange(n, dtype=torch.int64) * slot).cuda()
     ln = torch.full((n,), 12 + payload, dtype=torch.int32).cuda()
@@ -349,18 +355,22 @@ def test_large_uniform_batch_roundtrip():
     s = L.Session([pol])
     assert s.protect_device(d, off, ln, d, off, cap, st) == 0
     assert int(st.abs().sum()) == 0
-    assert bool((cap == 12 + payload + 10).all())
+    assert bool((cap == 12 + payload + trailer).all())
     prot = d.cpu().reshape(n, slot)
-    # whole-batch check through the oracle in order for a prefix
+    # the oracle, in order, on a prefix
     orc2 = O.Session([pol])
     for i in range(2000):
         rc, ref = orc2.protect(bytes(orig[i, :12 + payload].numpy()), slot)
         assert rc == 0 and bytes(prot[i, :len(ref)].numpy()) == ref, i
+    # ciphertext differs from the plaintext everywhere but the header
+    assert not torch.equal(prot[:, 12:12 + payload], orig[:, 12:12 + payload])
+    del prot
     r = L.Session([pol])
     ln2 = cap.clone()
     cap2 = ln2.clone()
     st2 = torch.zeros(n, dtype=torch.int32).cuda()
     assert r.unprotect_device(d, off, ln2, d, off, cap2, st2) == 0
     assert int(st2.abs().sum()) == 0
+    assert bool((cap2 == 12 + payload).all())
     back = d.cpu().reshape(n, slot)
     assert torch.equal(back[:, :12 + payload], orig[:, :12 + payload])
