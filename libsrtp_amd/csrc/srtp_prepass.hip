@@ -108,9 +108,13 @@ struct ClassifyArgs {
     srtp_dev_hdr_t *hdr;
     uint32_t *pstat, *skey, *perm, *bcount, *abort;
     // order-free form only (null otherwise): per-packet index guessed from
-    // the stored index, per-stream highest index
+    // the stored index, per-stream highest index; the packet's crypto
+    // descriptor and protected length, written here (no header summary and
+    // no permutation are kept: commit only copies status and length)
     uint64_t *est;
     unsigned long long *new_index;
+    srtp_dev_meta_t *meta;
+    uint32_t *olen;
 };
 
 // index_guess against a stream's stored index (srtp_host.c estimate /
@@ -215,7 +219,8 @@ __device__ void agg_stream(uint32_t key, uint64_t e, uint32_t *bcount,
     }
 }
 
-__device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i);
+__device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i,
+                                 srtp_dev_hdr_t &h);
 
 // parse, stream lookup, the per-packet checks of pre_protect that do not
 // depend on stream state (srtp_host.c pre_protect; srtp.c:2515-2600)
@@ -225,15 +230,32 @@ __global__ void k_pp_classify(ClassifyArgs A)
     uint32_t key = NOCHAIN;
     uint64_t e = 0;
     if (i < A.n) {
-        key = classify_one(A, i);
-        if (A.est && key != NOCHAIN) {
-            const uint32_t seq = A.hdr[i].seq_len & 0xffffu;
-            // at or below the stored index (a replay, or an advance the
-            // guess from the stored index cannot see): the sorted path
-            // decides
-            if (guess_index(A.st[key].index, seq, &e) < 1)
-                atomicOr(A.abort, AB_ORDER);
-            A.est[i] = e;
+        srtp_dev_hdr_t h;
+        key = classify_one(A, i, h);
+        if (A.est) {
+            srtp_dev_meta_t m;
+            m.key = 0;
+            m.roc = 0;
+            m.len = 0;
+            m.info = 0xff0000u;   // no crypto
+            if (key != NOCHAIN) {
+                const srtp_dev_stream_t &S = A.st[key];
+                const uint32_t seq = h.seq_len & 0xffffu;
+                // at or below the stored index (a replay, or an advance the
+                // guess from the stored index cannot see): the sorted path
+                // decides
+                if (guess_index(S.index, seq, &e) < 1)
+                    atomicOr(A.abort, AB_ORDER);
+                A.est[i] = e;
+                if (A.pstat[i] == 0) {
+                    m.key = S.key;
+                    m.roc = (uint32_t)(e >> 16);
+                    m.info = h.enc_start | (S.variant << 24);
+                    m.len = h.len;
+                    A.olen[i] = h.len + S.trailer;
+                }
+            }
+            A.meta[i] = m;
         }
     }
     if (A.est)
@@ -270,13 +292,16 @@ __global__ void k_pp_usetbits(const uint32_t *skey, const uint64_t *est,
 
 // one packet of k_pp_classify: header, stream, status code; returns the
 // chain key (stream id) or NOCHAIN
-__device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i)
+__device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i,
+                                 srtp_dev_hdr_t &h)
 {
     const uint64_t off = A.in_off[i];
     const uint32_t len = A.in_len[i];
-    const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
-    A.hdr[i] = h;
-    A.perm[i] = i;
+    h = srtp_parse_rtp(A.in + off, off, len);
+    if (!A.est) {   // the sorted chain form reads them back
+        A.hdr[i] = h;
+        A.perm[i] = i;
+    }
     uint32_t code = 0, key = NOCHAIN;
     if (h.enc_start >> 24) {
         code = h.enc_start >> 24;   // header does not parse: no stream touched
@@ -501,6 +526,21 @@ __global__ void k_pp_commit_pkt(CommitArgs A)
     }
     A.meta[i] = m;
     A.status[i] = (int32_t)code;   // error packets keep out_len = capacity
+}
+
+// order-free form: classify wrote the descriptors; unless aborted, the
+// caller's status and protected length
+__global__ void k_pp_commit_of(const uint32_t *pstat, const uint32_t *olen,
+                               uint32_t n, const uint32_t *abort,
+                               int32_t *status, uint32_t *out_len)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || *abort)
+        return;
+    const uint32_t code = pstat[i];
+    status[i] = (int32_t)code;
+    if (code == 0)
+        out_len[i] = olen[i];   // error packets keep out_len = capacity
 }
 
 __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
@@ -996,6 +1036,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     C.abort = P->abort;
     C.est = unordered ? P->est : nullptr;
     C.new_index = unordered ? (unsigned long long *)P->new_index : nullptr;
+    C.meta = P->meta;
+    C.olen = P->skey2;   // protected lengths (skey2 is the sorted path's)
     hipLaunchKernelGGL(k_pp_classify, gp, blk, 0, stream, C);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "classify"))
@@ -1070,7 +1112,11 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     K.meta = P->meta;
     K.status = b->status;
     K.out_len = b->out_len;
-    hipLaunchKernelGGL(k_pp_commit_pkt, gp, blk, 0, stream, K);
+    if (unordered)
+        hipLaunchKernelGGL(k_pp_commit_of, gp, blk, 0, stream, P->pstat,
+                           P->skey2, N, P->abort, b->status, b->out_len);
+    else
+        hipLaunchKernelGGL(k_pp_commit_pkt, gp, blk, 0, stream, K);
     if (pp_step(stream, "commit_pkt"))
         return -1;
     hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
