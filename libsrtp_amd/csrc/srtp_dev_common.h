@@ -93,9 +93,8 @@ DEV uint32_t aes_t0(uint32_t x)
 // Fills the replicated tables; every thread of the block must call it.  The
 // caller synchronises the block before the first lookup.
 template <bool TAB4>
-DEV void load_aes_tables(void *lds)
+DEV void load_aes_tables(void *lds, uint32_t *s_t0)   // s_t0: 1 KiB of LDS
 {
-    __shared__ uint32_t s_t0[256];
     for (int x = threadIdx.x; x < 256; x += blockDim.x)
         s_t0[x] = aes_t0((uint32_t)x);
     __syncthreads();
@@ -107,6 +106,13 @@ DEV void load_aes_tables(void *lds)
         const uint32_t v = rotl(s_t0[(e >> 4) & 255], 8 * tab);
         d[e] = u32x4{ v, v, v, v };
     }
+}
+
+template <bool TAB4>
+DEV void load_aes_tables(void *lds)
+{
+    __shared__ uint32_t s_t0[256];
+    load_aes_tables<TAB4>(lds, s_t0);
 }
 
 struct AesLds {

@@ -27,6 +27,15 @@ namespace {
 #ifndef ICM_COOP
 #define ICM_COOP 1   // wave-cooperative coalesced loads / aligned stores
 #endif
+#ifndef ICM_SEQ
+#define ICM_SEQ 0    // low-register cooperative loop (icm_seq_run)
+#endif
+#ifndef ICM_PIPE
+#define ICM_PIPE 0   // icm_seq_run: keystream computed one chunk ahead
+#endif
+#ifndef ICM_LDSX
+#define ICM_LDSX 0   // icm_seq_run: lane-quad exchange through LDS
+#endif
 
 // per-packet constants of the chunk loop
 struct IcmPkt {
@@ -368,6 +377,180 @@ DEV void icm_coop_run(uint32_t &b, uint32_t e, const IcmPkt &p,
             *(u32x4 *)(p.out + 16 * (4 * e - 4 + t)) = prev[t];
 }
 
+// The cooperative steady chunks with a small live set, for 3-4 waves per
+// SIMD (ICM_SEQ): per chunk the keystream, then the exchange and store,
+// then SHA-1, one after the other, so at most one phase's temporaries are
+// live; the other waves of the SIMD fill each phase's LDS / VALU latency.
+// Loads and stores are addressed as 32-bit offsets from the (uniform)
+// arena bases; only the next chunk's data is held ahead.
+template <int S, int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_seq_run(uint32_t &b, uint32_t e, const IcmPkt &p,
+                     const CtrCache &C, const KEY &rk, const AesLds &T,
+                     uint32_t ks_prev[4], uint32_t hst[5], u32x4 (&prev)[4],
+                     const uint8_t *ib, uint8_t *ob, const uint32_t (&io)[4],
+                     const uint32_t (&so)[4], uint32_t r0)
+{
+#if ICM_PIPE
+    // keystream one chunk ahead: chunk b+1's AES and chunk b's SHA-1 share
+    // a basic block, so one wave mixes LDS-bound and VALU-bound work
+    uint32_t ks[4][4];
+    coop_keystream<NR, TAB4>(b, p, C, rk, T, ks);
+#endif
+    for (; b < e; b++) {
+        // the chunk's data is in flight during its keystream
+        u32x4 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            v[j] = *(gcptr)(ib + (io[j] + 64 * b));
+#if !ICM_PIPE
+        uint32_t ks[4][4];
+        coop_keystream<NR, TAB4>(b, p, C, rk, T, ks);
+#endif
+        quad_transpose(v);
+        uint32_t wv[16];
+        if (!PROTECT) {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    wv[4 * t + u] = bswap(v[t][u]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                v[t][u] ^= u >= S ? ks[t][u - S]
+                                  : (t ? ks[t - 1][u - S + 4]
+                                       : ks_prev[u - S + 4]);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            ks_prev[u] = ks[3][u];
+        u32x4 sg[4];
+        seg_funnel(prev, v, r0, sg);
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            prev[t] = v[t];
+        quad_transpose(sg);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            *(gptr)(ob + (so[j] + 64 * b)) = sg[j];
+        if (AUTH && PROTECT) {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    wv[4 * t + u] = bswap(prev[t][u]);
+        }
+#if ICM_PIPE
+        if (b + 1 < e)
+            coop_keystream<NR, TAB4>(b + 1, p, C, rk, T, ks);
+#endif
+        if (AUTH)
+            sha1_compress(hst, wv);
+    }
+    // quads 4e - r0 .. 4e - 1 (the head of segment e) are not stored yet
+#pragma unroll
+    for (int t = 1; t < 4; t++)
+        if (4 - (int)r0 <= t)
+            *(u32x4 *)(p.out + 16 * (4 * e - 4 + t)) = prev[t];
+}
+
+#if ICM_LDSX
+// The cooperative steady chunks with the lane-quad exchange done by the LDS
+// instead of DPP transposes (64 DPP moves + 64 selects per chunk each way).
+// Each wave owns 4 KiB of LDS (xb): one chunk of its 64 packets.
+//   in:  4 global_load_lds_dwordx4 (LDS DMA, no VGPRs, no VALU): in
+//        instruction j, lane 4m+q reads 16 bytes of the chunk of packet
+//        16j+m and the DMA puts them at slot 64j+4m+q; then every lane reads
+//        its own packet's four 16-byte pieces (4 ds_read_b128)
+//   out: every lane writes its aligned segment's four pieces (4
+//        ds_write_b128), lane 4m+q of instruction j reads piece q of the
+//        segment of packet 16j+m back (ds_read_b128) and stores it: 64
+//        contiguous aligned bytes per quad, as before
+// Piece t of the packet of lane L = 4m+j sits in slot 64j + 4m + ((t+m+j)&3):
+// the rotation by m + j keeps every ds_read_b128 lane group (16 lanes) and
+// every ds_write_b128 group (8 lanes) on distinct banks, and the DMA lanes
+// of a quad still read 64 contiguous bytes (in rotated order).
+template <int S, int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_ldsx_run(uint32_t &b, uint32_t e, const IcmPkt &p,
+                      const CtrCache &C, const KEY &rk, const AesLds &T,
+                      uint32_t ks_prev[4], uint32_t hst[5], u32x4 (&prev)[4],
+                      const uint8_t *ib, uint8_t *ob, const uint32_t (&ibq)[4],
+                      const uint32_t (&so)[4], uint32_t r0, u32x4 *xb)
+{
+    const uint32_t L = threadIdx.x & 63, m = L >> 2, q = L & 3;
+    uint32_t io[4], rs[4], ro[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        io[j] = ibq[j] + 16 * ((q - m - (uint32_t)j) & 3);   // DMA source
+        rs[j] = 64 * q + 4 * m + ((j + m + q) & 3);          // own piece j
+        ro[j] = 64 * j + 4 * m + ((q + m + (uint32_t)j) & 3);  // store read
+    }
+    for (; b < e; b++) {
+        // the previous chunk's store reads are complete before the DMA
+        // overwrites the buffer
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            __builtin_amdgcn_global_load_lds(
+                (const void __attribute__((address_space(1))) *)(ib + (io[j] + 64 * b)),
+                (void __attribute__((address_space(3))) *)(xb + 64 * j), 16, 0,
+                0);
+        uint32_t ks[4][4];
+        coop_keystream<NR, TAB4>(b, p, C, rk, T, ks);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        u32x4 v[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            v[t] = xb[rs[t]];
+        uint32_t wv[16];
+        if (!PROTECT) {
+#pragma unroll
+            for (int t = 0; t < 4; t++)
+#pragma unroll
+                for (int u = 0; u < 4; u++)
+                    wv[4 * t + u] = bswap(v[t][u]);
+        }
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                v[t][u] ^= u >= S ? ks[t][u - S]
+                                  : (t ? ks[t - 1][u - S + 4]
+                                       : ks_prev[u - S + 4]);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            ks_prev[u] = ks[3][u];
+        u32x4 sg[4];
+        seg_funnel(prev, v, r0, sg);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            prev[t] = v[t];
+            xb[rs[t]] = sg[t];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            *(gptr)(ob + (so[j] + 64 * b)) = xb[ro[j]];
+        if (AUTH) {
+            if (PROTECT) {
+#pragma unroll
+                for (int t = 0; t < 4; t++)
+#pragma unroll
+                    for (int u = 0; u < 4; u++)
+                        wv[4 * t + u] = bswap(prev[t][u]);
+            }
+            sha1_compress(hst, wv);
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // quads 4e - r0 .. 4e - 1 (the head of segment e) are not stored yet
+#pragma unroll
+    for (int t = 1; t < 4; t++)
+        if (4 - (int)r0 <= t)
+            *(u32x4 *)(p.out + 16 * (4 * e - 4 + t)) = prev[t];
+}
+#endif
+
 // all 64 lanes active and in the same steady state: the cooperative path
 DEV bool wave_uniform(uint32_t x)
 {
@@ -375,22 +558,11 @@ DEV bool wave_uniform(uint32_t x)
            ~0ull;
 }
 
-// one packet, front to back: header chunks, steady payload chunks, tail
-// chunks, partial quad, outer hash, tag (srtp.c:2694-2818 protect,
-// 2987-3093 unprotect: the tag is compared, the caller decides)
-template <int NR, bool TAB4, bool AUTH, bool PROTECT, bool UNIFORM, class KEY>
-DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
+// per-packet constants from the packet's meta record and header
+template <int NR, bool AUTH>
+DEV IcmPkt make_pkt(const IcmArgs &A, uint32_t i, const srtp_dev_meta_t &m,
+                    const srtp_dev_key_t *key)
 {
-    const srtp_dev_meta_t m = A.meta[i];
-    constexpr uint32_t VID = (NR == 0 ? 0u : 8u + 2u * ((NR - 8) / 2)) +
-                             (AUTH ? 1u : 0u);
-    if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
-        return;
-    const uint32_t slot = UNIFORM ? A.uni : m.key;
-    const srtp_dev_key_t *key = A.keys + slot;
-    if constexpr (!UNIFORM && NR > 0)
-        rk.load(key);
-
     IcmPkt p;
     p.in = A.in + A.in_off[i];
     p.out = A.out + A.out_off[i];
@@ -415,6 +587,28 @@ DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
     p.cb[2] = key->salt[2] ^ bswap(m.roc);
     p.cb[3] = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
 
+    return p;
+}
+
+// one packet, front to back: header chunks, steady payload chunks, tail
+// chunks, partial quad, outer hash, tag (srtp.c:2694-2818 protect,
+// 2987-3093 unprotect: the tag is compared, the caller decides)
+template <int NR, bool TAB4, bool AUTH, bool PROTECT, bool UNIFORM, class KEY>
+DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk,
+                    u32x4 *xb)
+{
+    const srtp_dev_meta_t m = A.meta[i];
+    constexpr uint32_t VID = (NR == 0 ? 0u : 8u + 2u * ((NR - 8) / 2)) +
+                             (AUTH ? 1u : 0u);
+    if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
+        return;
+    const uint32_t slot = UNIFORM ? A.uni : m.key;
+    const srtp_dev_key_t *key = A.keys + slot;
+    if constexpr (!UNIFORM && NR > 0)
+        rk.load(key);
+
+    IcmPkt p = make_pkt<NR, AUTH>(A, i, m, key);
+
     uint32_t hst[5];
 #pragma unroll
     for (int k = 0; k < 5; k++)
@@ -424,6 +618,9 @@ DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
     uint32_t tailq[4] = { 0, 0, 0, 0 };
     u32x4 prev[4];   // output quads of the last chunk done
     uint32_t b = 0;
+#ifdef ICM_EXP_NOHEAD   // timing experiment only: skip the header chunks
+    b = p.bclean;
+#endif
     for (; b < p.bclean && b < p.nb; b++)
         icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, rk, T, ks_prev, hst, tailq,
                                            prev);
@@ -432,6 +629,9 @@ DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
     // epoch 0 (j <= 255, 4 KiB of payload)
     uint32_t se = p.L >> 6;
     se = se < ((256 + p.qoff) >> 2) ? se : ((256 + p.qoff) >> 2);
+#ifdef ICM_EXP_NOSTEADY   // timing experiment only: skip the steady chunks
+    b = se;
+#endif
     if (b < se) {
         CtrCache C{};
         if constexpr (NR > 0) {
@@ -448,7 +648,53 @@ DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
                    wave_uniform(p.conf ? 1u : 0u) &&
                    __builtin_amdgcn_ballot_w64(al == 0) == ~0ull;
         }
-        if (coop) {
+#if ICM_SEQ
+        // 32-bit offsets from the arena bases must cover the steady chunks
+        const uint8_t *ib = A.in;
+        uint8_t *ob = (uint8_t *)((uintptr_t)A.out & ~(uintptr_t)63);
+        const uint64_t ioff = (uint64_t)(p.in - ib);
+        const uint64_t soff = (uint64_t)(((uintptr_t)p.out & ~(uintptr_t)63) -
+                                         (uintptr_t)ob);
+        if (coop && __builtin_amdgcn_ballot_w64(ioff + 64 * se < (1ull << 32) &&
+                                                soff + 64 * se + 64 <
+                                                    (1ull << 32)) == ~0ull) {
+            const uint32_t lq = 16 * (threadIdx.x & 3);
+            const uint32_t i32 = (uint32_t)ioff, s32 = (uint32_t)soff;
+            const uint32_t r0 = (uint32_t)(((uintptr_t)p.out >> 4) & 3);
+            const uint32_t io[4] = { qperm<0x00>(i32) + lq, qperm<0x55>(i32) + lq,
+                                     qperm<0xAA>(i32) + lq, qperm<0xFF>(i32) + lq };
+            const uint32_t so[4] = { qperm<0x00>(s32) + lq, qperm<0x55>(s32) + lq,
+                                     qperm<0xAA>(s32) + lq, qperm<0xFF>(s32) + lq };
+#if ICM_LDSX
+            const uint32_t ibq[4] = { qperm<0x00>(i32), qperm<0x55>(i32),
+                                      qperm<0xAA>(i32), qperm<0xFF>(i32) };
+#define ICM_RUN(SS)                                                            \
+    icm_ldsx_run<SS, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T, ks_prev,     \
+                                             hst, prev, ib, ob, ibq, so, r0, xb)
+#else
+            (void)xb;
+#define ICM_RUN(SS)                                                            \
+    icm_seq_run<SS, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T, ks_prev, hst, \
+                                            prev, ib, ob, io, so, r0)
+#endif
+            switch (p.s) {
+            case 0:
+                ICM_RUN(0);
+                break;
+            case 1:
+                ICM_RUN(1);
+                break;
+            case 2:
+                ICM_RUN(2);
+                break;
+            default:
+                ICM_RUN(3);
+                break;
+            }
+#undef ICM_RUN
+        } else
+#endif
+        if (!ICM_SEQ && coop) {
             const uint64_t lq = 16 * (threadIdx.x & 3);
             const uint64_t pin = (uint64_t)(uintptr_t)p.in;
             const uint64_t seg0 = (uint64_t)(uintptr_t)p.out & ~63ull;
@@ -501,6 +747,10 @@ DEV void icm_packet(const IcmArgs &A, uint32_t i, const AesLds &T, KEY &rk)
             }
         }
     }
+#if ICM_SEQ
+    // re-derived rather than held in registers across the steady loop
+    p = make_pkt<NR, AUTH>(A, i, A.meta[i], key);
+#endif
     for (; b < p.nb; b++)
         icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, rk, T, ks_prev, hst, tailq,
                                            prev);
@@ -578,10 +828,15 @@ void k_icm_hmac(IcmArgs A)
     constexpr int NRK = NR ? NR : 1;
     constexpr int LDSB = NR ? (TAB4 ? AES_TAB4_BYTES : AES_TAB2_BYTES) : 16;
     __shared__ u32x4 s_tab[LDSB / 16];
+    // per-wave exchange buffers of the LDS cooperative path (4 KiB a wave);
+    // their first KiB also holds the S-box during the table build
+    constexpr int XB = (UNIFORM && NR && ICM_LDSX) ? ICM_THREADS_UNI / 64 * 256
+                                                   : 64;
+    __shared__ u32x4 s_x[XB];
     if (A.abort && *A.abort)
         return;
     if (NR)
-        load_aes_tables<TAB4>(s_tab);
+        load_aes_tables<TAB4>(s_tab, (uint32_t *)s_x);
     __syncthreads();
     const AesLds T = make_aes_lds(s_tab);
 
@@ -595,7 +850,8 @@ void k_icm_hmac(IcmArgs A)
     const uint32_t first = blockIdx.x * blockDim.x + (threadIdx.x & ~63u) +
                            16 * (L & 3) + (L >> 2);
     for (uint32_t i = first; i < A.n; i += stride)
-        icm_packet<NR, TAB4, AUTH, PROTECT, UNIFORM>(A, i, T, rk);
+        icm_packet<NR, TAB4, AUTH, PROTECT, UNIFORM>(
+            A, i, T, rk, s_x + (XB > 64 ? (threadIdx.x >> 6) * 256 : 0));
 }
 
 }   // namespace
@@ -620,6 +876,11 @@ int launch_icm_nr(const IcmArgs &A, bool auth, bool prot, int ncu,
             hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, false>), grid, block,   \
                                0, st, A);                                      \
     } while (0)
+#ifdef ICM_EXP_ONLY   // experiment builds: the bench kernel only
+    ICM_GO(true, true);
+    (void)auth;
+    (void)prot;
+#else
     if (auth && prot)
         ICM_GO(true, true);
     else if (auth)
@@ -628,6 +889,7 @@ int launch_icm_nr(const IcmArgs &A, bool auth, bool prot, int ncu,
         ICM_GO(false, true);
     else
         ICM_GO(false, false);
+#endif
 #undef ICM_GO
     HIPCHK(hipGetLastError());
     return 0;

@@ -47,6 +47,15 @@ print(json.dumps({"kernel_ms": tail[len(tail) // 2], "min": tail[0]}))
 
 
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--one":
+        # one build in this process (for rocprofv3 -- python3 ... --one NAME)
+        name, cfg = sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else "icm128"
+        so = os.path.join(ROOT, "libsrtp_amd", "libsrtp_mi355x.so") \
+            if name == "tree" else os.path.join(ROOT, "exp_build", name,
+                                                "libsrtp_mi355x.so")
+        os.environ["LIBSRTP_MI355X_LIB"] = so
+        exec(CHILD % (ROOT, so, cfg, 1 << 20), {"__name__": "child"})
+        return
     cfg = sys.argv[1] if len(sys.argv) > 1 else "icm128"
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
     names = sorted(os.listdir(os.path.join(ROOT, "exp_build"))) \
