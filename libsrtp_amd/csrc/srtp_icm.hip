@@ -36,6 +36,21 @@ namespace {
 #ifndef ICM_LDSX
 #define ICM_LDSX 0   // icm_seq_run: lane-quad exchange through LDS
 #endif
+// cooperative-path packet loads / segment stores: plain, or non-temporal
+// (streaming: each byte is touched once)
+#ifndef ICM_NT
+#define ICM_NT 0
+#endif
+#if ICM_NT & 1
+#define ICM_LD(P) __builtin_nontemporal_load(P)
+#else
+#define ICM_LD(P) (*(P))
+#endif
+#if ICM_NT & 2
+#define ICM_ST(V, P) __builtin_nontemporal_store((V), (P))
+#else
+#define ICM_ST(V, P) (*(P) = (V))
+#endif
 
 // per-packet constants of the chunk loop
 struct IcmPkt {
@@ -308,7 +323,7 @@ DEV void coop_step(uint32_t b, const IcmPkt &p, const CtrCache &C,
 #ifdef ICM_EXP_L2   // timing experiment only: re-read 2 chunks (cache hits)
             nx[j] = *(gcptr)(cp.in[j] + 64 * (1 + ((b + 1) & 1)));
 #else
-            nx[j] = *(gcptr)(cp.in[j] + 64 * (b + 1));
+            nx[j] = ICM_LD((gcptr)(cp.in[j] + 64 * (b + 1)));
 #endif
     }
     quad_transpose(v);
@@ -339,7 +354,7 @@ DEV void coop_step(uint32_t b, const IcmPkt &p, const CtrCache &C,
 #ifdef ICM_EXP_L2
         *(gptr)(cp.seg[j] + 64 * (1 + (b & 1))) = sg[j];
 #else
-        *(gptr)(cp.seg[j] + 64 * b) = sg[j];
+        ICM_ST(sg[j], (gptr)(cp.seg[j] + 64 * b));
 #endif
     if (NEXT)
         coop_keystream<NR, TAB4>(b + 1, p, C, rk, T, ks);
@@ -361,7 +376,7 @@ DEV void icm_coop_run(uint32_t &b, uint32_t e, const IcmPkt &p,
     u32x4 nx[4];
 #pragma unroll
     for (int j = 0; j < 4; j++)
-        nx[j] = *(gcptr)(cp.in[j] + 64 * b);
+        nx[j] = ICM_LD((gcptr)(cp.in[j] + 64 * b));
     uint32_t ks[4][4];
     coop_keystream<NR, TAB4>(b, p, C, rk, T, ks);
     for (; b + 1 < e; b++)
@@ -486,16 +501,21 @@ DEV void icm_ldsx_run(uint32_t &b, uint32_t e, const IcmPkt &p,
         rs[j] = 64 * q + 4 * m + ((j + m + q) & 3);          // own piece j
         ro[j] = 64 * j + 4 * m + ((q + m + (uint32_t)j) & 3);  // store read
     }
-    for (; b < e; b++) {
+    // chunk b's DMA is issued once chunk b-1 has left the buffer, before
+    // chunk b-1's SHA-1 and chunk b's AES: both cover its latency
+    auto dma = [&](uint32_t c) {
         // the previous chunk's store reads are complete before the DMA
         // overwrites the buffer
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int j = 0; j < 4; j++)
             __builtin_amdgcn_global_load_lds(
-                (const void __attribute__((address_space(1))) *)(ib + (io[j] + 64 * b)),
+                (const void __attribute__((address_space(1))) *)(ib + (io[j] + 64 * c)),
                 (void __attribute__((address_space(3))) *)(xb + 64 * j), 16, 0,
                 0);
+    };
+    dma(b);
+    for (; b < e; b++) {
         uint32_t ks[4][4];
         coop_keystream<NR, TAB4>(b, p, C, rk, T, ks);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -531,6 +551,8 @@ DEV void icm_ldsx_run(uint32_t &b, uint32_t e, const IcmPkt &p,
 #pragma unroll
         for (int j = 0; j < 4; j++)
             *(gptr)(ob + (so[j] + 64 * b)) = xb[ro[j]];
+        if (b + 1 < e)
+            dma(b + 1);
         if (AUTH) {
             if (PROTECT) {
 #pragma unroll
