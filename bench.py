@@ -166,19 +166,21 @@ def timed_steps(step, steps, warmup, world, sync=None):
     with seconds = the MAX over ranks (gloo all_reduce)."""
     import torch.distributed as dist
     sync = sync or (lambda: None)
+    # a process group of one rank (SRTP_FORCE_DIST=1) takes the same path
+    on = world > 1 or (dist.is_available() and dist.is_initialized())
     for _ in range(warmup):
         step()
     sync()
-    if world > 1:
+    if on:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     res = [step() for _ in range(steps)]
     sync()
-    if world > 1:
+    if on:
         dist.barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if on:
         import torch
         dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
@@ -256,7 +258,7 @@ def distribute_keys(keys_hex, world, dev):
     import torch.distributed as dist
     raw = b"".join(bytes.fromhex(k) for k in keys_hex)
     blob = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
-    if world > 1:
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         dist.broadcast(blob, src=0)
     raw = blob.cpu().numpy().tobytes()
     w = len(raw) // len(keys_hex)
@@ -276,7 +278,9 @@ def main():
         traffic = measure_traffic(a, kname)
     import torch
     import torch.distributed as dist
-    if world > 1:
+    # SRTP_FORCE_DIST=1: a one-rank process group, so the RCCL barrier,
+    # key broadcast and max-over-ranks reduction run on a one-GPU box too
+    if world > 1 or os.environ.get("SRTP_FORCE_DIST") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group(

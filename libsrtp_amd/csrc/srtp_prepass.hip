@@ -188,6 +188,11 @@ __device__ void agg_stream(uint32_t key, uint64_t e, uint32_t *bcount,
             atomicMax(&new_index[lead], (unsigned long long)v);
         }
         done = done || mine;
+        // a stream that only one lane of the wave holds: the packets of the
+        // wave are spread over many streams (64k-stream batches), so the
+        // rest go straight to their own atomics
+        if (__popcll((unsigned long long)mm) == 1)
+            break;
     }
     if (!done) {
         atomicAdd(&bcount[key], 1u);

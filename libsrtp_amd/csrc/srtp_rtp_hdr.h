@@ -33,8 +33,11 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
     } else if (len < 12) {
         err = 2;
     } else {
-        uint32_t w0 = srtp_bswap32(*(const uint32_t *)p);
-        h.ssrc = srtp_bswap32(*(const uint32_t *)(p + 8));
+        // one 16-byte load: the packet is 16-B aligned and readable to
+        // roundup16(len) >= 16
+        const uint4 q = *(const uint4 *)p;
+        uint32_t w0 = srtp_bswap32(q.x);
+        h.ssrc = srtp_bswap32(q.z);
         h.seq_len = w0 & 0xffffu;
         es = 12 + 4 * ((w0 >> 24) & 0xfu);
         if (len < es) {
