@@ -267,6 +267,11 @@ def distribute_keys(keys_hex, world, dev):
 
 def main():
     a = parse()
+    # stdout carries exactly the one JSON line: native libraries' banners
+    # (RCCL prints its version block at communicator init) go to stderr
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -419,7 +424,7 @@ def main():
         "prepass": {"device_batches": dev_b, "host_batches": host_b,
                     "last_abort": sess.prepass_last_abort()},
     }
-    print(json.dumps(out))
+    print(json.dumps(out), file=json_out, flush=True)
 
 
 if __name__ == "__main__":
