@@ -85,8 +85,41 @@ struct PpState {
     void *cub = nullptr;
     size_t cub_bytes = 0;
     uint32_t *abort = nullptr;      // device word
-    uint32_t *h_abort = nullptr;    // pinned
+    uint32_t *h_abort = nullptr;    // pinned, host-coherent: the final abort
+                                    // word, published by the commit kernel
+    uint32_t *h_abort_dev = nullptr;   // its device address
 };
+
+// the host reads the published abort word after the stream synchronises
+constexpr uint32_t ABORT_UNSET = 0xffffffffu;
+
+// one launch instead of a memset per array: the abort word and the
+// per-stream aggregates of a pre-pass round
+__global__ void k_pp_reset(uint32_t *abort, uint32_t *bcount,
+                           unsigned long long *new_index, uint32_t *bcount2,
+                           unsigned long long *new_index2, uint32_t ns)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s == 0)
+        *abort = 0;
+    if (s >= ns)
+        return;
+    bcount[s] = 0;
+    new_index[s] = 0;
+    if (bcount2) {
+        bcount2[s] = 0;
+        new_index2[s] = 0;
+    }
+}
+
+// the final abort word to host memory, from the last kernel that reads it
+__device__ __forceinline__ void publish_abort(uint32_t *pub,
+                                              const uint32_t *abort)
+{
+    if (pub && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_store(pub, *abort, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ uint32_t map_hash(uint32_t k, uint32_t mask)
 {
@@ -551,8 +584,10 @@ __global__ void k_pp_commit_of(const uint32_t *pstat, const uint32_t *olen,
 __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
                                    const uint64_t *new_index,
                                    const uint32_t *bcount, const uint32_t *wnew,
-                                   uint32_t *win, const uint32_t *abort)
+                                   uint32_t *win, const uint32_t *abort,
+                                   uint32_t *pub)
 {
+    publish_abort(pub, abort);
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns || *abort)
         return;
@@ -779,8 +814,9 @@ __global__ void k_pu_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
                                    const uint32_t *bcount,
                                    const uint32_t *bcount2,
                                    const uint32_t *wnew, uint32_t *win,
-                                   const uint32_t *abort)
+                                   const uint32_t *abort, uint32_t *pub)
 {
+    publish_abort(pub, abort);
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ns || *abort)
         return;
@@ -957,7 +993,10 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     }
     if (!P->abort) {
         PPCHK(hipMalloc((void **)&P->abort, 4));
-        PPCHK(hipHostMalloc((void **)&P->h_abort, 4, hipHostMallocDefault));
+        PPCHK(hipHostMalloc((void **)&P->h_abort, 4,
+                            hipHostMallocMapped | hipHostMallocCoherent));
+        PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
+                                      0));
     }
     P->ns = ns;
     P->nwords = nwords;
@@ -1019,9 +1058,10 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     }();
     bool unordered = ns > 1 && !force_sorted;
     for (;;) {
-    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
-    PPCHK(hipMemsetAsync(P->bcount, 0, ns * 4ull, stream));
-    PPCHK(hipMemsetAsync(P->new_index, 0, ns * 8ull, stream));
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    hipLaunchKernelGGL(k_pp_reset, dim3(ns / 256 + 1), blk, 0, stream, P->abort, P->bcount,
+                       (unsigned long long *)P->new_index, nullptr, nullptr,
+                       ns);
 
     ClassifyArgs C;
     C.in = b->in;
@@ -1125,7 +1165,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     if (pp_step(stream, "commit_pkt"))
         return -1;
     hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
-                       P->new_index, P->bcount, P->wnew, P->win, P->abort);
+                       P->new_index, P->bcount, P->wnew, P->win, P->abort,
+                       P->h_abort_dev);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "commit_stream"))
         return -1;
@@ -1146,9 +1187,10 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
     if (pp_step(stream, "crypto"))
         return -1;
-    PPCHK(hipMemcpyAsync(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost,
-                         stream));
+    // the commit kernel published the final abort word to host memory
     PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
     if (unordered && *P->h_abort == AB_ORDER) {
         unordered = false;   // nothing was committed: the sorted path
         continue;
@@ -1185,11 +1227,10 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     // more packets than the replay window); several: order-free first
     bool unordered = ns > 1 && !force_sorted;
     for (;;) {
-    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
-    PPCHK(hipMemsetAsync(P->bcount, 0, ns * 4ull, stream));
-    PPCHK(hipMemsetAsync(P->new_index, 0, ns * 8ull, stream));
-    PPCHK(hipMemsetAsync(P->bcount2, 0, ns * 4ull, stream));
-    PPCHK(hipMemsetAsync(P->new_index2, 0, ns * 8ull, stream));
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    hipLaunchKernelGGL(k_pp_reset, dim3(ns / 256 + 1), blk, 0, stream, P->abort, P->bcount,
+                       (unsigned long long *)P->new_index, P->bcount2,
+                       (unsigned long long *)P->new_index2, ns);
 
     ClassifyArgs C;
     C.in = b->in;
@@ -1297,7 +1338,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                        P->wnew);
     hipLaunchKernelGGL(k_pu_commit_stream, gs, blk, 0, stream, P->st, ns,
                        P->new_index2, P->bcount, P->bcount2, P->wnew, P->win,
-                       P->abort);
+                       P->abort, P->h_abort_dev);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "pu_commit"))
         return -1;
@@ -1305,9 +1346,10 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     // speculative decryption is undone
     if (srtp_gpu_undo(g, n, b->out, b->out_off, P->meta, stream))
         return -1;
-    PPCHK(hipMemcpyAsync(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost,
-                         stream));
+    // the commit kernel published the final abort word to host memory
     PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
     if (unordered && *P->h_abort == AB_ORDER) {
         unordered = false;   // nothing ran or changed: the chain form
         continue;
