@@ -64,13 +64,18 @@ __global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
                                               uint32_t n)
 {
     __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    srtp_dev_meta_t m = {};
+    if (i < n)
+        m = meta[i];
+    const bool todo = i < n && !SRTP_META_STATUS(m.info);
+    // most blocks have nothing to undo (every packet authenticated): they
+    // leave before building the tables
+    if (!__syncthreads_or(todo))
+        return;
     load_aes_tables<false>(s_tab);
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const srtp_dev_meta_t m = meta[i];
-    if (SRTP_META_STATUS(m.info))
+    if (!todo)
         return;
     const srtp_dev_key_t *key = keys + m.key;
     const AesLds T = make_aes_lds(s_tab);
@@ -321,13 +326,18 @@ __global__ __launch_bounds__(256) void k_rtcp(uint8_t *arena,
                                               int protect)
 {
     __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    srtp_dev_meta_t m = {};
+    if (i < n)
+        m = meta[i];
+    const bool todo = i < n && !SRTP_META_STATUS(m.info);
+    // most blocks have nothing to undo (every packet authenticated): they
+    // leave before building the tables
+    if (!__syncthreads_or(todo))
+        return;
     load_aes_tables<false>(s_tab);
     __syncthreads();
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const srtp_dev_meta_t m = meta[i];
-    if (SRTP_META_STATUS(m.info))
+    if (!todo)
         return;
     const srtp_dev_key_t *key = keys + m.key;
     const AesLds T = make_aes_lds(s_tab);
