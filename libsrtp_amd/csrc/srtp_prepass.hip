@@ -639,7 +639,8 @@ __global__ void k_pu_classify(ClassifyArgs A)
         const uint32_t len = A.in_len[i];
         const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
         A.hdr[i] = h;
-        A.perm[i] = i;
+        if (!A.est)   // the sorted chain form sorts it; order-free: identity
+            A.perm[i] = i;
         uint32_t code = 0;
         if (h.enc_start >> 24) {
             code = h.enc_start >> 24;   // header does not parse: no stream
@@ -693,7 +694,7 @@ __global__ void k_pu_meta(const uint32_t *skey, const uint32_t *perm,
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n)
         return;
-    const uint32_t i = perm[k];
+    const uint32_t i = perm ? perm[k] : k;   // null: the identity
     srtp_dev_meta_t m;
     m.key = 0;
     m.roc = 0;
@@ -770,7 +771,7 @@ __global__ void k_pu_accept(const uint32_t *skey, const uint32_t *perm,
     uint32_t key = NOCHAIN;
     uint64_t e = 0;
     if (live) {
-        const uint32_t i = perm[k];
+        const uint32_t i = perm ? perm[k] : k;   // null: the identity
         const uint32_t s = skey[k];
         if (s >= ns) {
             status[i] = (int32_t)pstat[i];   // header errors; out_len kept
@@ -799,7 +800,7 @@ __global__ void k_pu_setbits(const uint32_t *skey, const uint32_t *perm,
     if (k >= n || *abort)
         return;
     const uint32_t s = skey[k];
-    if (s >= ns || !auth[perm[k]])
+    if (s >= ns || !auth[perm ? perm[k] : k])
         return;
     const uint32_t bits = st[s].win_bits;
     const uint64_t dist = new_index2[s] - est[k];
@@ -1260,7 +1261,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         hipLaunchKernelGGL(k_pp_usetbits, gp, blk, 0, stream, P->skey, P->est,
                            P->st, ns, N, P->new_index, P->wnew, P->abort);
         ks = P->skey;
-        kp = P->perm;
+        kp = nullptr;   // the packet order itself
     } else {
         // chain form: stable stream order, advances, segmented sum
         size_t tb = P->cub_bytes;
