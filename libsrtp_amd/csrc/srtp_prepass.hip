@@ -938,7 +938,12 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipcub::DeviceScan::ExclusiveScanByKey(
         nullptr, c2, P->skey2, P->val, P->top, hipcub::Max(), (uint64_t)0,
         (int)c, hipcub::Equality(), stream));
+    size_t c3 = 0;
+    PPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, c3, P->val, P->est,
+                                           (int)c, stream));
     P->cub_bytes = a > b ? a : b;
+    if (c3 > P->cub_bytes)
+        P->cub_bytes = c3;
     if (c1 > P->cub_bytes)
         P->cub_bytes = c1;
     if (c2 > P->cub_bytes)
@@ -1030,6 +1035,21 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
                              hipMemcpyDeviceToHost, stream));
     PPCHK(hipStreamSynchronize(stream));
     return 0;
+}
+
+// 48-bit index of every sorted position: the segmented sum of the advances
+// by stream.  One stream: its chain packets come first and every other
+// position has advance 0 and is never read back, so a plain prefix sum is
+// the same and costs half the segmented one.
+static hipError_t index_scan(PpState *P, size_t &tb, uint32_t ns, uint32_t N,
+                             hipStream_t stream)
+{
+    if (ns == 1)
+        return hipcub::DeviceScan::InclusiveSum(P->cub, tb, P->val, P->est,
+                                                (int)N, stream);
+    return hipcub::DeviceScan::InclusiveScanByKey(
+        P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
+        hipcub::Equality(), stream);
 }
 
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
@@ -1128,9 +1148,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     if (pp_step(stream, "delta"))
         return -1;
     tb = P->cub_bytes;
-    PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
-        P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
-        hipcub::Equality(), stream));
+    PPCHK(index_scan(P, tb, ns, N, stream));
     if (pp_step(stream, "scan"))
         return -1;
     hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est, ns,
@@ -1284,9 +1302,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                            P->hdr, P->st, ns, N, P->val, P->seg_first,
                            P->abort);
         tb = P->cub_bytes;
-        PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
-            P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
-            hipcub::Equality(), stream));
+        PPCHK(index_scan(P, tb, ns, N, stream));
         // candidates per stream (AES-GCM key usage)
         hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est,
                            ns, N, P->seg_first, P->bcount, P->new_index);
