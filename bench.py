@@ -369,12 +369,16 @@ def main():
     out_len.fill_(slot)
     torch.cuda.synchronize()
     k_step = [0]
-    fn = sess.protect_device if a.op == "protect" else sess.unprotect_device
+    fn = sess.protect_prepared if a.op == "protect" else \
+        sess.unprotect_prepared
+    # one descriptor per batch, built before the timed region
+    descs = [sess.prepare_device(ar, off, in_len, ar, off, out_len, status,
+                                 stream=stream) for ar in arenas]
 
     def step():
-        ar = arenas[k_step[0]]
+        b = descs[k_step[0]]
         k_step[0] += 1
-        st = fn(ar, off, in_len, ar, off, out_len, status, stream=stream)
+        st = fn(b)
         if st != 0:
             raise RuntimeError("srtp_%s_device: %s" % (a.op, st))
         return sess.last_kernel_ms()

@@ -416,6 +416,30 @@ class Session:
     def protect_device(self, *a, **k):
         return self._device(self.L.srtp_protect_device, *a, **k)
 
+    # A batch descriptor built once and submitted many times (the arenas it
+    # points at keep their addresses): what a C caller does, without the
+    # per-call ctypes marshalling of nine tensor pointers.
+    @staticmethod
+    def prepare_device(arena_in, in_off, in_len, arena_out, out_off, out_len,
+                       status, stream=None):
+        b = DeviceBatch()
+        b.n = in_off.numel()
+        b.in_ = arena_in.data_ptr()
+        b.in_off = in_off.data_ptr()
+        b.in_len = in_len.data_ptr()
+        b.out = arena_out.data_ptr()
+        b.out_off = out_off.data_ptr()
+        b.out_len = out_len.data_ptr()
+        b.status = status.data_ptr()
+        b.stream = stream
+        return b
+
+    def protect_prepared(self, b):
+        return self.L.srtp_protect_device(self.h, C.byref(b))
+
+    def unprotect_prepared(self, b):
+        return self.L.srtp_unprotect_device(self.h, C.byref(b))
+
     def unprotect_device(self, *a, **k):
         return self._device(self.L.srtp_unprotect_device, *a, **k)
 
