@@ -90,6 +90,11 @@ def parse():
     ap.add_argument("--packets", type=int, default=0,
                     help="override packets per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="protect through srtp_protect_device_async: the "
+                    "next batch is submitted while the previous one's "
+                    "kernel runs (kernel_ms then comes from the warmup "
+                    "launches, which run synchronously with timing on)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
@@ -375,16 +380,30 @@ def main():
     descs = [sess.prepare_device(ar, off, in_len, ar, off, out_len, status,
                                  stream=stream) for ar in arenas]
 
+    pipelined = a.pipelined and a.op == "protect"
+    warm_ms = []
+
     def step():
         b = descs[k_step[0]]
         k_step[0] += 1
-        st = fn(b)
+        if pipelined and k_step[0] > a.warmup:
+            if k_step[0] == a.warmup + 1:
+                sess.set_timing(False)   # timing would synchronise
+            st = sess.protect_prepared_async(b)
+        else:
+            st = fn(b)
         if st != 0:
             raise RuntimeError("srtp_%s_device: %s" % (a.op, st))
-        return sess.last_kernel_ms()
+        if pipelined and k_step[0] <= a.warmup:
+            warm_ms.append(sess.last_kernel_ms())
+        return None if pipelined else sess.last_kernel_ms()
 
     dt, kms = timed_steps(step, a.steps, a.warmup, world,
                           sync=torch.cuda.synchronize)
+    if pipelined:
+        if not warm_ms:
+            raise SystemExit("--pipelined needs --warmup >= 1 (kernel timing)")
+        kms = warm_ms
     assert int((status != 0).sum()) == 0
     dev_b, host_b = sess.prepass_stats()
 
@@ -416,7 +435,9 @@ def main():
         "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": n,
                    "streams_per_gpu": nstreams,
                    "payload_bytes": payload, "rtp_bytes": rtp_len,
-                   "srtp_bytes": rtp_len + tag, "parallelism": "dp%d" % world},
+                   "srtp_bytes": rtp_len + tag, "parallelism": "dp%d" % world,
+                   "submission": "pipelined (srtp_protect_device_async)"
+                   if pipelined else "synchronous (srtp_%s_device)" % a.op},
         "payload_GBps": value * payload / 1e9,
         "roofline": {"bound": "hbm", "achieved": achieved,
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s",

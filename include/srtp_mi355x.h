@@ -360,6 +360,16 @@ typedef struct srtp_device_batch_t {
 } srtp_device_batch_t;
 
 srtp_err_status_t srtp_protect_device(srtp_t ctx, const srtp_device_batch_t *b);
+/* As srtp_protect_device, but for a batch the GPU pre-pass takes the call
+ * returns as soon as the pre-pass has committed it (stream state, status[]
+ * and out_len[] written on the device, the protect kernel queued on
+ * b->stream); the output bytes are complete when that stream gets past the
+ * call.  Consecutive batches on one stream then keep the GPU busy while the
+ * host submits the next one.  A batch the pre-pass declines runs to
+ * completion before the call returns, as with srtp_protect_device.  No
+ * counterpart for unprotect: its verdict needs the tags. */
+srtp_err_status_t srtp_protect_device_async(srtp_t ctx,
+                                            const srtp_device_batch_t *b);
 srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
                                         const srtp_device_batch_t *b);
 

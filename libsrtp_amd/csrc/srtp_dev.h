@@ -227,6 +227,8 @@ typedef struct srtp_gpu_pp_batch {
     uint32_t mask;
     int sorted;             /* out: the sorted chain path ran (not the
                                order-free form) */
+    int async;              /* protect: return once the pre-pass verdict is
+                               published, the crypto kernel still queued */
 } srtp_gpu_pp_batch_t;
 
 /* pre-pass + crypto for protect.  *fallback != 0: nothing was written (no

@@ -2008,7 +2008,8 @@ static int xrtp_protect_results(srtp_t ctx, size_t n, srtp_err_status_t *status,
 /* ------------------------------------------------------------------------
  * batch API over host buffers
  * ---------------------------------------------------------------------- */
-static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b);
+static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
+                               int async);
 static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b);
 
 /* a parallel for over [0, n) on up to 8 host threads: the gather into and
@@ -2130,7 +2131,7 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
     b.status = sg->d_st;
     b.stream = hs;
     int fast = unprotect ? unprotect_device_fast(ctx, &b)
-                         : protect_device_fast(ctx, &b);
+                         : protect_device_fast(ctx, &b, 0);
     if (fast <= 0)
         return fast;
     ctx->dt.fast_batches++;
@@ -2674,7 +2675,8 @@ static void dev_pull(srtp_t ctx)
 
 /* the device pre-pass; returns 1 when the batch was completed on the GPU,
  * 0 when the host path must run it, -1 on a device error */
-static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
+static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
+                               int async)
 {
     devtab_t *dt = &ctx->dt;
     if (!ctx->n || b->n > 0x7fffffffu) {
@@ -2702,6 +2704,7 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     pb.stream = b->stream;
     pb.uniform_key = dt->uniform;
     pb.mask = dt->mask;
+    pb.async = async;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))
@@ -2718,13 +2721,30 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     return 1;
 }
 
+static srtp_err_status_t protect_device(srtp_t ctx,
+                                        const srtp_device_batch_t *b,
+                                        int async);
+
 srtp_err_status_t srtp_protect_device(srtp_t ctx, const srtp_device_batch_t *b)
+{
+    return protect_device(ctx, b, 0);
+}
+
+srtp_err_status_t srtp_protect_device_async(srtp_t ctx,
+                                            const srtp_device_batch_t *b)
+{
+    return protect_device(ctx, b, 1);
+}
+
+static srtp_err_status_t protect_device(srtp_t ctx,
+                                        const srtp_device_batch_t *b,
+                                        int async)
 {
     if (!ctx || !b)
         return srtp_err_status_bad_param;
     if (!b->n)
         return srtp_err_status_ok;
-    int fast = protect_device_fast(ctx, b);
+    int fast = protect_device_fast(ctx, b, async);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         return srtp_err_status_fail;

@@ -1041,6 +1041,23 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
 // by stream.  One stream: its chain packets come first and every other
 // position has advance 0 and is never read back, so a plain prefix sum is
 // the same and costs half the segmented one.
+// Waits for the commit kernel's published abort word without waiting for
+// the kernels queued after it.  Returns the word, or ABORT_UNSET when the
+// stream drained without it (the caller then synchronises and reads the
+// device word).
+static uint32_t wait_published(PpState *P, hipStream_t stream)
+{
+    volatile uint32_t *w = (volatile uint32_t *)P->h_abort;
+    for (uint32_t k = 1;; k++) {
+        const uint32_t v = *w;
+        if (v != ABORT_UNSET)
+            return v;
+        if ((k & 1023) == 0 && hipStreamQuery(stream) == hipSuccess)
+            return *w;
+        __builtin_ia32_pause();
+    }
+}
+
 static hipError_t index_scan(PpState *P, size_t &tb, uint32_t ns, uint32_t N,
                              hipStream_t stream)
 {
@@ -1207,6 +1224,12 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     if (pp_step(stream, "crypto"))
         return -1;
     // the commit kernel published the final abort word to host memory
+    if (b->async && wait_published(P, stream) == 0) {
+        // committed: the crypto kernel is queued behind it on the stream
+        b->sorted = !unordered;
+        *fallback = 0;
+        return 0;
+    }
     PPCHK(hipStreamSynchronize(stream));
     if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
         PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));

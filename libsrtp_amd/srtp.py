@@ -135,6 +135,7 @@ def lib():
         "srtp_protect_rtcp_batch": ([P, S, P, P, P, P, P, P], C.c_int),
         "srtp_unprotect_rtcp_batch": ([P, S, P, P, P, P, P], C.c_int),
         "srtp_protect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
+        "srtp_protect_device_async": ([P, C.POINTER(DeviceBatch)], C.c_int),
         "srtp_unprotect_device": ([P, C.POINTER(DeviceBatch)], C.c_int),
         "srtp_get_protect_trailer_length": ([P, S, SP], C.c_int),
         "srtp_get_protect_rtcp_trailer_length": ([P, S, SP], C.c_int),
@@ -436,6 +437,11 @@ class Session:
 
     def protect_prepared(self, b):
         return self.L.srtp_protect_device(self.h, C.byref(b))
+
+    def protect_prepared_async(self, b):
+        """srtp_protect_device_async: returns once the GPU pre-pass has
+        committed the batch; the bytes are done when the stream is."""
+        return self.L.srtp_protect_device_async(self.h, C.byref(b))
 
     def unprotect_prepared(self, b):
         return self.L.srtp_unprotect_device(self.h, C.byref(b))
