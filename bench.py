@@ -401,9 +401,11 @@ def main():
     dt, kms = timed_steps(step, a.steps, a.warmup, world,
                           sync=torch.cuda.synchronize)
     if pipelined:
+        # the warmup launches, synchronous with timing on; the first one
+        # also pays the cold start, so it is left out when there are more
         if not warm_ms:
             raise SystemExit("--pipelined needs --warmup >= 1 (kernel timing)")
-        kms = warm_ms
+        kms = warm_ms[1:] or warm_ms
     assert int((status != 0).sum()) == 0
     dev_b, host_b = sess.prepass_stats()
 
