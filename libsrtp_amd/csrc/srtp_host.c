@@ -184,6 +184,9 @@ typedef struct {
     uint64_t fast_batches, host_batches;
     uint64_t sorted_batches; /* fast batches that needed the sorted path  */
     int last_abort;         /* reason of the most recent fallback         */
+    int async_pending;      /* srtp_protect_device_async left its protect
+                               kernel (and the tail of its commit) queued */
+    void *async_stream;     /* ... on this stream                          */
 } devtab_t;
 
 struct srtp_ctx_t_ {
@@ -215,6 +218,7 @@ struct srtp_ctx_t_ {
 };
 
 static void dev_pull(srtp_t ctx);
+static void async_drain(srtp_t ctx);
 
 /* the session's own stream: host-buffer batches run on it.  Device-API
  * batches run on the caller's stream, NULL meaning the HIP null stream
@@ -1229,6 +1233,7 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    async_drain(ctx);
     ctx->kq_n = 0; /* keys about to be freed need no derivation */
     for (size_t i = 0; i < ctx->n; i++)
         stream_free(ctx, ctx->list[i]);
@@ -2130,6 +2135,7 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
     b.out_len = sg->d_cap;
     b.status = sg->d_st;
     b.stream = hs;
+    async_drain(ctx);   /* staged on the library's own stream */
     int fast = unprotect ? unprotect_device_fast(ctx, &b)
                          : protect_device_fast(ctx, &b, 0);
     if (fast <= 0)
@@ -2550,6 +2556,7 @@ static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
  * ---------------------------------------------------------------------- */
 static int dev_build(srtp_t ctx)
 {
+    async_drain(ctx);
     devtab_t *dt = &ctx->dt;
     uint32_t ns = (uint32_t)ctx->n;
     size_t nwords = 0;
@@ -2645,9 +2652,22 @@ out:
 
 /* bring the device-advanced stream state back into the host streams and
  * drop the mirror (the caller is about to use or change host state) */
+/* work srtp_protect_device_async left queued is finished before anything
+ * reads or changes the device stream table, the keys or the staging arenas
+ * from another stream */
+static void async_drain(srtp_t ctx)
+{
+    if (!ctx->dt.async_pending)
+        return;
+    ctx->dt.async_pending = 0;
+    if (srtp_gpu_sync(ctx->gpu, ctx->dt.async_stream))
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+}
+
 static void dev_pull(srtp_t ctx)
 {
     devtab_t *dt = &ctx->dt;
+    async_drain(ctx);
     if (!dt->valid)
         return;
     dt->valid = 0;
@@ -2744,6 +2764,9 @@ static srtp_err_status_t protect_device(srtp_t ctx,
         return srtp_err_status_bad_param;
     if (!b->n)
         return srtp_err_status_ok;
+    /* the same stream orders a queued batch before this one */
+    if (ctx->dt.async_pending && ctx->dt.async_stream != b->stream)
+        async_drain(ctx);
     int fast = protect_device_fast(ctx, b, async);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
@@ -2751,6 +2774,8 @@ static srtp_err_status_t protect_device(srtp_t ctx,
     }
     if (fast) {
         ctx->dt.fast_batches++;
+        ctx->dt.async_pending = async;   /* else the stream was synchronised */
+        ctx->dt.async_stream = b->stream;
         return srtp_err_status_ok;
     }
     ctx->dt.host_batches++;
@@ -2841,6 +2866,7 @@ srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
         return srtp_err_status_bad_param;
     if (!b->n)
         return srtp_err_status_ok;
+    async_drain(ctx);
     int fast = unprotect_device_fast(ctx, b);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());

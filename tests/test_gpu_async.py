@@ -111,3 +111,46 @@ def test_async_single_stream_large_then_sync_call():
     for i, p in enumerate(tail):
         rc, ref = orc2.protect(p, len(p) + 16)
         assert st[i] == rc and (rc or out[i] == ref), i
+
+
+def test_async_then_host_calls_without_synchronize():
+    """host-buffer batches, get_roc and a synchronous call on another stream
+    right after queued async batches: the library finishes the queued work
+    before it touches the stream table from elsewhere"""
+    _gpu()
+    import torch
+    rng = random.Random(12)
+    pol = policy("icm128_hmac80", ssrc=0x5150)
+    lib, orc = L.Session([pol]), O.Session([pol])
+    stream = torch.cuda.current_stream().cuda_stream
+    seq, staged, batches = 0xff00, [], []
+    for _ in range(3):
+        pk = [rtp_packet(rng, 0x5150, (seq + j) & 0xffff, 1200)
+              for j in range(20000)]
+        seq += 20000
+        caps = [len(p) + 16 for p in pk]
+        t = _stage(pk, caps)
+        t["desc"] = lib.prepare_device(t["arena"], t["off"], t["ln"],
+                                       t["arena"], t["off"], t["cap"],
+                                       t["st"], stream=stream)
+        assert lib.protect_prepared_async(t["desc"]) == 0
+        staged.append(t)
+        batches.append((pk, caps))
+    # no synchronize: a host-buffer batch on the library's own stream
+    tail = [rtp_packet(rng, 0x5150, (seq + j) & 0xffff, 80)
+            for j in range(300)]
+    st_tail, out_tail = lib.protect_batch(tail, [len(p) + 16 for p in tail])
+    roc = lib.get_roc(0x5150)[1]
+    torch.cuda.synchronize()
+    for (pk, caps), t in zip(batches, staged):
+        st = t["st"].cpu().tolist()
+        host = t["arena"].cpu().numpy().tobytes()
+        for i, p in enumerate(pk):
+            rc, ref = orc.protect(p, caps[i])
+            assert rc == 0 and st[i] == 0, i
+            o = t["offs"][i]
+            assert host[o:o + len(ref)] == ref, i
+    for i, p in enumerate(tail):
+        rc, ref = orc.protect(p, len(p) + 16)
+        assert st_tail[i] == rc and (rc or out_tail[i] == ref), i
+    assert roc == orc.get_roc(0x5150)[1]
