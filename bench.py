@@ -22,7 +22,17 @@ Multi-GPU: one process per GPU (torch.distributed.run, nccl = RCCL), each
 rank protects its own 2^20-packet batch of its own stream (weak scaling).
 The master keys are rank 0's and reach the other ranks in one broadcast over
 xGMI (the session (re)key step); the data path has no collective.  value =
-all ranks' packets / max rank time.
+all ranks' packets / max rank time.  `--gpus N` with N > 1 and no
+WORLD_SIZE in the environment starts the N ranks itself (a
+torch.distributed.run child, before this process touches the GPU) and exits
+with its status; under a launcher WORLD_SIZE must equal N.
+BASELINE configs[4] (AES-256-GCM, 8M x 1400 B over 8 x MI355X, RCCL key
+broadcast) is `python bench.py --config gcm256 --gpus 8`: 2^20 packets per
+rank, 8 ranks.
+
+--dry-run: the same orchestration (rank launch, barrier-bracketed timing,
+max over ranks, the one JSON line) over gloo on the CPU with a stub step
+(rank r sleeps (r + 1) ms), for tests without a GPU.
 
 Extra fields: roofline (dominant kernel, HIP-event timed on the stream the
 kernels ran on), cpu_baseline (the reference, cisco/libsrtp built from its
@@ -63,6 +73,9 @@ TEST_KEY = ("e1f97a0d3e018be0d64fa32c06de41390ec675ad498afeebb6960b3aabe6"
             "c173c317f2dabe357793b6960b3aabe6")
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 STREAMS = {"icm128": 1, "gcm256": 1, "g711": 65536}
+# (config, multi-GPU) -> the BASELINE.json configs[] entry the line measures
+BASELINE_CONFIG = {("icm128", False): 1, ("gcm256", False): 2,
+                   ("g711", False): 3, ("gcm256", True): 4}
 
 
 def stream_keys(n, seed=0x5352545030303031):
@@ -82,7 +95,10 @@ def stream_keys(n, seed=0x5352545030303031):
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default: WORLD_SIZE or 1")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="gloo on the CPU with a stub step (no GPU)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="icm128", choices=sorted(CONFIGS))
@@ -270,16 +286,119 @@ def distribute_keys(keys_hex, world, dev):
     return [raw[i * w:(i + 1) * w].hex() for i in range(len(keys_hex))]
 
 
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(a, argv):
+    """--gpus N > 1 without a launcher: run torch.distributed.run as a
+    CHILD process (this process has not touched the GPU and never execs),
+    one rank per GPU on this node; rank 0's JSON line reaches our stdout
+    through the inherited descriptor.  Returns the child's exit status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node=%d" % a.gpus, "--master-addr=127.0.0.1",
+           "--master-port=%d" % _free_port(), os.path.abspath(__file__)]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd + list(argv), env=env)
+
+
+def resolve_world(a):
+    """(world, rank, local rank); --gpus must agree with a launcher's
+    WORLD_SIZE"""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus is None:
+        a.gpus = world
+    if a.gpus != world:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d" % (a.gpus, world))
+    return (world, int(os.environ.get("RANK", "0")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def dry_run(a, world, rank, json_out):
+    """the multi-rank orchestration without a GPU: gloo process group, a
+    stub step that takes (rank + 1) ms, the same timing and JSON line"""
+    import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+    pol, payload, npk, tag = CONFIGS[a.config]
+    n = a.packets or npk
+
+    def step():
+        time.sleep(1e-3 * (rank + 1))
+        return 0.0
+
+    dt, _ = timed_steps(step, a.steps, a.warmup, world)
+    if rank == 0:
+        rec = result_line(a, world, n, payload, tag, dt, None, None, None)
+        rec["dry_run"] = True
+        print(json.dumps(rec), file=json_out, flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def result_line(a, world, n, payload, tag, dt, roofline, cpu, prepass):
+    rtp_len = 12 + payload
+    value = n * a.steps * world / dt
+    return {
+        "metric": "SRTP packets/sec + payload GB/s, device-resident, "
+                  "1M×1400B batch",
+        "op": a.op,
+        "value": value,
+        "unit": "pkt/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (random payloads, seq advanced per step)",
+        "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": n,
+                   "packets_total": n * world,
+                   "streams_per_gpu": STREAMS[a.config],
+                   "payload_bytes": payload, "rtp_bytes": rtp_len,
+                   "srtp_bytes": rtp_len + tag, "parallelism": "dp%d" % world,
+                   "baseline_config": BASELINE_CONFIG.get(
+                       (a.config, world > 1), None),
+                   "submission": "pipelined (srtp_protect_device_async)"
+                   if a.pipelined and a.op == "protect"
+                   else "synchronous (srtp_%s_device)" % a.op},
+        "payload_GBps": value * payload / 1e9,
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "prepass": prepass,
+    }
+
+
 def main():
     a = parse()
+    if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
+        sys.exit(launch_ranks(a, sys.argv[1:]))
+    world, rank, local = resolve_world(a)
     # stdout carries exactly the one JSON line: native libraries' banners
     # (RCCL prints its version block at communicator init) go to stderr
     sys.stdout.flush()
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.dry_run:
+        dry_run(a, world, rank, json_out)
+        return
+    try:
+        run_gpu(a, world, rank, local, json_out)
+    finally:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def run_gpu(a, world, rank, local, json_out):
     pol, payload, npk, tag = CONFIGS[a.config]
     kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
     # PMC passes first: child processes, before this one touches the GPU
@@ -353,6 +472,11 @@ def main():
     in_len = torch.full((n,), rtp_len, dtype=torch.int32, device=dev)
     out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
+    # one status array per batch, preset to a value no status takes, so the
+    # check after the timed region sees every step's verdicts (a batch that
+    # never ran keeps the preset)
+    statuses = [torch.full((n,), -1, dtype=torch.int32, device=dev)
+                for _ in range(nb)]
     stream = torch.cuda.current_stream().cuda_stream
     if a.op == "unprotect":
         # the sender's side, untimed: protect every batch in place; the
@@ -377,8 +501,9 @@ def main():
     fn = sess.protect_prepared if a.op == "protect" else \
         sess.unprotect_prepared
     # one descriptor per batch, built before the timed region
-    descs = [sess.prepare_device(ar, off, in_len, ar, off, out_len, status,
-                                 stream=stream) for ar in arenas]
+    descs = [sess.prepare_device(ar, off, in_len, ar, off, out_len, st,
+                                 stream=stream)
+             for ar, st in zip(arenas, statuses)]
 
     pipelined = a.pipelined and a.op == "protect"
     warm_ms = []
@@ -398,6 +523,7 @@ def main():
             warm_ms.append(sess.last_kernel_ms())
         return None if pipelined else sess.last_kernel_ms()
 
+    dev_b0, host_b0 = sess.prepass_stats()
     dt, kms = timed_steps(step, a.steps, a.warmup, world,
                           sync=torch.cuda.synchronize)
     if pipelined:
@@ -406,11 +532,11 @@ def main():
         if not warm_ms:
             raise SystemExit("--pipelined needs --warmup >= 1 (kernel timing)")
         kms = warm_ms[1:] or warm_ms
-    assert int((status != 0).sum()) == 0
+    bad = sum(int((st != 0).sum()) for st in statuses)
     dev_b, host_b = sess.prepass_stats()
-
-    total_pk = n * a.steps * world
-    value = total_pk / dt
+    if bad or host_b != host_b0:
+        raise SystemExit("bench: %d packets with a nonzero status, %d batches "
+                         "on the host path" % (bad, host_b - host_b0))
     kernel_ms = sum(kms) / len(kms)
     algo_bytes = n * (rtp_len + rtp_len + tag)   # rtp + srtp, read + write
     achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
@@ -419,38 +545,16 @@ def main():
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
-    out = {
-        "metric": "SRTP packets/sec + payload GB/s, device-resident, "
-                  "1M×1400B batch",
-        "op": a.op,
-        "value": value,
-        "unit": "pkt/s",
-        "n_gpus": world,
-        "steps": a.steps,
-        "warmup": a.warmup,
-        "ms_per_step": dt / a.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (random payloads, seq advanced per step)",
-        "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": n,
-                   "streams_per_gpu": nstreams,
-                   "payload_bytes": payload, "rtp_bytes": rtp_len,
-                   "srtp_bytes": rtp_len + tag, "parallelism": "dp%d" % world,
-                   "submission": "pipelined (srtp_protect_device_async)"
-                   if pipelined else "synchronous (srtp_%s_device)" % a.op},
-        "payload_GBps": value * payload / 1e9,
-        "roofline": {"bound": "hbm", "achieved": achieved,
-                     "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBPS,
-                     "traffic": traffic,
-                     "kernel": kname, "kernel_ms": kernel_ms,
-                     "algorithmic_bytes_per_launch": algo_bytes},
-        "cpu_baseline": cpu,
-        "prepass": {"device_batches": dev_b, "host_batches": host_b,
-                    "last_abort": sess.prepass_last_abort()},
-    }
+    roofline = {"bound": "hbm", "achieved": achieved,
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "kernel": kname, "kernel_ms": kernel_ms,
+                "algorithmic_bytes_per_launch": algo_bytes}
+    prepass = {"device_batches": dev_b - dev_b0,
+               "host_batches": host_b - host_b0,
+               "last_abort": sess.prepass_last_abort()}
+    out = result_line(a, world, n, payload, tag, dt, roofline, cpu, prepass)
     print(json.dumps(out), file=json_out, flush=True)
 
 

@@ -404,6 +404,14 @@ int srtp_mi355x_gpu_available(void);
 srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
                                                   uint64_t num_left);
 
+/* test hook: make the next `count` waits for the device pre-pass verdict
+ * (srtp_protect_device_async) or drains of a queued async batch report a
+ * GPU failure, as a stream in an error state would.  A failed drain leaves
+ * the session refusing packet calls (srtp_err_status_fail). */
+#define SRTP_MI355X_FAIL_VERDICT_WAIT 1
+#define SRTP_MI355X_FAIL_ASYNC_DRAIN 2
+void srtp_mi355x_debug_inject_failure(int what, int count);
+
 /* ========================================================================
  * The crypto-kernel plugin ABI (srtp.def:46-69): libsrtp's cipher / auth
  * vtables (crypto/include/cipher.h:60-260, auth.h:55-200), the type

@@ -187,6 +187,8 @@ typedef struct {
     int async_pending;      /* srtp_protect_device_async left its protect
                                kernel (and the tail of its commit) queued */
     void *async_stream;     /* ... on this stream                          */
+    int async_err;          /* a queued batch failed on the GPU: sticky,
+                               every later packet call returns _fail      */
 } devtab_t;
 
 struct srtp_ctx_t_ {
@@ -218,7 +220,22 @@ struct srtp_ctx_t_ {
 };
 
 static void dev_pull(srtp_t ctx);
-static void async_drain(srtp_t ctx);
+static int async_drain(srtp_t ctx);
+
+/* after a queued (async) batch failed on the GPU the device stream state is
+ * unknown: no packet call may run on the session any more */
+#define ASYNC_POISON_CHECK(ctx)                                                \
+    do {                                                                       \
+        if ((ctx) && (ctx)->dt.async_err)                                      \
+            return srtp_err_status_fail;                                       \
+    } while (0)
+/* the same, after the queued batch (if any) has finished: for calls that
+ * read or change the stream state from the host */
+#define ASYNC_DRAIN_CHECK(ctx)                                                 \
+    do {                                                                       \
+        if ((ctx) && async_drain(ctx))                                         \
+            return srtp_err_status_fail;                                       \
+    } while (0)
 
 /* the session's own stream: host-buffer batches run on it.  Device-API
  * batches run on the caller's stream, NULL meaning the HIP null stream
@@ -1233,7 +1250,7 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
 {
     if (!ctx)
         return srtp_err_status_bad_param;
-    async_drain(ctx);
+    (void)async_drain(ctx);   /* an error is logged; freeing goes on */
     ctx->kq_n = 0; /* keys about to be freed need no derivation */
     for (size_t i = 0; i < ctx->n; i++)
         stream_free(ctx, ctx->list[i]);
@@ -1316,15 +1333,31 @@ static srtp_err_status_t update_template(srtp_t ctx, const srtp_policy_t *p)
     /* streams cloned from the old template are re-cloned, keeping their
      * extended sequence number; other streams are kept as they are */
     keyset_t *old = ctx->templ->keys;
+    /* every clone is made before any stream is replaced: an allocation
+     * failure leaves the session exactly as it was */
+    srtp_stream_ctx_t **nc =
+        (srtp_stream_ctx_t **)calloc(ctx->n ? ctx->n : 1, sizeof *nc);
+    if (!nc) {
+        stream_free(ctx, nt);
+        return srtp_err_status_alloc_fail;
+    }
     for (size_t i = 0; i < ctx->n; i++) {
         srtp_stream_ctx_t *s = ctx->list[i];
         if (s->keys != old)
             continue;
-        srtp_stream_ctx_t *c = stream_clone(nt, s->ssrc);
-        if (!c) {
+        nc[i] = stream_clone(nt, s->ssrc);
+        if (!nc[i]) {
+            for (size_t k = 0; k < i; k++)
+                stream_free(ctx, nc[k]);
+            free(nc);
             stream_free(ctx, nt);
             return srtp_err_status_alloc_fail;
         }
+    }
+    for (size_t i = 0; i < ctx->n; i++) {
+        srtp_stream_ctx_t *s = ctx->list[i], *c = nc[i];
+        if (!c)
+            continue;
         /* srtp.c:3459-3483: extended sequence number and SRTCP replay
          * database carried over */
         c->rdbx.index = s->rdbx.index;
@@ -1334,6 +1367,7 @@ static srtp_err_status_t update_template(srtp_t ctx, const srtp_policy_t *p)
         ctx->list[i] = c;
         stream_free(ctx, s);
     }
+    free(nc);
     stream_free(ctx, ctx->templ);
     ctx->templ = nt; /* direction stays unknown, as srtp_stream_init leaves it */
     map_rebuild(ctx, ctx->map.cap ? ctx->map.cap : 64);
@@ -2135,7 +2169,8 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
     b.out_len = sg->d_cap;
     b.status = sg->d_st;
     b.stream = hs;
-    async_drain(ctx);   /* staged on the library's own stream */
+    if (async_drain(ctx))   /* staged on the library's own stream */
+        return -1;
     int fast = unprotect ? unprotect_device_fast(ctx, &b)
                          : protect_device_fast(ctx, &b, 0);
     if (fast <= 0)
@@ -2161,6 +2196,7 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    ASYNC_DRAIN_CHECK(ctx);
     if (!n)
         return srtp_err_status_ok;
     if (!mki_index || !memchr_nonzero(mki_index, n)) {
@@ -2400,6 +2436,7 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    ASYNC_DRAIN_CHECK(ctx);
     if (!n)
         return srtp_err_status_ok;
     int fast = batch_device_fast(ctx, 1, n, srtp, srtp_len, rtp, rtp_len,
@@ -2556,7 +2593,8 @@ static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
  * ---------------------------------------------------------------------- */
 static int dev_build(srtp_t ctx)
 {
-    async_drain(ctx);
+    if (async_drain(ctx))
+        return -1;
     devtab_t *dt = &ctx->dt;
     uint32_t ns = (uint32_t)ctx->n;
     size_t nwords = 0;
@@ -2655,19 +2693,40 @@ out:
 /* work srtp_protect_device_async left queued is finished before anything
  * reads or changes the device stream table, the keys or the staging arenas
  * from another stream */
-static void async_drain(srtp_t ctx)
+static int g_fail_drains;   /* test hook: srtp_mi355x_debug_inject_failure */
+
+/* returns -1 (and poisons the session) when the queued batch failed */
+static int async_drain(srtp_t ctx)
 {
+    if (ctx->dt.async_err)
+        return -1;
     if (!ctx->dt.async_pending)
-        return;
+        return 0;
     ctx->dt.async_pending = 0;
-    if (srtp_gpu_sync(ctx->gpu, ctx->dt.async_stream))
-        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+    int bad = srtp_gpu_sync(ctx->gpu, ctx->dt.async_stream) != 0;
+    if (g_fail_drains > 0) {
+        g_fail_drains--;
+        bad = 1;
+    }
+    if (bad) {
+        ctx->dt.async_err = 1;
+        log_msg(srtp_log_level_error,
+                "a queued srtp_protect_device_async batch failed on the GPU; "
+                "the session refuses further packets");
+        return -1;
+    }
+    return 0;
 }
 
 static void dev_pull(srtp_t ctx)
 {
     devtab_t *dt = &ctx->dt;
-    async_drain(ctx);
+    if (async_drain(ctx)) {
+        /* never take stream state from a table a failed batch left */
+        dt->valid = 0;
+        dt->dirty = 0;
+        return;
+    }
     if (!dt->valid)
         return;
     dt->valid = 0;
@@ -2762,11 +2821,13 @@ static srtp_err_status_t protect_device(srtp_t ctx,
 {
     if (!ctx || !b)
         return srtp_err_status_bad_param;
+    ASYNC_POISON_CHECK(ctx);
     if (!b->n)
         return srtp_err_status_ok;
     /* the same stream orders a queued batch before this one */
-    if (ctx->dt.async_pending && ctx->dt.async_stream != b->stream)
-        async_drain(ctx);
+    if (ctx->dt.async_pending && ctx->dt.async_stream != b->stream &&
+        async_drain(ctx))
+        return srtp_err_status_fail;
     int fast = protect_device_fast(ctx, b, async);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
@@ -2864,9 +2925,11 @@ srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
 {
     if (!ctx || !b)
         return srtp_err_status_bad_param;
+    ASYNC_POISON_CHECK(ctx);
     if (!b->n)
         return srtp_err_status_ok;
-    async_drain(ctx);
+    if (async_drain(ctx))
+        return srtp_err_status_fail;
     int fast = unprotect_device_fast(ctx, b);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
@@ -3100,6 +3163,7 @@ srtp_err_status_t srtp_protect_rtcp_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    ASYNC_DRAIN_CHECK(ctx);
     dev_pull(ctx);
     if (!n)
         return srtp_err_status_ok;
@@ -3254,6 +3318,7 @@ srtp_err_status_t srtp_unprotect_rtcp_batch(srtp_t ctx, size_t n,
 {
     if (!ctx)
         return srtp_err_status_bad_param;
+    ASYNC_DRAIN_CHECK(ctx);
     dev_pull(ctx);
     if (!n)
         return srtp_err_status_ok;
@@ -3583,6 +3648,7 @@ srtp_err_status_t srtp_get_protect_rtcp_trailer_length(srtp_t session,
 srtp_err_status_t srtp_stream_set_roc(srtp_t session, uint32_t ssrc,
                                       uint32_t roc)
 {
+    ASYNC_DRAIN_CHECK(session);
     if (session)
         dev_pull(session);
     srtp_stream_ctx_t *s = session ? map_get(session, ssrc) : NULL;
@@ -3595,6 +3661,7 @@ srtp_err_status_t srtp_stream_set_roc(srtp_t session, uint32_t ssrc,
 srtp_err_status_t srtp_stream_get_roc(srtp_t session, uint32_t ssrc,
                                       uint32_t *roc)
 {
+    ASYNC_DRAIN_CHECK(session);
     if (session)
         dev_pull(session);
     srtp_stream_ctx_t *s = session ? map_get(session, ssrc) : NULL;
@@ -3631,6 +3698,16 @@ void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
  * `ssrc` (host order) -- what a test of the reference writes into the
  * stream's srtp_key_limit_ctx_t to reach the soft / hard limits (key.c:74-90)
  * without 2^48 packets. */
+void srtp_gpu_pp_debug_fail_waits(int n);
+
+void srtp_mi355x_debug_inject_failure(int what, int count)
+{
+    if (what == SRTP_MI355X_FAIL_VERDICT_WAIT)
+        srtp_gpu_pp_debug_fail_waits(count);
+    else if (what == SRTP_MI355X_FAIL_ASYNC_DRAIN)
+        g_fail_drains = count;
+}
+
 srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
                                                   uint64_t num_left)
 {

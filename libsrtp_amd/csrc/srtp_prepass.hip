@@ -47,6 +47,8 @@
 #include "srtp_dev.h"
 #include "srtp_rtp_hdr.h"
 
+int srtp_gpu_fail(hipError_t e, const char *what);   // srtp_gpu.hip
+
 namespace {
 
 constexpr uint32_t SEQ_MEDIAN = 32768;
@@ -834,13 +836,12 @@ __global__ void k_pu_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
         win[off + w] = wnew[off + w];
 }
 
-static thread_local char pp_err[256];
-
+// recorded where srtp_gpu_last_error() reports it (the host logs it)
 int pp_fail(hipError_t e, const char *what)
 {
-    snprintf(pp_err, sizeof pp_err, "%s: %s", what, hipGetErrorString(e));
-    fprintf(stderr, "srtp_mi355x: %s\n", pp_err);
-    return -1;
+    char m[160];
+    snprintf(m, sizeof m, "device pre-pass: %s", what);
+    return srtp_gpu_fail(e, m);
 }
 
 #define PPCHK(x)                                                               \
@@ -1045,15 +1046,36 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
 // the kernels queued after it.  Returns the word, or ABORT_UNSET when the
 // stream drained without it (the caller then synchronises and reads the
 // device word).
-static uint32_t wait_published(PpState *P, hipStream_t stream)
+// A stream in an error state never publishes the word and never drains:
+// any hipStreamQuery result but hipErrorNotReady ends the wait, with the
+// error in *err (srtp_mi355x_debug_fail_async_wait injects one for tests).
+static int g_fail_waits;
+
+extern "C" void srtp_gpu_pp_debug_fail_waits(int n) { g_fail_waits = n; }
+
+static uint32_t wait_published(PpState *P, hipStream_t stream, hipError_t *err)
 {
     volatile uint32_t *w = (volatile uint32_t *)P->h_abort;
+    *err = hipSuccess;
+    if (g_fail_waits > 0) {
+        g_fail_waits--;
+        (void)hipStreamSynchronize(stream);   // leave nothing running
+        *err = hipErrorLaunchFailure;
+        return ABORT_UNSET;
+    }
     for (uint32_t k = 1;; k++) {
         const uint32_t v = *w;
         if (v != ABORT_UNSET)
             return v;
-        if ((k & 1023) == 0 && hipStreamQuery(stream) == hipSuccess)
-            return *w;
+        if ((k & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(stream);
+            if (q == hipSuccess)
+                return *w;
+            if (q != hipErrorNotReady) {
+                *err = q;
+                return ABORT_UNSET;
+            }
+        }
         __builtin_ia32_pause();
     }
 }
@@ -1224,11 +1246,17 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     if (pp_step(stream, "crypto"))
         return -1;
     // the commit kernel published the final abort word to host memory
-    if (b->async && wait_published(P, stream) == 0) {
-        // committed: the crypto kernel is queued behind it on the stream
-        b->sorted = !unordered;
-        *fallback = 0;
-        return 0;
+    if (b->async) {
+        hipError_t we;
+        const uint32_t v = wait_published(P, stream, &we);
+        if (we != hipSuccess)
+            return pp_fail(we, "waiting for the pre-pass verdict");
+        if (v == 0) {
+            // committed: the crypto kernel is queued behind it on the stream
+            b->sorted = !unordered;
+            *fallback = 0;
+            return 0;
+        }
     }
     PPCHK(hipStreamSynchronize(stream));
     if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)

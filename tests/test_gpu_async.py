@@ -154,3 +154,44 @@ def test_async_then_host_calls_without_synchronize():
         rc, ref = orc.protect(p, len(p) + 16)
         assert st_tail[i] == rc and (rc or out_tail[i] == ref), i
     assert roc == orc.get_roc(0x5150)[1]
+
+
+def test_async_failure_is_reported_not_spun_on():
+    """a stream in an error state must end the wait for the
+    pre-pass verdict with srtp_err_status_fail (not spin), and a queued
+    batch whose drain fails must poison the session: every later packet
+    call returns srtp_err_status_fail, no stream state is taken from the
+    device table it left (srtp_mi355x_debug_inject_failure)."""
+    import torch
+    _gpu()
+    rng = random.Random(5)
+    ssrcs = [0x5100]
+    pols = [policy("icm128_hmac80", ssrc=s) for s in ssrcs]
+    lib = L.Session(pols)
+    fail = lib.L.srtp_mi355x_debug_inject_failure
+    stream = torch.cuda.current_stream().cuda_stream
+    pk, nxt = _chains(rng, ssrcs, 300, [10], big=0)
+    t = _stage(pk, [len(p) + 32 for p in pk])
+    d = lib.prepare_device(t["arena"], t["off"], t["ln"], t["arena"],
+                           t["off"], t["cap"], t["st"], stream=stream)
+    fail(1, 1)                                # verdict wait sees an error
+    assert lib.protect_prepared_async(d) == 1    # srtp_err_status_fail
+    fail(1, 0)
+    # a good async batch, then its drain fails
+    pk, _ = _chains(rng, ssrcs, 300, [nxt[ssrcs[0]] + 1000], big=0)
+    t = _stage(pk, [len(p) + 32 for p in pk])
+    d = lib.prepare_device(t["arena"], t["off"], t["ln"], t["arena"],
+                           t["off"], t["cap"], t["st"], stream=stream)
+    assert lib.protect_prepared_async(d) == 0
+    fail(2, 1)
+    with pytest.raises(RuntimeError, match="fail"):
+        lib.protect_batch([rtp_packet(rng, 0x5100, 5, 100)])
+    fail(2, 0)
+    # sticky: the session refuses packets and stream-state queries
+    with pytest.raises(RuntimeError, match="fail"):
+        lib.protect_batch([rtp_packet(rng, 0x5100, 6, 100)])
+    st, _ = lib.get_roc(0x5100)
+    assert int(st) == 1              # srtp_err_status_fail
+    assert lib.protect_prepared_async(d) == 1
+    torch.cuda.synchronize()
+    lib.close()

@@ -80,3 +80,45 @@ def test_key_broadcast_world2():
     want = bench.stream_keys(3, seed=100)
     assert out[0] == out[1] == want
     assert all(len(bytes.fromhex(k)) == 46 for k in want)
+
+
+def _bench(args, env=None):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    e = dict(os.environ)
+    e.pop("WORLD_SIZE", None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py")] +
+                          args, capture_output=True, text=True, env=e,
+                          timeout=180)
+
+
+def test_bench_gpus2_launches_two_ranks():
+    """`bench.py --gpus 2` (the driver's N>1 form, here without a launcher)
+    starts two ranks itself; rank 0 prints the one JSON line, whose time is
+    the slower rank's (the stub step takes (rank + 1) ms)"""
+    import json
+    r = _bench(["--gpus", "2", "--dry-run", "--steps", "5", "--warmup", "2"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["dry_run"] is True
+    assert rec["config"]["parallelism"] == "dp2"
+    assert rec["config"]["packets_total"] == 2 * rec["config"]["packets_per_gpu"]
+    assert rec["ms_per_step"] >= 2.0            # max over ranks: rank 1's 2 ms
+    assert rec["value"] == pytest.approx(
+        2 * rec["config"]["packets_per_gpu"] * 5 / (rec["ms_per_step"] * 5e-3))
+
+
+def test_bench_gpus1_and_world_mismatch():
+    import json
+    r = _bench(["--dry-run", "--steps", "2", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    rec = json.loads(r.stdout)
+    assert rec["n_gpus"] == 1 and rec["config"]["parallelism"] == "dp1"
+    assert rec["config"]["baseline_config"] == 1
+    # under a launcher, --gpus must equal WORLD_SIZE
+    r = _bench(["--dry-run", "--gpus", "2"], env={"WORLD_SIZE": "1"})
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
