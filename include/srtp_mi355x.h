@@ -408,6 +408,12 @@ srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
  * (srtp_protect_device_async) or drains of a queued async batch report a
  * GPU failure, as a stream in an error state would.  A failed drain leaves
  * the session refusing packet calls (srtp_err_status_fail). */
+/* Device pre-pass tuning (process-wide): batches with many keys are laid
+ * out in key buckets so that a wave's 64 packets share one key, instead of
+ * one key per lane.  Off by default (no gain measured on
+ * BASELINE configs[3]); SRTP_PP_BUCKETS=1 in the environment also sets it. */
+void srtp_mi355x_set_key_buckets(int on);
+
 #define SRTP_MI355X_FAIL_VERDICT_WAIT 1
 #define SRTP_MI355X_FAIL_ASYNC_DRAIN 2
 void srtp_mi355x_debug_inject_failure(int what, int count);

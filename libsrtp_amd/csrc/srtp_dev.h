@@ -61,6 +61,14 @@ typedef struct srtp_dev_meta {
     uint32_t len;   /* bytes authenticated / encrypted region end            */
 } srtp_dev_meta_t;
 
+/* one packet of a key-bucketed crypto pass (device pre-pass, batches with
+ * many keys): its descriptor and offsets, stored at its bucket position so
+ * the crypto kernel reads them contiguously */
+typedef struct srtp_dev_rec {
+    uint64_t in_off, out_off;
+    srtp_dev_meta_t meta;
+} srtp_dev_rec_t;
+
 #define SRTP_META_ENC_START(i) ((i) & 0xffffu)
 #define SRTP_META_STATUS(i) (((i) >> 16) & 0xffu)
 #define SRTP_META_VARIANT(i) (((i) >> 24) & 0xffu)
@@ -148,6 +156,15 @@ typedef struct srtp_gpu_batch {
     void *stream;           /* hipStream_t or NULL for the context stream */
     const uint32_t *abort;  /* device word; non-zero -> kernels do nothing
                                (device pre-pass fell back), or NULL     */
+    /* key buckets (or NULL): the AES-ICM kernels walk rec[] instead of the
+     * packet order.  rec_range (device) = {0, a, a, a + b}: [0, a) holds
+     * one stream per aligned group of 64 records (one key per wave),
+     * [a, a + b) the streams with few packets (keys differ per lane);
+     * records with a nonzero status are gaps.  rec_idx[pos] = the packet
+     * index of rec[pos] (unprotect's auth_ok[]). */
+    const srtp_dev_rec_t *rec;
+    const uint32_t *rec_idx;
+    const uint32_t *rec_range;
 } srtp_gpu_batch_t;
 
 int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b);

@@ -1191,7 +1191,20 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
-    return launch_icm_nr<NR>(A, AUTH, PROT, g->ncu, st);
+    A.rec = b->rec;
+    A.rec_idx = b->rec_idx;
+    A.range = b->rec_range;
+    if (A.rec) {
+        // key buckets: the wave-aligned groups with a key per wave, then
+        // the streams with few packets with a key per lane
+        IcmArgs Ln = A;
+        Ln.range = A.range + 2;
+        return launch_icm_km<NR, KM_WAVE>(A, AUTH, PROT, g->ncu, st) |
+               launch_icm_km<NR, KM_LANE>(Ln, AUTH, PROT, g->ncu, st);
+    }
+    if (A.uni != 0xffffffffu)
+        return launch_icm_km<NR, KM_UNI>(A, AUTH, PROT, g->ncu, st);
+    return launch_icm_km<NR, KM_LANE>(A, AUTH, PROT, g->ncu, st);
 }
 
 template <int NR, bool PROT>

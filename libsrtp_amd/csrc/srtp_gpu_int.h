@@ -51,6 +51,11 @@ struct IcmArgs {
     const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;            // uniform key slot, ~0 if keys differ
+    // key buckets (srtp_gpu_batch_t rec / rec_idx / rec_range), or null:
+    // this launch walks rec[range[0] .. range[1])
+    const srtp_dev_rec_t *rec;
+    const uint32_t *rec_idx;
+    const uint32_t *range;
 };
 
 // AES-GCM kernel arguments
@@ -84,9 +89,18 @@ int srtp_gpu_fail(hipError_t e, const char *what);
             return srtp_gpu_fail(e_, #x);                                      \
     } while (0)
 
-// k_icm_hmac launchers (srtp_icm.hip, one object per NR in {0,10,12,14})
-template <int NR>
-int launch_icm_nr(const IcmArgs &A, bool auth, bool prot, int ncu,
+// where a k_icm_hmac launch takes each packet's key from
+enum IcmKeyMode {
+    KM_UNI = 0,    // one key for the whole batch (A.uni): SGPR schedule
+    KM_LANE = 1,   // per lane (meta.key): VGPR schedule
+    KM_WAVE = 2    // per aligned 64-record group of a key bucket: SGPR
+                   // schedule, reloaded for every group
+};
+
+// k_icm_hmac launchers (srtp_icm.hip, one object per NR in {0,10,12,14}
+// and key mode)
+template <int NR, int KM>
+int launch_icm_km(const IcmArgs &A, bool auth, bool prot, int ncu,
                   hipStream_t st);
 
 // k_gcm_wave launcher (srtp_gcm_wave.hip): 1 when it launched (A.rest /

@@ -3699,6 +3699,9 @@ void srtp_mi355x_unprotect_stats(srtp_t ctx, uint32_t *rounds,
  * stream's srtp_key_limit_ctx_t to reach the soft / hard limits (key.c:74-90)
  * without 2^48 packets. */
 void srtp_gpu_pp_debug_fail_waits(int n);
+void srtp_gpu_pp_set_buckets(int on);
+
+void srtp_mi355x_set_key_buckets(int on) { srtp_gpu_pp_set_buckets(on); }
 
 void srtp_mi355x_debug_inject_failure(int what, int count)
 {

@@ -39,13 +39,13 @@
 // has more than SOFT_LIMIT uses left after the batch.
 
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 
 #include "srtp_dev.h"
 #include "srtp_rtp_hdr.h"
+#include "srtp_scan.h"
 
 int srtp_gpu_fail(hipError_t e, const char *what);   // srtp_gpu.hip
 
@@ -84,12 +84,19 @@ struct PpState {
     uint64_t *top = nullptr;        // unprotect chain: highest accepted before
     uint32_t *bcount2 = nullptr;    // unprotect: authenticated per stream
     uint64_t *new_index2 = nullptr; // unprotect: highest authenticated
-    void *cub = nullptr;
-    size_t cub_bytes = 0;
+    // scratch of the scans and the radix sort (srtp_scan.h)
+    srtp_scan::Agg *agg = nullptr;
+    uint32_t *hist = nullptr;
     uint32_t *abort = nullptr;      // device word
     uint32_t *h_abort = nullptr;    // pinned, host-coherent: the final abort
                                     // word, published by the commit kernel
     uint32_t *h_abort_dev = nullptr;   // its device address
+    // key buckets (many-key order-free batches): per-stream record offset
+    // and cursor, the records and their packet indices, the region bounds
+    uint32_t *bk_off = nullptr, *bk_cur = nullptr;
+    srtp_dev_rec_t *rec = nullptr;
+    uint32_t *rec_idx = nullptr;
+    uint32_t *bk_range = nullptr;
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -392,11 +399,23 @@ __device__ uint32_t classify_one(const ClassifyArgs &A, uint32_t i,
 // by stream id is a stable partition into the chain packets (key 0) and the
 // rest (NOCHAIN), placed by an exclusive scan of the chain flags -- a scan
 // and a scatter instead of a full radix sort.
-struct IsChain {
-    __host__ __device__ __forceinline__ uint32_t operator()(const uint32_t &k) const
-    {
-        return k == 0u ? 1u : 0u;
-    }
+// scan traits (srtp_scan.h): the chain flags of one stream -> positions
+struct ChainFlags {
+    const uint32_t *skey;
+    uint32_t *out;
+    __device__ uint32_t key(uint32_t) const { return 0; }
+    __device__ uint64_t val(uint32_t i) const { return skey[i] == 0u; }
+    __device__ void store(uint32_t i, uint64_t v) const { out[i] = (uint32_t)v; }
+};
+
+// 64-bit values, segmented by keys (null: one segment)
+struct Seg64 {
+    const uint32_t *keys;
+    const uint64_t *in;
+    uint64_t *out;
+    __device__ uint32_t key(uint32_t i) const { return keys ? keys[i] : 0u; }
+    __device__ uint64_t val(uint32_t i) const { return in[i]; }
+    __device__ void store(uint32_t i, uint64_t v) const { out[i] = v; }
 };
 
 __global__ void k_pp_partition1(const uint32_t *skey, const uint32_t *excl,
@@ -836,6 +855,138 @@ __global__ void k_pu_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
         win[off + w] = wnew[off + w];
 }
 
+// ---------------------------------------------------------------------------
+// Key buckets: a batch of many streams with distinct keys
+// is laid out for the crypto kernel as one bucket of records per stream, so
+// that a wave's 64 packets share one key (SGPR round keys, the four-table
+// LDS layout) instead of gathering a key per lane.  A counting sort of the
+// packets by stream, not of their bytes: a 32-byte record (offsets and
+// descriptor) per packet.  Streams with at least BK_MIN packets get buckets
+// padded to a multiple of 64 records, in region A = [0, a); the others are
+// packed into region B = [a, a + b), where keys differ per lane.  Padding and
+// unused slots are records with a nonzero status.  Order inside a bucket is
+// irrelevant: on the order-free form every packet's index is already fixed.
+constexpr uint32_t BK_MIN = 32;
+
+__device__ __forceinline__ uint64_t bk_size(uint32_t c)
+{
+    return c >= BK_MIN ? (uint64_t)((c + 63) & ~63u) << 32 : (uint64_t)c;
+}
+
+// one workgroup: per-stream record offsets (exclusive scans of the bucket
+// sizes of both regions, packed in one 64-bit word), cursors reset, the
+// region bounds {0, a, a, a + b}
+__global__ __launch_bounds__(1024) void k_bk_offsets(const uint32_t *bcount,
+                                                     uint32_t ns, uint32_t *off,
+                                                     uint32_t *cur,
+                                                     uint32_t *range)
+{
+    __shared__ uint64_t s_part[1024];
+    const uint32_t t = threadIdx.x, T = blockDim.x;
+    const uint32_t per = (ns + T - 1) / T;
+    const uint32_t s0 = t * per < ns ? t * per : ns;
+    const uint32_t s1 = s0 + per < ns ? s0 + per : ns;
+    uint64_t sum = 0;   // (region A records << 32) | region B records
+    for (uint32_t s = s0; s < s1; s++)
+        sum += bk_size(bcount[s]);
+    s_part[t] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < T; d <<= 1) {
+        const uint64_t v = t >= d ? s_part[t - d] : 0;
+        __syncthreads();
+        s_part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = s_part[t] - sum;   // exclusive
+    const uint64_t tot = s_part[T - 1];
+    const uint32_t atot = (uint32_t)(tot >> 32), btot = (uint32_t)tot;
+    for (uint32_t s = s0; s < s1; s++) {
+        const uint32_t c = bcount[s];
+        off[s] = c >= BK_MIN ? (uint32_t)(run >> 32) : atot + (uint32_t)run;
+        cur[s] = 0;
+        run += bk_size(c);
+    }
+    if (t == 0) {
+        range[0] = 0;
+        range[1] = atot;
+        range[2] = atot;
+        range[3] = atot + btot;
+    }
+}
+
+// a slot in stream s's bucket: one atomic per stream present in the wave
+// (up to four), the rest (a wave spread over many streams) one per lane
+__device__ __forceinline__ uint32_t bk_claim(uint32_t s, uint32_t *cur)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    bool done = s == NOCHAIN;
+    uint32_t pos = 0;
+    for (int it = 0; it < 4; it++) {
+        const uint64_t am = __ballot(!done);
+        if (!am)
+            return pos;
+        const int ll = __ffsll((unsigned long long)am) - 1;
+        const uint32_t lead = (uint32_t)__shfl((int)s, ll);
+        const bool mine = !done && s == lead;
+        const uint64_t mm = __ballot(mine);
+        uint32_t base = 0;
+        if ((int)lane == ll)
+            base = atomicAdd(&cur[lead], (uint32_t)__popcll((unsigned long long)mm));
+        base = (uint32_t)__shfl((int)base, ll);
+        if (mine) {
+            pos = base + (uint32_t)__popcll((unsigned long long)(mm & ((1ull << lane) - 1)));
+            done = true;
+        }
+        if (__popcll((unsigned long long)mm) == 1)
+            break;
+    }
+    if (!done)
+        pos = atomicAdd(&cur[s], 1u);
+    return pos;
+}
+
+// every crypto packet (a stream, status 0) to its bucket
+__global__ void k_bk_scatter(const uint32_t *skey, const uint32_t *pstat,
+                             const srtp_dev_meta_t *meta,
+                             const uint64_t *in_off, const uint64_t *out_off,
+                             uint32_t n, uint32_t ns, const uint32_t *off,
+                             uint32_t *cur, srtp_dev_rec_t *rec,
+                             uint32_t *rec_idx)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t s = NOCHAIN;
+    if (i < n) {
+        s = skey[i];
+        if (s >= ns || pstat[i])
+            s = NOCHAIN;
+    }
+    const uint32_t pos = bk_claim(s, cur);
+    if (s == NOCHAIN)
+        return;
+    const uint32_t at = off[s] + pos;
+    srtp_dev_rec_t r;
+    r.in_off = in_off[i];
+    r.out_off = out_off[i];
+    r.meta = meta[i];
+    rec[at] = r;
+    rec_idx[at] = i;
+}
+
+// the unused slots of every bucket (wave padding, packets that left the
+// chain with an error) become gaps
+__global__ void k_bk_pad(const uint32_t *bcount, uint32_t ns,
+                         const uint32_t *off, const uint32_t *cur,
+                         srtp_dev_rec_t *rec)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns)
+        return;
+    const uint32_t c = bcount[s];
+    const uint32_t end = c >= BK_MIN ? (c + 63) & ~63u : c;
+    for (uint32_t p = cur[s]; p < end; p++)
+        rec[off[s] + p].meta.info = 0xff0000u;
+}
+
 // recorded where srtp_gpu_last_error() reports it (the host logs it)
 int pp_fail(hipError_t e, const char *what)
 {
@@ -906,8 +1057,8 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     while (c < n)
         c *= 2;
     void *old[] = { P->hdr, P->pstat, P->skey, P->skey2, P->perm,
-                    P->perm2, P->val, P->est, P->meta, P->cub, P->auth,
-                    P->top };
+                    P->perm2, P->val, P->est, P->meta, P->agg, P->hist,
+                    P->auth, P->top, P->rec, P->rec_idx };
     for (void *o : old)
         if (o)
             PPCHK(hipFree(o));
@@ -922,34 +1073,15 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipMalloc((void **)&P->meta, c * sizeof(srtp_dev_meta_t)));
     PPCHK(hipMalloc((void **)&P->auth, c));
     PPCHK(hipMalloc((void **)&P->top, c * 8));
-    // temp storage for the largest sort and scan of c items
-    size_t a = 0, b = 0;
-    PPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, a, P->skey, P->skey2,
-                                             P->perm, P->perm2, (int)c, 0, 32,
-                                             stream));
-    PPCHK(hipcub::DeviceScan::InclusiveScanByKey(
-        nullptr, b, P->skey2, P->val, P->est, hipcub::Sum(), (int)c,
-        hipcub::Equality(), stream));
-    size_t c1 = 0;
-    hipcub::TransformInputIterator<uint32_t, IsChain, const uint32_t *> it(
-        P->skey, IsChain());
-    PPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, c1, it, P->perm, (int)c,
-                                           stream));
-    size_t c2 = 0;
-    PPCHK(hipcub::DeviceScan::ExclusiveScanByKey(
-        nullptr, c2, P->skey2, P->val, P->top, hipcub::Max(), (uint64_t)0,
-        (int)c, hipcub::Equality(), stream));
-    size_t c3 = 0;
-    PPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, c3, P->val, P->est,
-                                           (int)c, stream));
-    P->cub_bytes = a > b ? a : b;
-    if (c3 > P->cub_bytes)
-        P->cub_bytes = c3;
-    if (c1 > P->cub_bytes)
-        P->cub_bytes = c1;
-    if (c2 > P->cub_bytes)
-        P->cub_bytes = c2;
-    PPCHK(hipMalloc(&P->cub, P->cub_bytes));
+    // buckets: region A <= 2 x its packets (>= BK_MIN per stream, padded
+    // to 64), region B <= its packets
+    PPCHK(hipMalloc((void **)&P->rec, 2 * c * sizeof(srtp_dev_rec_t)));
+    PPCHK(hipMalloc((void **)&P->rec_idx, 2 * c * 4));
+    // scan / sort scratch: digit histograms of 256 bins per tile, one scan
+    // aggregate per tile of the largest scan (the histograms)
+    const size_t nt = (c + srtp_scan::TILE - 1) / srtp_scan::TILE;
+    PPCHK(hipMalloc((void **)&P->hist, 256 * nt * 4));
+    PPCHK(hipMalloc((void **)&P->agg, (nt + 2) * sizeof(srtp_scan::Agg)));
     P->n_cap = c;
     return 0;
 }
@@ -966,8 +1098,9 @@ void srtp_gpu_pp_free(void *p)
     void *bufs[] = { P->st, P->win, P->wnew, P->hkey, P->hval, P->bcount,
                      P->seg_first, P->bcount2, P->new_index2,
                      P->new_index, P->hdr, P->pstat, P->skey, P->skey2,
-                     P->perm, P->perm2, P->val, P->est, P->meta, P->cub,
-                     P->auth, P->top, P->abort };
+                     P->perm, P->perm2, P->val, P->est, P->meta, P->agg,
+                     P->hist, P->auth, P->top, P->abort, P->bk_off, P->bk_cur,
+                     P->rec, P->rec_idx, P->bk_range };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -984,12 +1117,14 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     PpState *P = pp_of(g);
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
     uint32_t c1 = P->ns_cap, c2 = P->ns_cap, c5 = P->ns_cap,
-             c6 = P->ns_cap, c7 = P->ns_cap, c3 = P->nwords_cap;
+             c6 = P->ns_cap, c7 = P->ns_cap, c8 = P->ns_cap, c9 = P->ns_cap,
+             c3 = P->nwords_cap;
     if (regrow(&P->st, &P->ns_cap, ns + 1) ||
         regrow(&P->bcount, &c1, ns + 1) || regrow(&P->new_index, &c2, ns + 1) ||
         regrow(&P->seg_first, &c5, ns + 1) ||
         regrow(&P->bcount2, &c6, ns + 1) ||
         regrow(&P->new_index2, &c7, ns + 1) ||
+        regrow(&P->bk_off, &c8, ns + 1) || regrow(&P->bk_cur, &c9, ns + 1) ||
         regrow(&P->win, &P->nwords_cap, nwords + 1) ||
         regrow(&P->wnew, &c3, nwords + 1))
         return -1;
@@ -1000,6 +1135,7 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     }
     if (!P->abort) {
         PPCHK(hipMalloc((void **)&P->abort, 4));
+        PPCHK(hipMalloc((void **)&P->bk_range, 16));
         PPCHK(hipHostMalloc((void **)&P->h_abort, 4,
                             hipHostMallocMapped | hipHostMallocCoherent));
         PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
@@ -1080,15 +1216,74 @@ static uint32_t wait_published(PpState *P, hipStream_t stream, hipError_t *err)
     }
 }
 
-static hipError_t index_scan(PpState *P, size_t &tb, uint32_t ns, uint32_t N,
+// the key buckets of an order-free batch with more than one key; the crypto
+// batch then walks them (srtp_gpu_batch_t rec / rec_idx / rec_range)
+static int bucket_pass(PpState *P, uint32_t N, const srtp_gpu_pp_batch_t *b,
+                       srtp_gpu_batch_t *cb, hipStream_t stream)
+{
+    const uint32_t ns = P->ns;
+    const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
+    hipLaunchKernelGGL(k_bk_offsets, dim3(1), dim3(1024), 0, stream,
+                       P->bcount, ns, P->bk_off, P->bk_cur, P->bk_range);
+    hipLaunchKernelGGL(k_bk_scatter, gp, blk, 0, stream, P->skey, P->pstat,
+                       P->meta, b->in_off, b->out_off, N, ns, P->bk_off,
+                       P->bk_cur, P->rec, P->rec_idx);
+    hipLaunchKernelGGL(k_bk_pad, gs, blk, 0, stream, P->bcount, ns,
+                       P->bk_off, P->bk_cur, P->rec);
+    PPCHK(hipGetLastError());
+    cb->rec = P->rec;
+    cb->rec_idx = P->rec_idx;
+    cb->rec_range = P->bk_range;
+    return pp_step(stream, "buckets");
+}
+
+// Many-key batches through the key buckets: srtp_mi355x_set_key_buckets()
+// or SRTP_PP_BUCKETS=1.  Off by default: measured on configs[3] (64k streams
+// x 128 packets, round-robin) the bucketed kernel (one key per wave) took
+// 2.51 ms against 2.53 ms with a key per lane, and the bucket pass 0.39 ms
+// on top.
+static int g_buckets = -1;
+
+extern "C" void srtp_gpu_pp_set_buckets(int on) { g_buckets = on ? 1 : 0; }
+
+static bool buckets_on()
+{
+    if (g_buckets < 0) {
+        const char *e = getenv("SRTP_PP_BUCKETS");
+        g_buckets = e && *e == '1';
+    }
+    return g_buckets == 1;
+}
+
+static hipError_t index_scan(PpState *P, uint32_t ns, uint32_t N,
                              hipStream_t stream)
 {
-    if (ns == 1)
-        return hipcub::DeviceScan::InclusiveSum(P->cub, tb, P->val, P->est,
-                                                (int)N, stream);
-    return hipcub::DeviceScan::InclusiveScanByKey(
-        P->cub, tb, P->skey2, P->val, P->est, hipcub::Sum(), (int)N,
-        hipcub::Equality(), stream);
+    return srtp_scan::scan_run<srtp_scan::OP_SUM, false>(
+        Seg64{ ns == 1 ? nullptr : P->skey2, P->val, P->est }, N, P->agg,
+        stream);
+}
+
+// the stable order by stream: one stream, a partition of the chain packets
+// (a scan and a scatter); several, a radix sort over the stream-id bits
+static hipError_t stream_order(PpState *P, uint32_t ns, uint32_t N,
+                               hipStream_t stream)
+{
+    if (ns == 1) {
+        // perm (the sort's identity values) is free: it takes the scan
+        hipError_t e = srtp_scan::scan_run<srtp_scan::OP_SUM, true>(
+            ChainFlags{ P->skey, P->perm }, N, P->agg, stream);
+        if (e != hipSuccess)
+            return e;
+        hipLaunchKernelGGL(k_pp_partition1, dim3((N + 255) / 256), dim3(256),
+                           0, stream, P->skey, P->perm, N, P->skey2, P->perm2);
+        return hipGetLastError();
+    }
+    // NOCHAIN keys truncate to all-ones > any stream id
+    int end_bit = 1;
+    while ((1u << end_bit) <= ns && end_bit < 32)
+        end_bit++;
+    return srtp_scan::radix_sort(P->skey, P->perm, P->skey2, P->perm2, N,
+                                 end_bit, P->hist, P->agg, stream);
 }
 
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
@@ -1160,25 +1355,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         K.skey2 = P->skey;   // packet order: perm is the identity
         K.perm2 = P->perm;
     } else {
-    // stable sort by stream id; NOCHAIN keys truncate to all-ones > any sid
-    int end_bit = 1;
-    while ((1u << end_bit) <= ns && end_bit < 32)
-        end_bit++;
-    size_t tb = P->cub_bytes;
-    if (ns == 1) {
-        // perm (the sort's identity values) is free: it takes the scan
-        hipcub::TransformInputIterator<uint32_t, IsChain, const uint32_t *> it(
-            P->skey, IsChain());
-        PPCHK(hipcub::DeviceScan::ExclusiveSum(P->cub, tb, it, P->perm, (int)N,
-                                               stream));
-        hipLaunchKernelGGL(k_pp_partition1, gp, blk, 0, stream, P->skey,
-                           P->perm, N, P->skey2, P->perm2);
-        PPCHK(hipGetLastError());
-    } else {
-        PPCHK(hipcub::DeviceRadixSort::SortPairs(P->cub, tb, P->skey, P->skey2,
-                                                 P->perm, P->perm2, (int)N, 0,
-                                                 end_bit, stream));
-    }
+    PPCHK(stream_order(P, ns, N, stream));
     if (pp_step(stream, "sort"))
         return -1;
     hipLaunchKernelGGL(k_pp_delta, gp, blk, 0, stream, P->skey2, P->perm2,
@@ -1186,8 +1363,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     PPCHK(hipGetLastError());
     if (pp_step(stream, "delta"))
         return -1;
-    tb = P->cub_bytes;
-    PPCHK(index_scan(P, tb, ns, N, stream));
+    PPCHK(index_scan(P, ns, N, stream));
     if (pp_step(stream, "scan"))
         return -1;
     hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est, ns,
@@ -1230,6 +1406,9 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
 
     srtp_gpu_batch_t cb = {};
+    if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&
+        bucket_pass(P, N, b, &cb, stream))
+        return -1;
     cb.n = n;
     cb.in = b->in;
     cb.in_off = b->in_off;
@@ -1333,27 +1512,11 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         kp = nullptr;   // the packet order itself
     } else {
         // chain form: stable stream order, advances, segmented sum
-        size_t tb = P->cub_bytes;
-        if (ns == 1) {
-            hipcub::TransformInputIterator<uint32_t, IsChain, const uint32_t *>
-                it(P->skey, IsChain());
-            PPCHK(hipcub::DeviceScan::ExclusiveSum(P->cub, tb, it, P->perm,
-                                                   (int)N, stream));
-            hipLaunchKernelGGL(k_pp_partition1, gp, blk, 0, stream, P->skey,
-                               P->perm, N, P->skey2, P->perm2);
-        } else {
-            int end_bit = 1;
-            while ((1u << end_bit) <= ns && end_bit < 32)
-                end_bit++;
-            PPCHK(hipcub::DeviceRadixSort::SortPairs(
-                P->cub, tb, P->skey, P->skey2, P->perm, P->perm2, (int)N, 0,
-                end_bit, stream));
-        }
+        PPCHK(stream_order(P, ns, N, stream));
         hipLaunchKernelGGL(k_pp_delta, gp, blk, 0, stream, P->skey2, P->perm2,
                            P->hdr, P->st, ns, N, P->val, P->seg_first,
                            P->abort);
-        tb = P->cub_bytes;
-        PPCHK(index_scan(P, tb, ns, N, stream));
+        PPCHK(index_scan(P, ns, N, stream));
         // candidates per stream (AES-GCM key usage)
         hipLaunchKernelGGL(k_pp_seg_end, gp, blk, 0, stream, P->skey2, P->est,
                            ns, N, P->seg_first, P->bcount, P->new_index);
@@ -1367,6 +1530,9 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
 
     srtp_gpu_batch_t cb = {};
+    if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&
+        bucket_pass(P, N, b, &cb, stream))
+        return -1;
     cb.n = n;
     cb.in = b->in;
     cb.in_off = b->in_off;
@@ -1384,12 +1550,10 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
 
     if (!unordered) {
-        size_t tb = P->cub_bytes;
         hipLaunchKernelGGL(k_pu_accepted_est, gp, blk, 0, stream, P->skey2,
                            P->perm2, P->est, P->auth, ns, N, P->val);
-        PPCHK(hipcub::DeviceScan::ExclusiveScanByKey(
-            P->cub, tb, P->skey2, P->val, P->top, hipcub::Max(), (uint64_t)0,
-            (int)N, hipcub::Equality(), stream));
+        PPCHK((srtp_scan::scan_run<srtp_scan::OP_MAX, true>(
+            Seg64{ P->skey2, P->val, P->top }, N, P->agg, stream)));
         hipLaunchKernelGGL(k_pu_top_check, gp, blk, 0, stream, P->skey2,
                            P->perm2, P->hdr, P->est, P->top, P->st, ns, N,
                            P->abort);

@@ -152,6 +152,7 @@ def lib():
         "srtp_mi355x_debug_set_key_limit": ([P, C.c_uint32, C.c_uint64],
                                             C.c_int),
         "srtp_mi355x_debug_inject_failure": ([C.c_int, C.c_int], None),
+        "srtp_mi355x_set_key_buckets": ([C.c_int], None),
         "srtp_mi355x_unprotect_stats": ([P] + [C.POINTER(C.c_uint32)] * 3,
                                         None),
 

@@ -153,6 +153,24 @@ class Session:
                                mki_index)
         return rc, (out.raw[:n.value] if rc == 0 else None)
 
+    def protect_many(self, arena, offs, lens, out_cap):
+        """orc_protect_many over packets at arena[offs[i]:+lens[i]] (numpy
+        uint8 / uint64 / uint32 arrays), in order, into a new arena of the
+        arena with out_cap bytes per packet; returns (failures, outputs as
+        an (n, out_cap) array, out lengths)"""
+        import numpy as np
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        ooff = np.arange(len(lens), dtype=np.uint64) * np.uint64(out_cap)
+        out = np.zeros(len(lens) * out_cap, dtype=np.uint8)
+        olen = np.zeros(len(lens), dtype=np.uint32)
+        bad = lib().orc_protect_many(
+            self.h, len(lens), arena.ctypes.data, offs.ctypes.data,
+            lens.ctypes.data, out.ctypes.data, ooff.ctypes.data,
+            olen.ctypes.data, out_cap)
+        return bad, out.reshape(len(lens), out_cap), olen
+
     def unprotect(self, srtp, cap):
         out = C.create_string_buffer(max(cap, len(srtp)) + 64)
         n = C.c_size_t(cap)

@@ -323,6 +323,7 @@ def test_device_api_vs_oracle(name):
     ("icm128_hmac80", 65536, 10),
     ("icm128_hmac80", 1 << 20, 10),   # configs[1] at its own size
     ("gcm256_16", 65536, 16),         # configs[2]'s cipher, uniform key
+    ("gcm256_16", 1 << 20, 16),       # configs[2] at its own size
 ])
 def test_large_uniform_batch_roundtrip(name, n, trailer):
     """n x 1400 B through the device API (the bench shape): protect ->

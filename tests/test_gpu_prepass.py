@@ -340,3 +340,87 @@ def test_configs3_shape_64k_distinct_key_streams():
         seq0 += per
     assert lib.prepass_stats() == (2, 0), lib.prepass_last_abort()
     assert lib.prepass_sorted_batches() == 0
+
+
+def _rr_arena(ns, per, payload, seq0, base_ssrc, gen, slot):
+    """configs[3]-shaped arena on the GPU: ns streams round-robin, per
+    packets each (packet i: stream i % ns, its packet i // ns)"""
+    import torch
+    n = ns * per
+    a = torch.randint(0, 256, (n, slot), dtype=torch.uint8, device="cuda",
+                      generator=gen)
+    idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    a[:, 0] = 0x80
+    a[:, 1] = 96
+    seq = (idx // ns + seq0) & 0xffff
+    a[:, 2] = (seq >> 8).to(torch.uint8)
+    a[:, 3] = (seq & 0xff).to(torch.uint8)
+    a[:, 4:8] = 0
+    ssrc = base_ssrc + idx % ns
+    for k in range(4):
+        a[:, 8 + k] = ((ssrc >> (24 - 8 * k)) & 0xff).to(torch.uint8)
+    return a
+
+
+@pytest.mark.parametrize("buckets", [0, 1])
+def test_configs3_bench_shape_128_per_stream(buckets):
+    """BASELINE configs[3] at the bench's own shape: 65,536 streams with
+    distinct master keys x 128 packets x 160 B (8M packets, round-robin), so
+    every stream's batch spans hi - est = 127 against its 128-bit window --
+    the order-free form's acceptance boundary -- and the crypto runs from
+    the key buckets (one key per wave).  Two consecutive batches.  Every
+    packet of 1,024 sampled streams (131,072 per batch) is compared byte
+    for byte with the C oracle in stream order; every packet of the batch
+    must come back bit-identical through srtp_unprotect_device."""
+    _gpu()
+    import numpy as np
+    import torch
+    ns, per, payload, tag = 65536, 128, 160, 10
+    rtp_len = 12 + payload
+    slot = (rtp_len + tag + 15) & ~15
+    n = ns * per
+    base = 0x10000000
+    pols = [policy("icm128_hmac80", ssrc=base + k, seed=k) for k in range(ns)]
+    snd, rcv = L.Session(pols), L.Session(pols)
+    snd.L.srtp_mi355x_set_key_buckets(buckets)
+    sample = list(range(0, ns, 64))
+    orc = O.Session([pols[s] for s in sample])
+    # sampled packets in stream order: stream s, its packets k = 0..per-1
+    rows = torch.tensor([k * ns + s for s in sample for k in range(per)],
+                        dtype=torch.int64, device="cuda")
+    gen = torch.Generator(device="cuda").manual_seed(303)
+    off = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+    seq0 = 0xff00    # batch 2 runs 0xff80 .. 0x007f: across a ROC boundary
+    for batch in range(2):
+        a = _rr_arena(ns, per, payload, seq0, base, gen, slot)
+        orig = a.clone()
+        d = a.view(-1)
+        ln = torch.full((n,), rtp_len, dtype=torch.int32, device="cuda")
+        cap = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+        st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        assert snd.protect_device(d, off, ln, d, off, cap, st) == 0
+        assert int((st != 0).sum()) == 0
+        assert bool((cap == rtp_len + tag).all())
+        # the oracle on the sampled streams
+        pin = orig[rows, :rtp_len].cpu().numpy().reshape(-1)
+        m = len(sample) * per
+        offs = np.arange(m, dtype=np.uint64) * rtp_len
+        bad, ref, rlen = orc.protect_many(pin, offs, np.full(m, rtp_len),
+                                          rtp_len + tag)
+        assert bad == 0 and (rlen == rtp_len + tag).all()
+        got = a[rows, :rtp_len + tag].cpu().numpy()
+        diff = np.nonzero((got != ref).any(axis=1))[0]
+        assert len(diff) == 0, ("oracle mismatch", diff[:8])
+        # every packet back through the receiver
+        cap2 = cap.clone()
+        st2 = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        assert rcv.unprotect_device(d, off, cap, d, off, cap2, st2) == 0
+        assert int((st2 != 0).sum()) == 0
+        assert bool((cap2 == rtp_len).all())
+        assert torch.equal(a[:, :rtp_len], orig[:, :rtp_len])
+        del a, orig, d
+        seq0 = (seq0 + per) & 0xffff
+    assert snd.prepass_stats() == (2, 0), snd.prepass_last_abort()
+    assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
+    assert snd.prepass_sorted_batches() == 0
+    snd.L.srtp_mi355x_set_key_buckets(0)
