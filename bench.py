@@ -114,45 +114,54 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target wall time of the CPU-baseline sample")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
-                    help="auto: measure roofline.traffic with two rocprofv3 "
-                         "PMC passes (child processes, N=1 only)")
+                    help="auto: measure roofline.traffic and roofline.issue "
+                         "with rocprofv3 PMC passes (child processes, N=1 "
+                         "only)")
     return ap.parse_args()
 
 
 def pmc_counter(path, kernel_substr, counter):
-    """mean per-launch value (KB) of one rocprofv3 --pmc counter of the
+    """mean per-dispatch value of one rocprofv3 --pmc counter of the
     kernels whose name contains kernel_substr, from counter_collection.csv"""
     import csv
-    vals = []
+    tot, disp = 0.0, set()
     with open(path) as f:
         for row in csv.DictReader(f):
             if kernel_substr in row.get("Kernel_Name", "") and \
                     row.get("Counter_Name", "") == counter:
-                vals.append(float(row.get("Counter_Value", 0) or 0))
-    return sum(vals) / len(vals) if vals else None
+                tot += float(row.get("Counter_Value", 0) or 0)
+                disp.add(row.get("Dispatch_Id"))
+    return tot / len(disp) if disp else None
 
 
-def measure_traffic(a, kname):
-    """HBM bytes per launch of the dominant kernel: FETCH_SIZE and
-    WRITE_SIZE in separate rocprofv3 --pmc passes (MI355X_MICROARCH.md: one
-    pass cannot hold both) over a short run of this same workload, started
-    as child processes before this process touches the GPU.  FETCH_SIZE is
-    TCC_EA0_RDREQ x 64 B; the kernel's reads are 64-B pieces (lane quads)
-    and 16-B lane reads, and the measured value equals the algorithmic read
-    bytes within 3 %, so it is taken as is (the x2 correction of the guide
-    is for 128-B requests of fully coalesced 1 KiB wave reads)."""
+# PMC passes (MI355X_MICROARCH.md: one pass holds at most 4 TCC counters,
+# FETCH_SIZE takes 3 and WRITE_SIZE 2, so they run separately)
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
+              ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES"))
+
+
+def measure_pmc(a, kname):
+    """per-launch PMC counters of the dominant kernel over a short run of
+    this same workload, one rocprofv3 --pmc pass per entry of PMC_PASSES,
+    each a child process started before this process touches the GPU.
+    FETCH_SIZE is TCC_EA0_RDREQ x 64 B; the kernel's reads are 64-B pieces
+    (lane quads) and 16-B lane reads, and the measured value equals the
+    algorithmic read bytes within 3 %, so it is taken as is (the x2
+    correction of the guide is for 128-B requests of fully coalesced 1 KiB
+    wave reads)."""
     import glob
     import shutil
     import subprocess
     import tempfile
     prof = shutil.which("rocprofv3")
     if not prof:
-        return None
+        return {}
     base = tempfile.mkdtemp(prefix="srtp_pmc_", dir="/tmp")
     got = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(base, ctr)
-        cmd = [prof, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o",
+    for k, ctrs in enumerate(PMC_PASSES):
+        d = os.path.join(base, "p%d" % k)
+        cmd = [prof, "--pmc"] + list(ctrs) + [
+               "--output-format", "csv", "-d", d, "-o",
                "p", "--", sys.executable, os.path.abspath(__file__),
                "--config", a.config, "--op", a.op, "--steps", "2",
                "--warmup", "1",
@@ -164,16 +173,41 @@ def measure_traffic(a, kname):
                            stderr=subprocess.DEVNULL, timeout=150,
                            env=dict(os.environ, TMPDIR="/tmp"))
         except subprocess.TimeoutExpired:
-            return None
+            break
         csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"),
                          recursive=True)
         if not csvs:
-            return None
-        got[ctr] = pmc_counter(csvs[0], kname, ctr)
-        if got[ctr] is None:
-            return None
+            break
+        for c in ctrs:
+            v = pmc_counter(csvs[0], kname, c)
+            if v is not None:
+                got[c] = v
     shutil.rmtree(base, ignore_errors=True)
-    return (got["FETCH_SIZE"] + got["WRITE_SIZE"]) * 1024.0
+    return got
+
+
+# issue floors measured on MI355X by probes (tools/valu_rate.hip,
+# tools/lds_rate.hip): the fastest VALU wave-instruction
+# (xor / and / add / bitop3) per SIMD, and one conflict-free ds_read_b32
+# per CU
+VALU_NS_PER_SIMD = 1.10
+LDS_NS_PER_CU = 1.21
+SIMDS, CUS = 1024, 256
+
+
+def issue_roofline(pmc, kernel_ms):
+    """SURVEY §8(d)'s second ceiling: the kernel's VALU and LDS
+    wave-instructions (PMC) against the probe-measured issue floors"""
+    v, l = pmc.get("SQ_INSTS_VALU"), pmc.get("SQ_INSTS_LDS")
+    if v is None or l is None:
+        return None
+    fv = v * VALU_NS_PER_SIMD / SIMDS * 1e-6      # ms
+    fl = l * LDS_NS_PER_CU / CUS * 1e-6
+    return {"bound": "valu+lds issue", "valu_insts": v, "lds_insts": l,
+            "valu_floor_ms": fv, "lds_floor_ms": fl,
+            "frac": max(fv, fl) / kernel_ms,
+            "valu_ns_per_simd": VALU_NS_PER_SIMD,
+            "lds_ns_per_cu": LDS_NS_PER_CU}
 
 
 def rank_ssrc(rank):
@@ -210,16 +244,38 @@ def timed_steps(step, steps, warmup, world, sync=None):
     return dt, res
 
 
+# the one-GPU box's host share: gpurun grants 16 CPUs of a larger host
+# (os.cpu_count() shows the whole host there)
+HOST_SHARE = 16
+
+
 def _ref_rate(lib_path, op, payload, gcm, threads, seconds):
     """packets/s of the reference build at lib_path: calibrate on one thread,
-    then ~`seconds` of work on `threads` threads"""
+    then ~`seconds` of work on `threads` threads (sized for HOST_SHARE
+    CPUs, so a thread count above the share does not stretch the sample)"""
     L = C.CDLL(lib_path)
     fn = L.ref_bench if op == "protect" else L.ref_bench_unprotect
     fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
     secs = C.c_double()
     n = fn(1, 8192, payload, int(gcm), C.byref(secs))
-    per_thread = max(8192, int(n / max(secs.value, 1e-6) * seconds))
+    busy = min(threads, HOST_SHARE)
+    per_thread = max(2048, int(n / max(secs.value, 1e-6) * seconds * busy /
+                               threads))
     done = fn(threads, per_thread, payload, int(gcm), C.byref(secs))
+    return done / secs.value, done
+
+
+def _ref_rate_streams(lib_path, payload, nstreams, threads, cycles=2):
+    """the reference with nstreams specific-SSRC streams per srtp_t, packets
+    round-robin (BASELINE configs[3]; every srtp_protect() scans the
+    reference's stream list): `cycles` passes over the streams per thread"""
+    L = C.CDLL(lib_path)
+    fn = L.ref_bench_streams
+    fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    secs = C.c_double()
+    done = fn(threads, cycles * nstreams, payload, nstreams, C.byref(secs))
+    if done <= 0 or secs.value <= 0:
+        return None
     return done / secs.value, done
 
 
@@ -229,21 +285,26 @@ def cpu_baseline(cfg, op, payload, seconds):
     oracle/_ref/bench_ref_*.so, cisco/libsrtp built from its own sources).
     Both crypto backends are timed (`backends`): OpenSSL 3 and the built-in
     crypto kernel that north_star names (no AES-GCM); `value` is the faster
-    of the two for this workload.  Threads: the
-    CPUs this process may run on, capped at 16 -- the one-GPU box grants a
-    16-CPU share of a larger host (`host_cpus`)."""
+    of the two for this workload.  Threads: every CPU this process may run
+    on (`affinity_cpus`; `cores`), the sample sized for the HOST_SHARE CPUs
+    the one-GPU box grants; `value_16` is the same at 16 threads.  configs[3]
+    (g711) adds `many_ssrc`: the reference with its 65,536 streams in one
+    srtp_t, packets round-robin -- its own stream lookup is a linear scan
+    (srtp/srtp.c:5292-5305)."""
     gcm = cfg == "gcm256"
     ref = os.path.join(ROOT, "oracle", "_ref")
     ossl = os.path.join(ref, "bench_ref_ossl.so")
     intk = os.path.join(ref, "bench_ref_int.so")
     affinity = len(os.sched_getaffinity(0))
-    threads = max(1, min(16, affinity))
+    threads = max(1, min(256, affinity))
     call = "srtp_%s()" % op
-    res = {}
-    if os.path.exists(ossl):
-        res["ossl"] = _ref_rate(ossl, op, payload, gcm, threads, seconds)
-    if os.path.exists(intk) and not gcm:
-        res["int"] = _ref_rate(intk, op, payload, gcm, threads, seconds)
+    res, res16 = {}, {}
+    for k, path in (("ossl", ossl), ("int", intk)):
+        if not os.path.exists(path) or (k == "int" and gcm):
+            continue
+        res[k] = _ref_rate(path, op, payload, gcm, threads, seconds)
+        res16[k] = _ref_rate(path, op, payload, gcm, 16, seconds / 2) \
+            if threads != 16 else res[k]
     if not res:
         return None
     # `value` is the faster backend (the stronger baseline: OpenSSL wins on
@@ -260,12 +321,31 @@ def cpu_baseline(cfg, op, payload, seconds):
                      "(oracle/Makefile.ref)" % (done, call, payload, threads,
                                                  backend[main_key]),
            "payload_GBps": rate * payload / 1e9,
+           "value_16": max(v[0] for v in res16.values()),
            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
            "backends": {"openssl": res["ossl"][0] if "ossl" in res else None,
                         "internal_kernel": res["int"][0] if "int" in res
                         else None}}
     if gcm:
         out["backends"]["internal_kernel_note"] = "no AES-GCM in that kernel"
+    if cfg == "g711" and op == "protect":
+        ms = {}
+        th = min(threads, HOST_SHARE)   # 65,536 stream contexts per thread
+        for k, path in (("ossl", ossl), ("int", intk)):
+            r = _ref_rate_streams(path, payload, STREAMS[cfg], th) \
+                if os.path.exists(path) else None
+            if r:
+                ms[k] = r
+        if ms:
+            mk = max(ms, key=lambda k: ms[k][0])
+            out["many_ssrc"] = {
+                "value": ms[mk][0], "unit": "pkt/s", "threads": th,
+                "backend": backend[mk],
+                "sample": "%d x srtp_protect(), %d streams with distinct keys "
+                          "per srtp_t, round-robin" % (ms[mk][1], STREAMS[cfg]),
+                "backends": {"openssl": ms["ossl"][0] if "ossl" in ms else None,
+                             "internal_kernel": ms["int"][0] if "int" in ms
+                             else None}}
     return out
 
 
@@ -402,9 +482,12 @@ def run_gpu(a, world, rank, local, json_out):
     pol, payload, npk, tag = CONFIGS[a.config]
     kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
     # PMC passes first: child processes, before this one touches the GPU
-    traffic = None
+    pmc = {}
     if world == 1 and a.traffic == "auto":
-        traffic = measure_traffic(a, kname)
+        pmc = measure_pmc(a, kname)
+    traffic = None
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        traffic = (pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
     import torch
     import torch.distributed as dist
     # SRTP_FORCE_DIST=1: a one-rank process group, so the RCCL barrier,
@@ -550,7 +633,8 @@ def run_gpu(a, world, rank, local, json_out):
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "kernel": kname, "kernel_ms": kernel_ms,
-                "algorithmic_bytes_per_launch": algo_bytes}
+                "algorithmic_bytes_per_launch": algo_bytes,
+                "issue": issue_roofline(pmc, kernel_ms)}
     prepass = {"device_batches": dev_b - dev_b0,
                "host_batches": host_b - host_b0,
                "last_abort": sess.prepass_last_abort()}

@@ -97,6 +97,14 @@ struct PpState {
     srtp_dev_rec_t *rec = nullptr;
     uint32_t *rec_idx = nullptr;
     uint32_t *bk_range = nullptr;
+    // fused single-stream chain form (k_pp_chain1): per-tile look-back
+    // words, {next tile, uses} counters, two abort words used in turn (the
+    // commit kernel of one batch clears the next batch's), the turn
+    uint64_t *ch_tile = nullptr;
+    uint32_t *ch_ctl = nullptr;
+    uint32_t *ch_abort = nullptr;
+    uint32_t ch_par = 0;
+    size_t ch_tiles_cap = 0;
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -856,6 +864,420 @@ __global__ void k_pu_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
 }
 
 // ---------------------------------------------------------------------------
+// The chain form of ONE stream in two launches (the sender's common case,
+// BASELINE configs[1] / configs[2]).  k_pp_chain1 parses every header,
+// classifies the packet (classify_one's checks), and computes every chain
+// packet's 48-bit index as the stored index's guess for the batch's first
+// chain packet plus the sum of the 16-bit advances before it (the reference's
+// per-packet index_guess, rdbx.c:112-145, when every advance is in
+// [1, 2^15)) -- a single-pass scan with decoupled look-back over tiles of
+// 1024 packets taken in dispatch order.  k_pp_chain1_commit then writes the
+// statuses and lengths, and its block 0 the stream: index, key uses, the
+// window shifted by the advance with one bit per chain packet inside it
+// (rdbx_add, crypto/replay/rdbx.c:253-270), the host's abort word, and the
+// reset of the look-back state for the next batch.
+// tiles of 4096 packets: 1024 threads x 4, all of a thread's offset loads,
+// then all of its header loads in flight (256 tiles for 2^20 packets: one
+// round of workgroups on the 256 CUs); the commit kernel uses 256-thread
+// blocks
+constexpr int CH_THREADS = 1024;
+constexpr int CH_ITEMS = 4;
+constexpr int CH_TILE = CH_THREADS * CH_ITEMS;
+constexpr int CH_COMMIT_THREADS = 256;
+// look-back word: [63:62] 1 = tile aggregate, 2 = inclusive prefix; [61] a
+// chain packet seen; aggregate: [60:45] first seq, [44:29] last seq, [28:0]
+// sum of the advances inside; prefix: [47:0] index of the last chain packet
+constexpr uint64_t CH_AGG = 1ull << 62, CH_PRE = 2ull << 62,
+                   CH_HAS = 1ull << 61, CH_FLAGS = 3ull << 62;
+// chain aggregate of a run of packets: has a chain packet, the first and
+// last chain packets' sequence numbers, the sum of the advances between
+// consecutive chain packets inside the run
+struct ChAgg {
+    uint32_t has, first, last, internal;
+};
+
+__device__ __forceinline__ ChAgg ch_none() { return ChAgg{ 0, 0, 0, 0 }; }
+
+// advance from the previous chain packet, flagged outside [1, 2^15)
+__device__ __forceinline__ uint32_t ch_adv(uint32_t from, uint32_t to,
+                                           uint32_t *bad)
+{
+    const uint32_t d = (to - from) & 0xffffu;
+    if (d == 0 || d >= SEQ_MEDIAN)
+        *bad = 1;
+    return d;
+}
+
+__device__ __forceinline__ ChAgg ch_combine(const ChAgg &a, const ChAgg &b,
+                                            uint32_t *bad)
+{
+    if (!a.has)
+        return b;
+    if (!b.has)
+        return a;
+    return ChAgg{ 1, a.first, b.last,
+                  a.internal + ch_adv(a.last, b.first, bad) + b.internal };
+}
+
+// a prefix state (has, index of the last chain packet) followed by a run
+__device__ __forceinline__ void ch_apply(uint32_t &has, uint64_t &idx,
+                                         const ChAgg &a, uint64_t stored,
+                                         uint32_t *bad)
+{
+    if (!a.has)
+        return;
+    if (has) {
+        idx += ch_adv((uint32_t)idx & 0xffffu, a.first, bad) + a.internal;
+    } else {
+        uint64_t e;
+        if (guess_index(stored, a.first, &e) < 1)
+            *bad = 1;   // at or below the stored index: the host decides
+        idx = e + a.internal;
+        has = 1;
+    }
+}
+
+struct Chain1Args {
+    ClassifyArgs C;          // in, offsets, lengths, capacities, streams, map
+    uint64_t *tile;          // look-back words, zero at entry
+    uint32_t *ctl;           // [0] next tile, [1] key uses
+    uint32_t *abort;         // this batch's abort word, zero at entry
+    uint32_t ntiles;
+};
+
+__device__ __forceinline__ uint64_t ch_pack_agg(const ChAgg &a)
+{
+    return CH_AGG | (a.has ? CH_HAS : 0) | ((uint64_t)a.first << 45) |
+           ((uint64_t)a.last << 29) | (a.internal & 0x1fffffffu);
+}
+
+__device__ __forceinline__ ChAgg ch_unpack_agg(uint64_t v)
+{
+    return ChAgg{ (v & CH_HAS) ? 1u : 0u, (uint32_t)(v >> 45) & 0xffffu,
+                  (uint32_t)(v >> 29) & 0xffffu, (uint32_t)v & 0x1fffffffu };
+}
+
+__device__ __forceinline__ ChAgg ch_shfl_down(const ChAgg &a, int d)
+{
+    return ChAgg{ (uint32_t)__shfl_down((int)a.has, d),
+                  (uint32_t)__shfl_down((int)a.first, d),
+                  (uint32_t)__shfl_down((int)a.last, d),
+                  (uint32_t)__shfl_down((int)a.internal, d) };
+}
+
+// wave 0 of a tile: the published state of the tiles before it, 64 at a
+// time (lane l reads tile j0 - l): the aggregates after the nearest
+// inclusive prefix are combined in tile order by a shuffle reduction.
+// Returns (has, index of the last chain packet) before the tile.
+__device__ void ch_lookback(const uint64_t *tile, uint32_t t, uint64_t stored,
+                            uint32_t &has, uint64_t &idx, uint32_t *bad)
+{
+    const int lane = threadIdx.x & 63;
+    ChAgg suf = ch_none();   // combined aggregates after the prefix found
+    has = 0;
+    idx = 0;
+    for (int64_t j0 = (int64_t)t - 1; j0 >= 0; j0 -= 64) {
+        const int64_t j = j0 - lane;
+        uint64_t v = CH_PRE;   // before tile 0: the stored state
+        if (j >= 0)
+            while (!((v = __hip_atomic_load(&tile[j], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)) &
+                     CH_FLAGS))
+                __builtin_amdgcn_s_sleep(1);
+        const uint64_t pm = __ballot((v & CH_FLAGS) == CH_PRE);
+        const int fl = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
+        // lanes below fl: aggregates, lane fl - 1 the earliest tile
+        ChAgg a = lane < fl ? ch_unpack_agg(v) : ch_none();
+        for (int d = 1; d < 64; d <<= 1) {
+            const ChAgg o = ch_shfl_down(a, d);   // an earlier tile
+            if (lane + d < 64)
+                a = ch_combine(o, a, bad);
+        }
+        // lane 0 holds the aggregates of lanes [0, fl) in tile order
+        const ChAgg w{ (uint32_t)__shfl((int)a.has, 0),
+                       (uint32_t)__shfl((int)a.first, 0),
+                       (uint32_t)__shfl((int)a.last, 0),
+                       (uint32_t)__shfl((int)a.internal, 0) };
+        suf = ch_combine(w, suf, bad);
+        if (pm) {
+            const uint64_t pv = (uint64_t)__shfl((long long)v, fl);
+            has = (pv & CH_HAS) ? 1u : 0u;
+            idx = pv & 0xffffffffffffull;
+            break;
+        }
+    }
+    ch_apply(has, idx, suf, stored, bad);
+}
+
+__device__ __forceinline__ ChAgg ch_shfl_up(const ChAgg &a, int d)
+{
+    return ChAgg{ (uint32_t)__shfl_up((int)a.has, d),
+                  (uint32_t)__shfl_up((int)a.first, d),
+                  (uint32_t)__shfl_up((int)a.last, d),
+                  (uint32_t)__shfl_up((int)a.internal, d) };
+}
+
+// inclusive scan over the wave's lanes in lane order
+__device__ __forceinline__ ChAgg ch_wave_scan(ChAgg a, uint32_t *bad)
+{
+    const int lane = threadIdx.x & 63;
+    for (int d = 1; d < 64; d <<= 1) {
+        const ChAgg o = ch_shfl_up(a, d);   // an earlier lane
+        if (lane >= d)
+            a = ch_combine(o, a, bad);
+    }
+    return a;
+}
+
+__global__ __launch_bounds__(CH_THREADS) void k_pp_chain1(Chain1Args A)
+{
+    const ClassifyArgs &C = A.C;
+    __shared__ uint32_t s_tile, s_has, s_uses, s_abort;
+    __shared__ uint64_t s_idx;
+    __shared__ ChAgg s_w[CH_THREADS / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) {
+        s_tile = atomicAdd(&A.ctl[0], 1u);   // dispatch order: look-back safe
+        s_uses = 0;
+        s_abort = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    // one stream: its record and its one SSRC (the map's only entry)
+    const srtp_dev_stream_t S = C.st[0];
+    const uint64_t stored = S.index;
+    const uint32_t base = tile * CH_TILE + t * CH_ITEMS;
+    uint32_t bad = 0, uses = 0, abort = 0, chain = 0;
+    uint64_t off[CH_ITEMS];
+    uint32_t len[CH_ITEMS], cap[CH_ITEMS], code[CH_ITEMS], seq[CH_ITEMS];
+    srtp_dev_hdr_t hh[CH_ITEMS];
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        const uint32_t i = base + k < C.n ? base + k : C.n - 1;
+        off[k] = C.in_off[i];
+        len[k] = C.in_len[i];
+        cap[k] = C.cap[i];
+    }
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++)
+        hh[k] = srtp_parse_rtp(C.in + off[k], off[k], len[k]);
+    ChAgg mine = ch_none();
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        code[k] = 0;
+        seq[k] = 0;
+        if (base + k >= C.n)
+            continue;
+        const srtp_dev_hdr_t &h = hh[k];
+        // classify_one's checks (srtp_host.c pre_protect; srtp.c:2515-2600)
+        if (h.enc_start >> 24) {
+            code[k] = h.enc_start >> 24;   // header does not parse
+        } else if (h.ssrc != S.ssrc) {
+            abort |= AB_UNKNOWN_SSRC;      // template clone: host
+        } else {
+            if (!(S.flags & SRTP_DS_ELIGIBLE) || (S.dir & SRTP_DIR_RX))
+                abort |= AB_INELIGIBLE;
+            uses++;                        // key usage (key.c:74)
+            if (cap[k] < len[k] + S.trailer) {
+                code[k] = ST_BUFFER_SMALL;
+            } else if (h.enc_start > len[k]) {
+                code[k] = ST_PARSE_ERR;
+            } else {
+                chain |= 1u << k;
+                seq[k] = h.seq_len & 0xffffu;
+                // aes_icm.c:317-322: at most 0xffff keystream blocks
+                if ((S.flags & SRTP_DS_ICM_CONF) &&
+                    (len[k] - h.enc_start + 15) / 16 > 0xffffu)
+                    code[k] = ST_CIPHER_FAIL;   // index still advances
+                mine = ch_combine(mine, ChAgg{ 1, seq[k], seq[k], 0 }, &bad);
+            }
+        }
+    }
+    // the tile's aggregate and each thread's exclusive prefix in the tile:
+    // lanes by shuffles, waves through LDS
+    const ChAgg incl = ch_wave_scan(mine, &bad);
+    ChAgg lex = ch_shfl_up(incl, 1);
+    if (lane == 0)
+        lex = ch_none();
+    if (lane == 63)
+        s_w[wv] = incl;
+    __syncthreads();
+    if (t < 64) {
+        ChAgg a = t < CH_THREADS / 64 ? s_w[t] : ch_none();
+        a = ch_wave_scan(a, &bad);
+        if (t < CH_THREADS / 64)
+            s_w[t] = a;   // inclusive over waves 0..t
+    }
+    __syncthreads();
+    const ChAgg wex = wv ? s_w[wv - 1] : ch_none();
+    const ChAgg excl = ch_combine(wex, lex, &bad);
+    const ChAgg tot = s_w[CH_THREADS / 64 - 1];
+    if (t == 0 && tile > 0)   // the aggregate first: nobody waits on it
+        __hip_atomic_store(&A.tile[tile], ch_pack_agg(tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (t < 64) {
+        // wave 0: the exclusive prefix, then the inclusive one published
+        uint32_t has = 0;
+        uint64_t idx = 0;
+        if (tile > 0)
+            ch_lookback(A.tile, tile, stored, has, idx, &bad);
+        if (t == 0) {
+            s_has = has;
+            s_idx = idx;
+            ch_apply(has, idx, tot, stored, &bad);
+            __hip_atomic_store(&A.tile[tile],
+                               CH_PRE | (has ? CH_HAS : 0) |
+                                   (idx & 0xffffffffffffull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    // this thread's packets: indices from the tile's exclusive prefix
+    uint32_t has = s_has;
+    uint64_t idx = s_idx;
+    ch_apply(has, idx, excl, stored, &bad);
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        const uint32_t i = base + k;
+        if (i >= C.n)
+            break;
+        uint64_t e = 0;
+        if (chain >> k & 1) {
+            ch_apply(has, idx, ChAgg{ 1, seq[k], seq[k], 0 }, stored, &bad);
+            e = idx;
+        }
+        C.est[i] = e;
+        C.pstat[i] = code[k];
+        srtp_dev_meta_t m;
+        m.key = 0;
+        m.roc = 0;
+        m.len = 0;
+        m.info = 0xff0000u;   // no crypto
+        if ((chain >> k & 1) && code[k] == 0) {
+            m.key = S.key;
+            m.roc = (uint32_t)(e >> 16);
+            m.info = hh[k].enc_start | (S.variant << 24);
+            m.len = hh[k].len;
+            C.olen[i] = hh[k].len + S.trailer;
+        }
+        C.meta[i] = m;
+    }
+    if (bad)
+        abort |= AB_SEQUENCE;
+    if (abort)
+        atomicOr(&s_abort, abort);
+    if (uses)
+        atomicAdd(&s_uses, uses);
+    __syncthreads();
+    if (t == 0) {
+        if (s_abort)
+            atomicOr(A.abort, s_abort);
+        if (s_uses)
+            atomicAdd(&A.ctl[1], s_uses);
+    }
+}
+
+struct Chain1Commit {
+    const uint32_t *pstat, *olen;
+    const uint64_t *est;
+    uint32_t n;
+    srtp_dev_stream_t *st;
+    uint32_t *win;
+    uint64_t *tile;
+    uint32_t *ctl;
+    uint32_t ntiles;
+    const uint32_t *abort;     // this batch's
+    uint32_t *abort_next;      // the next batch's, cleared here
+    uint32_t *pub;             // host-coherent copy of the verdict
+    int32_t *status;
+    uint32_t *out_len;
+};
+
+__global__ __launch_bounds__(CH_COMMIT_THREADS) void k_pp_chain1_commit(Chain1Commit A)
+{
+    const uint32_t ab = *A.abort;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < A.n && !ab) {
+        const uint32_t code = A.pstat[i];
+        A.status[i] = (int32_t)code;
+        if (code == 0)
+            A.out_len[i] = A.olen[i];   // error packets keep out_len = capacity
+    }
+    if (blockIdx.x != 0)
+        return;
+    __shared__ uint32_t s_win[SEQ_MEDIAN / 32];   // up to 2^15 window bits
+    __shared__ uint32_t s_stop;
+    srtp_dev_stream_t &S = A.st[0];
+    const uint64_t last = A.tile[A.ntiles - 1];
+    const bool has = (last & CH_HAS) != 0;
+    const uint64_t hi = last & 0xffffffffffffull;
+    const uint32_t uses = A.ctl[1];
+    const uint32_t words = S.win_bits >> 5;
+    const uint64_t old = S.index;
+    if (!ab && has) {
+        // rdbx_add's shift by the advance, then one bit per chain packet
+        // within win_bits of the new index (crypto/math/datatypes.c
+        // bitvector_left_shift)
+        const uint64_t adv = hi - old;
+        const uint32_t *w = A.win + S.win_off;
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x) {
+            uint32_t v = 0;
+            if (adv < S.win_bits) {
+                const uint32_t b0 = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+                const uint32_t a = x + b0 < words ? w[x + b0] : 0u;
+                const uint32_t b = x + b0 + 1 < words ? w[x + b0 + 1] : 0u;
+                v = bi ? (a >> bi) | (b << (32 - bi)) : a;
+            }
+            s_win[x] = v;
+        }
+        if (threadIdx.x == 0)
+            s_stop = 0;
+        __syncthreads();
+        // chain indices increase along the batch: walk back from its end
+        // until a chain packet falls out of the window
+        for (int64_t c = (int64_t)A.n - 1; c >= 0; c -= blockDim.x) {
+            const int64_t j = c - (int64_t)threadIdx.x;
+            if (j >= 0) {
+                const uint64_t e = A.est[j];
+                if (e) {
+                    if (hi - e < S.win_bits) {
+                        const uint32_t bit = S.win_bits - 1 - (uint32_t)(hi - e);
+                        atomicOr(&s_win[bit >> 5], 1u << (bit & 31));
+                    } else {
+                        s_stop = 1;
+                    }
+                }
+            }
+            __syncthreads();
+            const uint32_t stop = s_stop;
+            __syncthreads();
+            if (stop)
+                break;
+        }
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x)
+            A.win[S.win_off + x] = s_win[x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!ab) {
+            S.uses += uses;
+            if (uses)
+                S.dir |= SRTP_DIR_TX;
+            if (has)
+                S.index = hi;
+        }
+        if (A.pub)
+            __hip_atomic_store(A.pub, ab, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        A.ctl[0] = 0;
+        A.ctl[1] = 0;
+        *A.abort_next = 0;
+    }
+    for (uint32_t x = threadIdx.x; x < A.ntiles; x += blockDim.x)
+        A.tile[x] = 0;
+}
+
+// ---------------------------------------------------------------------------
 // Key buckets: a batch of many streams with distinct keys
 // is laid out for the crypto kernel as one bucket of records per stream, so
 // that a wave's 64 packets share one key (SGPR round keys, the four-table
@@ -1082,6 +1504,13 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     const size_t nt = (c + srtp_scan::TILE - 1) / srtp_scan::TILE;
     PPCHK(hipMalloc((void **)&P->hist, 256 * nt * 4));
     PPCHK(hipMalloc((void **)&P->agg, (nt + 2) * sizeof(srtp_scan::Agg)));
+    // k_pp_chain1 look-back words: zero between batches
+    if (P->ch_tile)
+        PPCHK(hipFree(P->ch_tile));
+    PPCHK(hipMalloc((void **)&P->ch_tile, (nt + 1) * 8));
+    PPCHK(hipMemsetAsync(P->ch_tile, 0, (nt + 1) * 8, stream));
+    PPCHK(hipStreamSynchronize(stream));
+    P->ch_tiles_cap = nt;
     P->n_cap = c;
     return 0;
 }
@@ -1100,7 +1529,8 @@ void srtp_gpu_pp_free(void *p)
                      P->new_index, P->hdr, P->pstat, P->skey, P->skey2,
                      P->perm, P->perm2, P->val, P->est, P->meta, P->agg,
                      P->hist, P->auth, P->top, P->abort, P->bk_off, P->bk_cur,
-                     P->rec, P->rec_idx, P->bk_range };
+                     P->rec, P->rec_idx, P->bk_range, P->ch_tile,
+                     P->ch_ctl, P->ch_abort };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -1136,6 +1566,10 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     if (!P->abort) {
         PPCHK(hipMalloc((void **)&P->abort, 4));
         PPCHK(hipMalloc((void **)&P->bk_range, 16));
+        PPCHK(hipMalloc((void **)&P->ch_ctl, 8));
+        PPCHK(hipMalloc((void **)&P->ch_abort, 8));
+        PPCHK(hipMemset(P->ch_ctl, 0, 8));
+        PPCHK(hipMemset(P->ch_abort, 0, 8));
         PPCHK(hipHostMalloc((void **)&P->h_abort, 4,
                             hipHostMallocMapped | hipHostMallocCoherent));
         PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
@@ -1286,6 +1720,110 @@ static hipError_t stream_order(PpState *P, uint32_t ns, uint32_t N,
                                  end_bit, P->hist, P->agg, stream);
 }
 
+// SRTP_PP_FUSED=0: one-stream batches through the multi-launch chain form
+static bool fused_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("SRTP_PP_FUSED");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
+// the one-stream chain form in two launches (k_pp_chain1 + commit), then
+// the crypto kernels; see k_pp_chain1
+static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
+                             hipStream_t stream, int *fallback)
+{
+    const uint32_t N = (uint32_t)b->n;
+    const uint32_t nt = (N + CH_TILE - 1) / CH_TILE;
+    uint32_t *ab = P->ch_abort + P->ch_par;
+    uint32_t *ab_next = P->ch_abort + (P->ch_par ^ 1);
+    P->ch_par ^= 1;
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    Chain1Args A;
+    A.C.in = b->in;
+    A.C.in_off = b->in_off;
+    A.C.in_len = b->in_len;
+    A.C.cap = b->out_len;
+    A.C.st = P->st;
+    A.C.hkey = P->hkey;
+    A.C.hval = P->hval;
+    A.C.hmask = P->hcap - 1;
+    A.C.n = N;
+    A.C.hdr = P->hdr;
+    A.C.pstat = P->pstat;
+    A.C.skey = P->skey;
+    A.C.perm = P->perm;
+    A.C.bcount = P->bcount;
+    A.C.abort = ab;
+    A.C.est = P->est;
+    A.C.new_index = nullptr;
+    A.C.meta = P->meta;
+    A.C.olen = P->skey2;   // protected lengths
+    A.tile = P->ch_tile;
+    A.ctl = P->ch_ctl;
+    A.abort = ab;
+    A.ntiles = nt;
+    hipLaunchKernelGGL(k_pp_chain1, dim3(nt), dim3(CH_THREADS), 0, stream, A);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "chain1"))
+        return -1;
+    Chain1Commit K;
+    K.pstat = P->pstat;
+    K.olen = P->skey2;
+    K.est = P->est;
+    K.n = N;
+    K.st = P->st;
+    K.win = P->win;
+    K.tile = P->ch_tile;
+    K.ctl = P->ch_ctl;
+    K.ntiles = nt;
+    K.abort = ab;
+    K.abort_next = ab_next;
+    K.pub = P->h_abort_dev;
+    K.status = b->status;
+    K.out_len = b->out_len;
+    hipLaunchKernelGGL(k_pp_chain1_commit,
+                       dim3((N + CH_COMMIT_THREADS - 1) / CH_COMMIT_THREADS),
+                       dim3(CH_COMMIT_THREADS), 0, stream, K);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "chain1_commit"))
+        return -1;
+    srtp_gpu_batch_t cb = {};
+    cb.n = b->n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;
+    cb.auth_ok = nullptr;
+    cb.uniform_key = b->uniform_key;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = ab;
+    if (srtp_gpu_run(g, 0, &cb))
+        return -1;
+    if (pp_step(stream, "crypto"))
+        return -1;
+    b->sorted = 1;
+    if (b->async) {
+        hipError_t we;
+        const uint32_t v = wait_published(P, stream, &we);
+        if (we != hipSuccess)
+            return pp_fail(we, "waiting for the pre-pass verdict");
+        if (v == 0) {
+            *fallback = 0;
+            return 0;
+        }
+    }
+    PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, ab, 4, hipMemcpyDeviceToHost));
+    *fallback = (int)*P->h_abort;
+    return 0;
+}
+
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback)
 {
@@ -1304,6 +1842,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
     const uint32_t N = (uint32_t)n, ns = P->ns;
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
+    if (ns == 1 && fused_on())
+        return pp_protect_chain1(g, P, b, stream, fallback);
 
     // many streams: the order-free form first (no sort); AB_ORDER -> again
     // through the sorted chain path.  SRTP_PP_SORTED=1 forces the latter.

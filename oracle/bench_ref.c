@@ -12,6 +12,12 @@
  * (untimed) with a sender srtp_t, then srtp_unprotect()s it in place on a
  * receiver srtp_t (timed), pool after pool; *seconds is the slowest
  * thread's unprotect time.
+ *
+ * Many streams (BASELINE configs[3]): ref_bench_streams() -- each thread's
+ * srtp_t holds nstreams specific-SSRC streams with distinct master keys
+ * (srtp_create over a policy list; untimed) and protects packets
+ * round-robin over them, so every srtp_protect() goes through the
+ * reference's stream-list lookup (srtp/srtp.c:5292-5305, a linear scan).
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -116,8 +122,8 @@ static void *run(void *arg)
     return NULL;
 }
 
-static int bench(int threads, long pkts_per_thread, int payload, int gcm,
-                 int unprotect, double *seconds)
+/* srtp_init() once per process, whichever driver runs first */
+static int ref_init(void)
 {
     static int inited;
     if (!inited) {
@@ -125,6 +131,14 @@ static int bench(int threads, long pkts_per_thread, int payload, int gcm,
             return -1;
         inited = 1;
     }
+    return 0;
+}
+
+static int bench(int threads, long pkts_per_thread, int payload, int gcm,
+                 int unprotect, double *seconds)
+{
+    if (ref_init())
+        return -1;
     pthread_t th[256];
     job_t jobs[256];
     if (threads > 256)
@@ -153,6 +167,104 @@ static int bench(int threads, long pkts_per_thread, int payload, int gcm,
     *seconds = unprotect ? slowest
                          : (double)(b.tv_sec - a.tv_sec) +
                                1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+    return (int)done;
+}
+
+typedef struct {
+    long n;
+    int payload, nstreams;
+    long done;
+    double secs; /* protect time, setup excluded */
+} sjob_t;
+
+static void *run_streams(void *arg)
+{
+    sjob_t *j = (sjob_t *)arg;
+    const int ns = j->nstreams;
+    srtp_policy_t *p = (srtp_policy_t *)calloc((size_t)ns, sizeof *p);
+    uint8_t *keys = (uint8_t *)malloc((size_t)ns * 46);
+    uint64_t x = 0x5352545030303031ULL ^ (uint64_t)(uintptr_t)j;
+    for (size_t i = 0; i < (size_t)ns * 46; i++) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        keys[i] = (uint8_t)x;
+    }
+    for (int k = 0; k < ns; k++) {
+        srtp_crypto_policy_set_rtp_default(&p[k].rtp);
+        srtp_crypto_policy_set_rtcp_default(&p[k].rtcp);
+        p[k].ssrc.type = ssrc_specific;
+        p[k].ssrc.value = 0x10000000u + (uint32_t)k;
+        p[k].key = keys + 46 * (size_t)k;
+        p[k].window_size = 128;
+        p[k].next = k + 1 < ns ? &p[k + 1] : NULL;
+    }
+    srtp_t s;
+    if (srtp_create(&s, p)) {
+        free(keys);
+        free(p);
+        return NULL;
+    }
+    const size_t slot = (size_t)(12 + j->payload + 64 + 63) & ~(size_t)63;
+    const int pool = 4096;
+    uint8_t *buf = (uint8_t *)aligned_alloc(64, slot * (size_t)pool);
+    for (size_t i = 0; i < slot * (size_t)pool; i++) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        buf[i] = (uint8_t)x;
+    }
+    const double t0 = now();
+    for (long i = 0; i < j->n; i++) {
+        uint8_t *pk = buf + slot * (size_t)(i % pool);
+        const uint32_t ssrc = 0x10000000u + (uint32_t)(i % ns);
+        const uint16_t seq = (uint16_t)(0x1234 + i / ns);
+        pk[0] = 0x80;
+        pk[1] = 96;
+        pk[2] = (uint8_t)(seq >> 8);
+        pk[3] = (uint8_t)seq;
+        pk[8] = (uint8_t)(ssrc >> 24);
+        pk[9] = (uint8_t)(ssrc >> 16);
+        pk[10] = (uint8_t)(ssrc >> 8);
+        pk[11] = (uint8_t)ssrc;
+        size_t len = slot;
+        if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0)
+            j->done++;
+    }
+    j->secs = now() - t0;
+    free(buf);
+    srtp_dealloc(s);
+    free(keys);
+    free(p);
+    return NULL;
+}
+
+int ref_bench_streams(int threads, long pkts_per_thread, int payload,
+                      int nstreams, double *seconds)
+{
+    *seconds = 0;
+    if (ref_init())
+        return -1;
+    pthread_t th[256];
+    sjob_t jobs[256];
+    if (threads > 256)
+        threads = 256;
+    for (int t = 0; t < threads; t++) {
+        memset(&jobs[t], 0, sizeof jobs[t]);
+        jobs[t].n = pkts_per_thread;
+        jobs[t].payload = payload;
+        jobs[t].nstreams = nstreams;
+        pthread_create(&th[t], NULL, run_streams, &jobs[t]);
+    }
+    long done = 0;
+    double slowest = 0;
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        done += jobs[t].done;
+        if (jobs[t].secs > slowest)
+            slowest = jobs[t].secs;
+    }
+    *seconds = slowest;
     return (int)done;
 }
 
