@@ -285,9 +285,10 @@ def cpu_baseline(cfg, op, payload, seconds):
     oracle/_ref/bench_ref_*.so, cisco/libsrtp built from its own sources).
     Both crypto backends are timed (`backends`): OpenSSL 3 and the built-in
     crypto kernel that north_star names (no AES-GCM); `value` is the faster
-    of the two for this workload.  Threads: every CPU this process may run
-    on (`affinity_cpus`; `cores`), the sample sized for the HOST_SHARE CPUs
-    the one-GPU box grants; `value_16` is the same at 16 threads.  configs[3]
+    of the two for this workload.  Timed at every CPU this process may run
+    on (`value_affinity`; the sample sized for the HOST_SHARE CPUs the
+    one-GPU box grants) and at 16 threads (`value_16`); `value` / `cores` is
+    the faster of the two.  configs[3]
     (g711) adds `many_ssrc`: the reference with its 65,536 streams in one
     srtp_t, packets round-robin -- its own stream lookup is a linear scan
     (srtp/srtp.c:5292-5305)."""
@@ -314,14 +315,21 @@ def cpu_baseline(cfg, op, payload, seconds):
     backend = {"ossl": "OpenSSL 3 crypto backend",
                "int": "built-in crypto kernel"}
     rate, done = res[main_key]
-    out = {"value": rate, "unit": "pkt/s", "cores": threads,
+    k16 = max(res16, key=lambda k: res16[k][0])
+    # the stronger of the two thread counts is `value` (the one-GPU box
+    # grants 16 CPUs; more threads than that only share them)
+    best = (rate, done, threads, main_key)
+    if res16[k16][0] > rate:
+        best = (res16[k16][0], res16[k16][1], 16, k16)
+    out = {"value": best[0], "unit": "pkt/s", "cores": best[2],
            "kind": "reference",
            "sample": "%d x %s of %d-byte payloads, %d threads x 1 srtp_t, "
                      "cisco/libsrtp 3.0.0 with the %s, built from source "
-                     "(oracle/Makefile.ref)" % (done, call, payload, threads,
-                                                 backend[main_key]),
-           "payload_GBps": rate * payload / 1e9,
-           "value_16": max(v[0] for v in res16.values()),
+                     "(oracle/Makefile.ref)" % (best[1], call, payload,
+                                                 best[2], backend[best[3]]),
+           "payload_GBps": best[0] * payload / 1e9,
+           "value_affinity": rate, "threads_affinity": threads,
+           "value_16": res16[k16][0],
            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
            "backends": {"openssl": res["ossl"][0] if "ossl" in res else None,
                         "internal_kernel": res["int"][0] if "int" in res

@@ -588,6 +588,23 @@ DEV u32x4 GhTab<true>::get(uint32_t w, int k) const
     return *(const u32x4 *)(lds + a);
 }
 
+// The 8-copy Shoup table (32 KiB after the four AES tables, 160 KiB in
+// all): entry b of copy c at base + b * 128 + c * 16, c = lane & 7 (two
+// lanes of a ds_read_b128 group share a copy: a 2-way conflict when their
+// entries have the same parity).  The entry offset is a shift of the word
+// plus one full-rate v_bitop3 with the lane template (base | c * 16).
+struct GhTab8 {
+    const char *lds;   // LDS base (address 0)
+    uint32_t tmpl;     // table base | (lane & 7) * 16
+    DEV u32x4 get(uint32_t w, int k) const
+    {
+        // byte k of BE word w (k = 0 the most significant) -> bits 14:7
+        const uint32_t s = k == 3 ? (w << 7) : (w >> (17 - 8 * k));
+        return *(const u32x4 *)(lds + __builtin_amdgcn_bitop3_b32(
+                                          s, 0x7f80u, tmpl, 0xEA));
+    }
+};
+
 template <>
 DEV u32x4 GhTab<false>::get(uint32_t w, int k) const
 {
@@ -604,8 +621,8 @@ DEV u32x4 GhTab<false>::get(uint32_t w, int k) const
 //   word 0 ^= o ^ o>>1 ^ o>>2 ^ o>>7,  word 1 ^= o<<31 ^ o<<30 ^ o<<25
 // (6 shifts per 4 steps instead of 4 per step: the shifts are half-rate
 // VALU on gfx950, tools/valu_rate.hip).
-template <bool LDSM>
-DEV void ghash_mul(uint32_t x[4], const GhTab<LDSM> &T)
+template <class TAB>
+DEV void ghash_mul(uint32_t x[4], const TAB &T)
 {
     u32x4 z = T.get(x[3], 3);
     uint32_t o = 0;

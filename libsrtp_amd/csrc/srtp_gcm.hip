@@ -17,6 +17,11 @@ namespace {
 #ifndef GCM_PF
 #define GCM_PF 2   // 64-byte payload chunks loaded ahead of their use
 #endif
+// uniform-key batches: the four AES tables (128 KiB) with an 8-copy GHASH
+// table (32 KiB), instead of (T0, T1) with a 16-copy GHASH table
+#ifndef GCM_TAB4
+#define GCM_TAB4 1
+#endif
 
 DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
 {
@@ -31,9 +36,9 @@ DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
 // chunks of four CTR blocks whose counters stay in the cached epoch
 // (j + 2 <= 255: the first 4 KiB), data loaded GCM_PF chunks ahead; the
 // rest block by block with full AES.
-template <int NR, bool PROTECT, bool UNIFORM, class KEY>
-DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
-                    GhTab<UNIFORM> G, KEY &rk)
+template <int NR, bool PROTECT, bool UNIFORM, bool TAB4, class GT, class KEY>
+DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
+                    KEY &rk)
 {
     const srtp_dev_meta_t m = A.meta[i];
     constexpr uint32_t VID = 16u + 2u * ((NR - 8) / 2);
@@ -90,7 +95,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
     nfc = nfc < 63 ? nfc : 63;
     if (nfc) {
         const uint32_t cc[4] = { c0, c1, c2, 0u };   // BE32(j+2) < 256
-        const CtrCache C = ctr_cache<NR, false>(cc, rk, T);
+        const CtrCache C = ctr_cache<NR, TAB4>(cc, rk, T);
         u32x4 ring[GCM_PF][4];
 #pragma unroll
         for (int k = 0; k < GCM_PF; k++)
@@ -117,7 +122,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
             for (int g = 0; g < 4; g += 2) {
                 const uint32_t jb[2] = { (4 * c + g + 2) << 8,
                                          (4 * c + g + 3) << 8 };
-                aes_ctr<2, NR, false>(
+                aes_ctr<2, NR, TAB4>(
                     *reinterpret_cast<uint32_t(*)[2][4]>(&ks[g]), jb, C, rk, T);
             }
 #endif
@@ -148,7 +153,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
         else
             v = load_partial(pin + 16 * j, rem);
         uint32_t k0 = c0, k1 = c1, k2 = c2, k3 = bswap(j + 2);
-        aes_block<NR, false>(k0, k1, k2, k3, rk, T);
+        aes_block<NR, TAB4>(k0, k1, k2, k3, rk, T);
         u32x4 o = { v.x ^ k0, v.y ^ k1, v.z ^ k2, v.w ^ k3 };
         u32x4 ctv = PROTECT ? o : v;
         if (rem < 16) {   // zero-pad the last ciphertext block for GHASH
@@ -179,7 +184,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T,
     ghash_mul(x, G);
     // tag = E(J0) ^ S
     uint32_t e0 = c0, e1 = c1, e2 = c2, e3 = bswap(1u);
-    aes_block<NR, false>(e0, e1, e2, e3, rk, T);
+    aes_block<NR, TAB4>(e0, e1, e2, e3, rk, T);
     uint32_t tagw[4] = { bswap(x[0]) ^ e0, bswap(x[1]) ^ e1, bswap(x[2]) ^ e2,
                          bswap(x[3]) ^ e3 };   // little-endian words of tag
     if (PROTECT) {
@@ -207,13 +212,27 @@ constexpr int GCM_THREADS = GCM_THREADS_N;
 template <int NR, bool PROTECT, bool UNIFORM>
 __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 {
-    __shared__ u32x4 s_tab[(AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) / 16];
+    constexpr bool TAB4 = UNIFORM && GCM_TAB4;
+    constexpr int GH8 = 256 * 16 * 8;   // the 8-copy GHASH table
+    __shared__ u32x4 s_tab[(TAB4 ? AES_TAB4_BYTES + GH8
+                                 : AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) /
+                           16];
     if (A.abort && *A.abort)
         return;
-    if (A.rest && *A.any != A.any_seq)
-        return;   // k_gcm_wave took every group
+    if constexpr (TAB4) {
+        // the S-box row of the table build sits where the GHASH table goes
+        uint32_t *t0 = (uint32_t *)((char *)s_tab + AES_TAB4_BYTES);
+        load_aes_tables<true>(s_tab, t0);
+        __syncthreads();
+        const u32x4 *src =
+            (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
+        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB4_BYTES);
+        for (int e = threadIdx.x; e < 256 * 8; e += blockDim.x)
+            dst[e] = src[e >> 3];
+    } else {
     load_aes_tables<false>(s_tab);
-    if (UNIFORM) {
+    }
+    if (UNIFORM && !TAB4) {
         const u32x4 *src =
             (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
         u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB2_BYTES);
@@ -227,15 +246,23 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
     typename std::conditional<UNIFORM, UniKey<NR>, LaneKey<NR>>::type rk;
     if (UNIFORM)
         rk.load(A.keys + A.uni);
+    const uint32_t stride = gridDim.x * blockDim.x;
+    if constexpr (TAB4) {
+        GhTab8 G;
+        G.lds = lds;
+        G.tmpl = (uint32_t)AES_TAB4_BYTES | ((threadIdx.x & 7) * 16);
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+             i += stride)
+            gcm_packet<NR, PROTECT, UNIFORM, true>(A, i, T, G, rk);
+        return;
+    }
     GhTab<UNIFORM> G;
     G.lds = lds + AES_TAB2_BYTES - 0x10000;   // the 0x10000 comes from lane16
     G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
     G.g = nullptr;
-    const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
          i += stride)
-        if (!A.rest || A.rest[i >> 6])
-            gcm_packet<NR, PROTECT, UNIFORM>(A, i, T, G, rk);
+        gcm_packet<NR, PROTECT, UNIFORM, false>(A, i, T, G, rk);
 }
 
 }   // namespace

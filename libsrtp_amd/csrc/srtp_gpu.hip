@@ -1,8 +1,8 @@
 // srtp_gpu.hip -- the thin extern "C" FFI (srtp_dev.h) between the C host
 // engine and the HIP kernels: device context, key table, kernel dispatch,
 // plus the small kernels (speculative-unprotect undo, SRTCP, header parse).
-// The RTP crypto kernels live in srtp_icm.hip, srtp_gcm.hip and
-// srtp_gcm_wave.hip (srtp_gpu_int.h).
+// The RTP crypto kernels live in srtp_icm.hip and srtp_gcm.hip
+// (srtp_gpu_int.h).
 #include <stdio.h>
 #include <stdlib.h>
 
@@ -1222,13 +1222,6 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
-    A.rest = nullptr;
-    A.any = nullptr;
-    A.any_seq = 0;
-    // uniform-key batches: the cooperative wave kernel first; it leaves
-    // the groups it cannot take to k_gcm
-    if (launch_gcm_wave(g, A, NR, PROT, st) < 0)
-        return -1;
     return launch_gcm_nr<NR>(A, PROT, g->ncu, st);
 }
 
@@ -1295,11 +1288,6 @@ int srtp_gpu_open(srtp_gpu_t **gp)
                                  dev));
     if (g->ncu <= 0)
         g->ncu = 256;
-    // k_gcm_wave (uniform-key GCM groups on the cooperative memory path) is
-    // opt-in: it moves 10 % fewer HBM bytes than k_gcm but issues more VALU
-    // work per packet, and measured 3.5 % slower on MI355X
-    const char *wv = getenv("SRTP_MI355X_WAVE");
-    g->wave_off = !(wv && wv[0] == '1');
     HIPCHK(hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&g->ev0));
     HIPCHK(hipEventCreate(&g->ev1));
@@ -1315,8 +1303,6 @@ void srtp_gpu_close(srtp_gpu_t *g)
     srtp_gpu_pp_free(g->pp);
     (void)hipFree(g->d_keys);
     (void)hipFree(g->d_ghash);
-    (void)hipFree(g->d_rest);
-    (void)hipFree(g->d_any);
     (void)hipFree(g->d_raw);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);

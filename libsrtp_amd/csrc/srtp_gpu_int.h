@@ -7,8 +7,6 @@
 //                       HMAC-SHA1 kernel; compiled once per AES round count
 //   srtp_gcm.hip        k_gcm (AES-GCM), one lane per packet, any batch;
 //                       compiled once per round count
-//   srtp_gcm_wave.hip   k_gcm_wave: uniform-key GCM groups of 64 same-shape
-//                       packets on the cooperative memory path
 //   srtp_prepass.hip    the device pre-pass of srtp_protect_device
 #pragma once
 
@@ -28,11 +26,6 @@ struct srtp_gpu {
     float last_ms;
     void *pp;         // device pre-pass state (srtp_prepass.hip)
     int ncu;          // compute units (persistent grids)
-    uint8_t *d_rest;  // per-64-packet-group "left to the per-lane kernel"
-    size_t rest_cap;  // bytes of d_rest
-    uint32_t *d_any;  // = wave_seq when the last wave kernel left a group
-    uint32_t wave_seq;
-    int wave_off;     // k_gcm_wave disabled (SRTP_MI355X_WAVE != 1)
     // single-buffer cipher / auth calls of the crypto-kernel API
     // (srtp_plugin.c -> srtp_gpu_raw): scratch grown on demand
     uint8_t *d_raw;
@@ -71,12 +64,6 @@ struct GcmArgs {
     const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;
-    // hand-off from k_gcm_wave: group g of 64 packets is k_gcm's when
-    // rest[g] != 0; *any == any_seq when any group is.  NULL rest: every
-    // packet is k_gcm's.
-    const uint8_t *rest;
-    const uint32_t *any;
-    uint32_t any_seq;
 };
 
 // records a HIP error in the FFI's error string, returns -1
@@ -102,11 +89,6 @@ enum IcmKeyMode {
 template <int NR, int KM>
 int launch_icm_km(const IcmArgs &A, bool auth, bool prot, int ncu,
                   hipStream_t st);
-
-// k_gcm_wave launcher (srtp_gcm_wave.hip): 1 when it launched (A.rest /
-// A.any then set for k_gcm), 0 when the batch has no wave path, -1 on error
-int launch_gcm_wave(srtp_gpu_t *g, GcmArgs &A, int nr, bool prot,
-                    hipStream_t st);
 
 // k_gcm launchers (srtp_gcm.hip, one object per NR in {10,14})
 template <int NR>

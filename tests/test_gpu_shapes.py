@@ -1,6 +1,6 @@
 """GPU parity of the uniform-key protect paths (k_icm_hmac's lane-quad
-cooperative steady state, srtp_icm.hip; AES-GCM by k_gcm and the opt-in
-k_gcm_wave, srtp_gcm_wave.hip) over device
+cooperative steady state, srtp_icm.hip; AES-GCM by k_gcm, srtp_gcm.hip)
+over device
 arenas of many packet shapes, against the CPU oracle (oracle/srtp_oracle.c,
 pinned to the reference's fixtures).
 
@@ -199,26 +199,18 @@ def test_shapes_roc_wrap():
         assert rc == 0 and out[i * slot:i * slot + len(ref)] == ref, i
 
 
-# AES-GCM: k_gcm, and the opt-in k_gcm_wave (SRTP_MI355X_WAVE=1, read when
-# a session opens its device context)
-WAVE = pytest.mark.parametrize("wave", ["0", "1"], ids=["k_gcm", "k_gcm_wave"])
+# AES-GCM: k_gcm (uniform keys: four AES tables + 8-copy GHASH table)
 
 
-@WAVE
 @pytest.mark.parametrize("pname", ["gcm128_16", "gcm256_16", "gcm256_8"])
-def test_shapes_gcm_out_of_place(pname, wave, monkeypatch):
-    monkeypatch.setenv("SRTP_MI355X_WAVE", wave)
+def test_shapes_gcm_out_of_place(pname):
     _run(21, ngroups=40, inplace=False, tail=9, pname=pname)
 
 
-@WAVE
 @pytest.mark.parametrize("pname", ["gcm128_16", "gcm256_16"])
-def test_shapes_gcm_in_place_mixed(pname, wave, monkeypatch):
-    monkeypatch.setenv("SRTP_MI355X_WAVE", wave)
+def test_shapes_gcm_in_place_mixed(pname):
     _run(22, ngroups=30, inplace=True, mixed_every=3, pname=pname)
 
 
-@WAVE
-def test_shapes_gcm_template_many_ssrcs(wave, monkeypatch):
-    monkeypatch.setenv("SRTP_MI355X_WAVE", wave)
+def test_shapes_gcm_template_many_ssrcs():
     _run(23, ngroups=20, inplace=False, nssrc=7, tail=3, pname="gcm256_16")
