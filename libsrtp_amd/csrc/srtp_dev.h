@@ -80,6 +80,10 @@ typedef struct srtp_dev_rec {
  * caller's in-place flag (rtp == srtp in srtp_protect's terms) and bit 1
  * (undo only) says the run being undone applied cryptex */
 #define SRTP_VARIANT_X 24u
+/* session keys whose cipher or auth type an application replaced
+ * (srtp_replace_cipher_type / srtp_replace_auth_type): no kernel takes
+ * them; the host runs their crypto through the registered vtables */
+#define SRTP_VARIANT_V 25u
 #define SRTP_XI_INPLACE 1u
 #define SRTP_XI_CRYPTEX 2u
 /* k_xrtp result byte (auth_ok[i]): bit 0 authenticated (unprotect) / done,

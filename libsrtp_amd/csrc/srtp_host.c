@@ -106,6 +106,15 @@ typedef struct {
     /* RFC 6904 extension-header key (srtp.c:1385-1500): own device slot,
      * ~0 without header-extension encryption */
     uint32_t xslot;
+    /* routed key (variant SRTP_VARIANT_V): the RTP cipher / auth objects of
+     * the REGISTERED types, as the reference allocates them from its crypto
+     * kernel (srtp.c:594-752, 1342-1525), the AEAD salt, the services */
+    srtp_cipher_t *vc;
+    srtp_auth_t *va;
+    uint8_t vsalt[12];
+    uint32_t vcid;      /* cipher type id */
+    int vconf, vauth;   /* sec_serv_conf / auth in force */
+    size_t vmki;        /* MKI bytes of the stream */
 } hkey_t;
 
 typedef struct {
@@ -217,6 +226,14 @@ struct srtp_ctx_t_ {
     uint32_t *rel;          /* slots released while jobs were queued */
     size_t n_rel, rel_cap;
     int host_kdf;
+    /* routed keys by device slot (run_routed), per-packet results of the
+     * last routed run: protect status codes, unprotect's decrypted
+     * packets' original bytes (undo) */
+    hkey_t **vkeys;
+    size_t vkeys_cap;
+    uint8_t *vres;
+    uint8_t **vsave;
+    size_t vres_cap;
 };
 
 static void dev_pull(srtp_t ctx);
@@ -600,6 +617,53 @@ static void kdf_gen(const hc_aes_t *kdf, const uint8_t salt14[14],
     hc_icm_keystream(kdf, salt14, nonce, out, len);
 }
 
+/* a cipher / auth type id the application replaced: the reference then
+ * runs that id's crypto through the registered type (crypto_kernel.c:
+ * 272-348, 421-425, 445-506) */
+static int cipher_routed(srtp_cipher_type_id_t id)
+{
+    const srtp_cipher_type_t *r = srtp_mi355x_registered_cipher_type(id);
+    return r && r != srtp_mi355x_builtin_cipher_type(id);
+}
+
+static int auth_routed(srtp_auth_type_id_t id)
+{
+    const srtp_auth_type_t *r = srtp_mi355x_registered_auth_type(id);
+    return r && r != srtp_mi355x_builtin_auth_type(id);
+}
+
+/* the KDF's AES-ICM type by the KDF key length (srtp_kdf_init,
+ * srtp.c:1070-1103) */
+static srtp_cipher_type_id_t kdf_cipher_id(size_t kdf_keylen)
+{
+    return kdf_keylen == 46   ? SRTP_AES_ICM_256
+           : kdf_keylen == 38 ? SRTP_AES_ICM_192
+                              : SRTP_AES_ICM_128;
+}
+
+/* srtp_kdf_generate (srtp.c:1105-1131) through a registered AES-ICM type:
+ * key = the PRF key followed by its 14-byte salt (contiguous) */
+static int vt_kdf_gen(srtp_cipher_type_id_t id, const uint8_t *key_salt,
+                      size_t kdf_keylen, uint8_t label, uint8_t *out,
+                      size_t len)
+{
+    memset(out, 0, len);
+    if (!len)
+        return 0;
+    srtp_cipher_t *c = NULL;
+    if (srtp_cipher_type_alloc(srtp_mi355x_registered_cipher_type(id), &c,
+                               kdf_keylen, 0) || !c)
+        return -1;
+    uint8_t nonce[16] = { 0 };
+    nonce[7] = label;
+    size_t olen = len;
+    int bad = srtp_cipher_init(c, key_salt) ||
+              srtp_cipher_set_iv(c, nonce, srtp_direction_encrypt) ||
+              srtp_cipher_encrypt(c, out, len, out, &olen);
+    srtp_cipher_dealloc(c);
+    return bad ? -1 : 0;
+}
+
 static uint32_t alloc_slot(srtp_t ctx)
 {
     if (ctx->n_free)
@@ -686,12 +750,19 @@ typedef struct {
     int hmac, gcm_h, ghash;
     int tail;                 /* salt bytes salt_len, salt_len + 1 from tail */
     uint8_t tail_b[2];
+    /* routed KDF: the PRF runs through this registered AES-ICM type id
+     * (kdf_keylen = kdf_len + 14), on the host */
+    int vkdf;
+    srtp_cipher_type_id_t vkdf_id;
+    /* routed key: the derived bytes are returned here and the device
+     * record holds no key material */
+    uint8_t *raw_ek, *raw_sa, *raw_ak;
 } kspec_t;
 
 static int put_key(srtp_t ctx, uint32_t slot, srtp_dev_key_t *dk,
                    const kspec_t *q)
 {
-    if (!ctx->host_kdf) {
+    if (!ctx->host_kdf && !q->vkdf && !q->raw_ek) {
         srtp_kdf_job_t *j = kq_push(ctx);
         if (!j)
             return -1;
@@ -714,16 +785,39 @@ static int put_key(srtp_t ctx, uint32_t slot, srtp_dev_key_t *dk,
         j->slot = slot;
         return 0;
     }
-    hc_aes_t kdf;
-    hc_aes_init(&kdf, q->kk, q->kdf_len);
     uint8_t ek[32], sa[16], ak[20];
     memset(sa, 0, sizeof sa);
-    kdf_gen(&kdf, q->ks, q->lab_enc, ek, q->enc_len);
-    kdf_gen(&kdf, q->ks, q->lab_salt, sa, q->salt_len);
-    kdf_gen(&kdf, q->ks, q->lab_auth, ak, q->auth_len);
+    if (q->vkdf) {
+        const size_t kl = q->kdf_len + 14;
+        if (q->ks != q->kk + q->kdf_len ||
+            vt_kdf_gen(q->vkdf_id, q->kk, kl, q->lab_enc, ek, q->enc_len) ||
+            vt_kdf_gen(q->vkdf_id, q->kk, kl, q->lab_salt, sa, q->salt_len) ||
+            vt_kdf_gen(q->vkdf_id, q->kk, kl, q->lab_auth, ak, q->auth_len))
+            return -1;
+    } else {
+        hc_aes_t kdf;
+        hc_aes_init(&kdf, q->kk, q->kdf_len);
+        kdf_gen(&kdf, q->ks, q->lab_enc, ek, q->enc_len);
+        kdf_gen(&kdf, q->ks, q->lab_salt, sa, q->salt_len);
+        kdf_gen(&kdf, q->ks, q->lab_auth, ak, q->auth_len);
+    }
     if (q->tail) {
         sa[q->salt_len] = q->tail_b[0];
         sa[q->salt_len + 1] = q->tail_b[1];
+    }
+    if (q->raw_ek) {
+        /* routed: the registered types get the bytes; the device record
+         * stays empty (family NULL, no schedule: k_undo passes it by) */
+        memcpy(q->raw_ek, ek, q->enc_len);
+        memcpy(q->raw_sa, sa, q->salt_len);
+        memcpy(q->raw_ak, ak, q->auth_len);
+        memset(ek, 0, sizeof ek);
+        memset(ak, 0, sizeof ak);
+        srtp_dev_key_t z;
+        memset(&z, 0, sizeof z);
+        z.family = SRTP_DEV_NULL;
+        z.ghash_slot = slot;
+        return srtp_gpu_set_key(ctx->gpu, slot, &z, NULL);
     }
     for (int i = 0; i < 4; i++)
         dk->salt[i] = (uint32_t)sa[4 * i] | (uint32_t)sa[4 * i + 1] << 8 |
@@ -758,6 +852,57 @@ static int put_key(srtp_t ctx, uint32_t slot, srtp_dev_key_t *dk,
     memset(ek, 0, sizeof ek);
     memset(ak, 0, sizeof ak);
     return srtp_gpu_set_key(ctx->gpu, slot, dk, gtab);
+}
+
+static int vkeys_set(srtp_t ctx, uint32_t slot, hkey_t *hk)
+{
+    if (slot >= ctx->vkeys_cap) {
+        size_t nc = ctx->vkeys_cap ? ctx->vkeys_cap : 64;
+        while (nc <= slot)
+            nc *= 2;
+        hkey_t **v = (hkey_t **)realloc(ctx->vkeys, nc * sizeof *v);
+        if (!v)
+            return -1;
+        memset(v + ctx->vkeys_cap, 0, (nc - ctx->vkeys_cap) * sizeof *v);
+        ctx->vkeys = v;
+        ctx->vkeys_cap = nc;
+    }
+    ctx->vkeys[slot] = hk;
+    return 0;
+}
+
+/* a routed RTP key: cipher and auth objects of the registered types,
+ * allocated and keyed as srtp_stream_alloc / srtp_stream_init_keys do
+ * (srtp.c:615-641, 1378-1384, 1512-1518) */
+static int route_key(srtp_t ctx, hkey_t *hk, const srtp_crypto_policy_t *rtp,
+                     size_t base, size_t salt_len, const uint8_t *ek,
+                     const uint8_t *sa, const uint8_t *ak)
+{
+    uint8_t kb[64];
+    memcpy(kb, ek, base);
+    memcpy(kb + base, sa, salt_len);
+    if (srtp_cipher_type_alloc(srtp_mi355x_registered_cipher_type(
+                                   rtp->cipher_type),
+                               &hk->vc, rtp->cipher_key_len,
+                               rtp->auth_tag_len) ||
+        !hk->vc || srtp_cipher_init(hk->vc, kb)) {
+        memset(kb, 0, sizeof kb);
+        return -1;
+    }
+    memset(kb, 0, sizeof kb);
+    const srtp_auth_type_t *at = srtp_mi355x_registered_auth_type(rtp->auth_type);
+    if (!at || srtp_auth_type_alloc(at, &hk->va, rtp->auth_key_len,
+                                    rtp->auth_tag_len) ||
+        !hk->va || srtp_auth_init(hk->va, ak))
+        return -1;
+    memcpy(hk->vsalt, sa, 12);
+    hk->vcid = rtp->cipher_type;
+    hk->vconf = (rtp->sec_serv & sec_serv_conf) != 0 ||
+                hk->family == SRTP_DEV_GCM;
+    hk->vauth = (rtp->sec_serv & sec_serv_auth) != 0 &&
+                hk->family != SRTP_DEV_GCM;
+    hk->variant = SRTP_VARIANT_V;
+    return vkeys_set(ctx, hk->slot, hk);
 }
 
 /* srtp_stream_init_keys (srtp.c:1233-1607) for one master key: the host
@@ -795,6 +940,18 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         return srtp_err_status_init_fail;
     if (base != 0 && base != 16 && base != 24 && base != 32)
         return srtp_err_status_init_fail;
+    /* replaced types (srtp_replace_cipher_type / _auth_type): the KDF's
+     * AES-ICM and the RTP cipher / auth run through the registered vtables
+     * on the host, as the reference allocates them from its crypto kernel */
+    const int kdfr = cipher_routed(kdf_cipher_id(kdf_keylen));
+    const int gcm_rtp = rtp->cipher_type == SRTP_AES_GCM_128 ||
+                        rtp->cipher_type == SRTP_AES_GCM_256;
+    const int rtpr = cipher_routed(rtp->cipher_type) ||
+                     (!gcm_rtp && (rtp->sec_serv & sec_serv_auth) &&
+                      auth_routed(rtp->auth_type));
+    if (rtpr && ((p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0) ||
+                 p->use_cryptex))
+        return srtp_err_status_bad_param; /* not routed: refused, not faked */
 
     /* the PRF: AES keyed by the zero-padded master key, offset = the 14
      * bytes after it (srtp.c:1322-1340) */
@@ -874,6 +1031,8 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         q.kk = tmp;
         q.ks = kdf_salt;
         q.kdf_len = kdf_len;
+        q.vkdf = kdfr;
+        q.vkdf_id = kdf_cipher_id(kdf_keylen);
         q.lab_enc = 0x06; /* label_rtp_header_encryption */
         q.lab_salt = 0x07; /* label_rtp_header_salt */
         if (hk->family != SRTP_DEV_NULL) {
@@ -908,6 +1067,8 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         q.kk = tmp;
         q.ks = kdf_salt;
         q.kdf_len = kdf_len;
+        q.vkdf = kdfr;
+        q.vkdf_id = kdf_cipher_id(kdf_keylen);
         q.lab_enc = 0x00;
         q.lab_salt = 0x02;
         q.lab_auth = 0x01;
@@ -920,9 +1081,27 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         q.auth_len = q.hmac ? rtp->auth_key_len : 0;
         q.ghash = hk->family == SRTP_DEV_GCM;
         q.gcm_h = q.ghash;
+        uint8_t vek[32], vsa[16], vak[20];
+        if (rtpr) {
+            /* the salt the reference's cipher init reads: rtp_keylen - base
+             * bytes (14 AES-ICM, 12 AES-GCM; srtp.c:1353-1370) */
+            q.salt_len = salt_len < 14 ? salt_len : 14;
+            q.raw_ek = vek;
+            q.raw_sa = vsa;
+            q.raw_ak = vak;
+            memset(vsa, 0, sizeof vsa);
+        }
         srtp_dev_key_t rk = dk;
         if (put_key(ctx, hk->slot, &rk, &q))
             return srtp_err_status_init_fail;
+        if (rtpr) {
+            hk->vmki = mki_size;
+            int bad = route_key(ctx, hk, rtp, base, q.salt_len, vek, vsa, vak);
+            memset(vek, 0, sizeof vek);
+            memset(vak, 0, sizeof vak);
+            if (bad)
+                return srtp_err_status_init_fail;
+        }
     }
 
     /* SRTCP key: srtp.c:1527-1600 (labels 3 encryption, 5 salt, 4 auth).
@@ -935,7 +1114,11 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
     hk->rgcm = rtcp_gcm;
     /* srtp.c:4380-4384 picks the AEAD path from the RTP cipher: the two
      * must agree here */
-    int rtcp_gpu = rtcp_gcm == (hk->family == SRTP_DEV_GCM) &&
+    /* replaced RTCP types are not routed: srtp_protect_rtcp then reports
+     * no_such_op instead of running the built-in kernel */
+    int rtcp_gpu = !cipher_routed(rtcp->cipher_type) &&
+                   !auth_routed(rtcp->auth_type) &&
+                   rtcp_gcm == (hk->family == SRTP_DEV_GCM) &&
                    cipher_supported(rtcp) &&
                    (rtcp->auth_type == SRTP_NULL_AUTH ||
                     rtcp->auth_type == SRTP_HMAC_SHA1) &&
@@ -952,6 +1135,8 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
         q.kk = tmp;
         q.ks = kdf_salt;
         q.kdf_len = kdf_len;
+        q.vkdf = kdfr;
+        q.vkdf_id = kdf_cipher_id(kdf_keylen);
         q.lab_enc = 0x03;
         q.lab_salt = 0x05;
         q.lab_auth = 0x04;
@@ -989,6 +1174,13 @@ static void keyset_release(srtp_t ctx, keyset_t *ks)
     if (!ks || --ks->refs > 0)
         return;
     for (size_t i = 0; i < ks->n; i++) {
+        if (ks->k[i].vc)
+            srtp_cipher_dealloc(ks->k[i].vc);
+        if (ks->k[i].va)
+            srtp_auth_dealloc(ks->k[i].va);
+        if (ks->k[i].variant == SRTP_VARIANT_V &&
+            ks->k[i].slot < ctx->vkeys_cap)
+            ctx->vkeys[ks->k[i].slot] = NULL;
         release_slot(ctx, ks->k[i].slot);
         if (ks->k[i].rslot != 0xffffffffu)
             release_slot(ctx, ks->k[i].rslot);
@@ -1246,6 +1438,8 @@ static void stage_free(stage_t *st)
     memset(st, 0, sizeof *st);
 }
 
+static void routed_reset(srtp_t ctx);
+
 srtp_err_status_t srtp_dealloc(srtp_t ctx)
 {
     if (!ctx)
@@ -1265,6 +1459,10 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
     free(ctx->dt.hwin);
     free(ctx->kq);
     free(ctx->rel);
+    routed_reset(ctx);
+    free(ctx->vres);
+    free(ctx->vsave);
+    free(ctx->vkeys);
     srtp_gpu_close(ctx->gpu);
     free(ctx);
     return srtp_err_status_ok;
@@ -1983,6 +2181,222 @@ static uint32_t variants_of(const srtp_dev_meta_t *m, size_t n)
     return mask;
 }
 
+/* ------------------------------------------------------------------------
+ * routed keys (SRTP_VARIANT_V): packet crypto through the registered
+ * cipher / auth vtables, in the reference's call order
+ * ---------------------------------------------------------------------- */
+static void be32_put(uint8_t *p, uint32_t v)
+{
+    p[0] = (uint8_t)(v >> 24);
+    p[1] = (uint8_t)(v >> 16);
+    p[2] = (uint8_t)(v >> 8);
+    p[3] = (uint8_t)v;
+}
+
+/* the IV of srtp.c:2694-2717 (AES-ICM: 0^4 || SSRC || be64(idx << 16);
+ * any other non-AEAD cipher: 0^8 || be64(idx)) or srtp_calc_aead_iv
+ * (srtp.c:1925-1959: (00 00 || SSRC || ROC || SEQ) ^ salt) */
+static void vt_iv(const hkey_t *k, const uint8_t *pkt, uint32_t roc,
+                  uint8_t iv[16])
+{
+    const uint32_t seq = (uint32_t)pkt[2] << 8 | pkt[3];
+    const uint64_t idx = (uint64_t)roc << 16 | seq;
+    memset(iv, 0, 16);
+    if (k->family == SRTP_DEV_GCM) {
+        memcpy(iv + 2, pkt + 8, 4);
+        be32_put(iv + 6, roc);
+        iv[10] = (uint8_t)(seq >> 8);
+        iv[11] = (uint8_t)seq;
+        for (int j = 0; j < 12; j++)
+            iv[j] ^= k->vsalt[j];
+        return;
+    }
+    const uint64_t w = (k->vcid == SRTP_AES_ICM_128 ||
+                        k->vcid == SRTP_AES_ICM_192 ||
+                        k->vcid == SRTP_AES_ICM_256)
+                           ? idx << 16
+                           : idx;
+    if (k->vcid == SRTP_AES_ICM_128 || k->vcid == SRTP_AES_ICM_192 ||
+        k->vcid == SRTP_AES_ICM_256)
+        memcpy(iv + 4, pkt + 8, 4);
+    for (int j = 0; j < 8; j++)
+        iv[8 + j] = (uint8_t)(w >> (56 - 8 * j));
+}
+
+/* protect crypto of one packet in buf (L bytes in, room for the trailer):
+ * srtp.c:2688-2818 (ICM / null) and 2188-2264 (AEAD); 0 or a status */
+static srtp_err_status_t vt_protect(hkey_t *k, uint8_t *buf, size_t L,
+                                    size_t es, uint32_t roc)
+{
+    uint8_t iv[16];
+    vt_iv(k, buf, roc, iv);
+    if (srtp_cipher_set_iv(k->vc, iv, srtp_direction_encrypt))
+        return srtp_err_status_cipher_fail;
+    if (k->family == SRTP_DEV_GCM) {
+        size_t outlen = L - es + k->tag_len;
+        if (srtp_cipher_set_aad(k->vc, buf, es) ||
+            srtp_cipher_encrypt(k->vc, buf + es, L - es, buf + es, &outlen))
+            return srtp_err_status_cipher_fail;
+        memcpy(buf + es + outlen, k->mki, k->vmki);   /* MKI after the tag */
+        return srtp_err_status_ok;
+    }
+    if (k->vconf) {
+        size_t len = L - es;
+        if (srtp_cipher_encrypt(k->vc, buf + es, L - es, buf + es, &len))
+            return srtp_err_status_cipher_fail;
+    }
+    memcpy(buf + L, k->mki, k->vmki);
+    if (k->vauth) {
+        uint8_t rb[4];
+        be32_put(rb, roc);
+        srtp_err_status_t st;
+        if ((st = srtp_auth_start(k->va)) ||
+            (st = srtp_auth_update(k->va, buf, L)) ||
+            (st = srtp_auth_compute(k->va, rb, 4, buf + L + k->vmki)))
+            return st;
+    }
+    return srtp_err_status_ok;
+}
+
+/* unprotect crypto of one packet (srtp_len bytes, L authenticated): the
+ * tag check, then the decryption of an authenticated packet (srtp.c:
+ * 2925-3101, 2352-2420); 1 when it authenticated */
+static int vt_unprotect(hkey_t *k, uint8_t *buf, size_t srtp_len, size_t L,
+                        size_t es, uint32_t roc)
+{
+    uint8_t iv[16];
+    vt_iv(k, buf, roc, iv);
+    if (srtp_cipher_set_iv(k->vc, iv, srtp_direction_decrypt))
+        return 0;
+    if (k->family == SRTP_DEV_GCM) {
+        size_t enc = srtp_len - es - k->vmki;   /* ciphertext and tag */
+        size_t outlen = enc;
+        return !srtp_cipher_set_aad(k->vc, buf, es) &&
+               !srtp_cipher_decrypt(k->vc, buf + es, enc, buf + es, &outlen);
+    }
+    if (k->vauth) {
+        uint8_t rb[4], tag[SRTP_MAX_TAG_LEN];
+        be32_put(rb, roc);
+        if (srtp_auth_start(k->va) || srtp_auth_update(k->va, buf, L) ||
+            srtp_auth_compute(k->va, rb, 4, tag))
+            return 0;
+        /* constant time (datatypes.c:407 srtp_octet_string_equal) */
+        uint8_t d = 0;
+        for (size_t j = 0; j < k->tag_len; j++)
+            d |= tag[j] ^ buf[srtp_len - k->tag_len + j];
+        if (d)
+            return 0;
+    }
+    if (k->vconf) {
+        size_t len = L - es;
+        if (srtp_cipher_decrypt(k->vc, buf + es, L - es, buf + es, &len))
+            return 0;
+    }
+    return 1;
+}
+
+static void routed_reset(srtp_t ctx)
+{
+    for (size_t i = 0; i < ctx->vres_cap; i++) {
+        free(ctx->vsave[i]);
+        ctx->vsave[i] = NULL;
+        ctx->vres[i] = 0;
+    }
+}
+
+/* the routed packets of one crypto pass, their bytes copied from and back
+ * to the device arenas.  Protect: ctx->vres[i] = the status of a packet
+ * whose cipher / auth call failed (its output untouched).  Unprotect:
+ * auth_ok[i] = the verdict; only an authenticated packet is decrypted, its
+ * original bytes kept in ctx->vsave[i] for undo_runs. */
+static int run_routed(srtp_t ctx, int op, size_t n, const uint8_t *in,
+                      const uint64_t *in_off, uint8_t *out,
+                      const uint64_t *out_off, const srtp_dev_meta_t *h_meta,
+                      void *stream)
+{
+    size_t nv = 0;
+    for (size_t i = 0; i < n; i++)
+        if (!SRTP_META_STATUS(h_meta[i].info) &&
+            SRTP_META_VARIANT(h_meta[i].info) == SRTP_VARIANT_V)
+            nv++;
+    if (!nv)
+        return 0;
+    if (n > ctx->vres_cap) {
+        routed_reset(ctx);
+        free(ctx->vres);
+        free(ctx->vsave);
+        ctx->vres = (uint8_t *)calloc(n, 1);
+        ctx->vsave = (uint8_t **)calloc(n, sizeof(uint8_t *));
+        ctx->vres_cap = ctx->vres && ctx->vsave ? n : 0;
+        if (!ctx->vres_cap)
+            return -1;
+    }
+    uint64_t *io = (uint64_t *)malloc(n * 8), *oo = (uint64_t *)malloc(n * 8);
+    uint8_t *buf = (uint8_t *)malloc(65536 + 2 * SRTP_MAX_TRAILER_LEN);
+    int rc = -1;
+    if (!io || !oo || !buf || srtp_gpu_sync(ctx->gpu, stream) ||
+        srtp_gpu_d2h(ctx->gpu, io, in_off, n * 8, stream) ||
+        srtp_gpu_d2h(ctx->gpu, oo, out_off, n * 8, stream) ||
+        srtp_gpu_sync(ctx->gpu, stream))
+        goto out;
+    for (size_t i = 0; i < n; i++) {
+        const srtp_dev_meta_t m = h_meta[i];
+        if (SRTP_META_STATUS(m.info) ||
+            SRTP_META_VARIANT(m.info) != SRTP_VARIANT_V)
+            continue;
+        hkey_t *k = m.key < ctx->vkeys_cap ? ctx->vkeys[m.key] : NULL;
+        if (!k || m.len > 65535)
+            goto out;
+        const size_t L = m.len, es = SRTP_META_ENC_START(m.info);
+        const size_t total = L + k->vmki + k->tag_len;
+        if (op == 0) {
+            if (srtp_gpu_d2h(ctx->gpu, buf, in + io[i], L, stream) ||
+                srtp_gpu_sync(ctx->gpu, stream))
+                goto out;
+            srtp_err_status_t st = vt_protect(k, buf, L, es, m.roc);
+            ctx->vres[i] = (uint8_t)st;
+            if (!st && (srtp_gpu_h2d(ctx->gpu, out + oo[i], buf, total, stream) ||
+                        srtp_gpu_sync(ctx->gpu, stream)))
+                goto out;
+        } else {
+            if (srtp_gpu_d2h(ctx->gpu, buf, in + io[i], total, stream) ||
+                srtp_gpu_sync(ctx->gpu, stream))
+                goto out;
+            uint8_t *orig = (uint8_t *)malloc(L ? L : 1);
+            if (!orig)
+                goto out;
+            memcpy(orig, buf, L);
+            uint8_t ok = (uint8_t)vt_unprotect(k, buf, total, L, es, m.roc);
+            if (srtp_gpu_h2d(ctx->gpu, ctx->st.d_auth + i, &ok, 1, stream) ||
+                (ok && srtp_gpu_h2d(ctx->gpu, out + oo[i], buf, L, stream)) ||
+                srtp_gpu_sync(ctx->gpu, stream)) {
+                free(orig);
+                goto out;
+            }
+            free(ctx->vsave[i]);
+            ctx->vsave[i] = ok ? orig : NULL;
+            if (!ok)
+                free(orig);
+        }
+    }
+    rc = 0;
+out:
+    free(io);
+    free(oo);
+    free(buf);
+    return rc;
+}
+
+/* protect passes: statuses of routed packets whose crypto call failed */
+static void routed_status(srtp_t ctx, size_t n, srtp_err_status_t *status)
+{
+    for (size_t i = 0; i < n && i < ctx->vres_cap; i++) {
+        if (!status[i] && ctx->vres[i])
+            status[i] = (srtp_err_status_t)ctx->vres[i];
+        ctx->vres[i] = 0;
+    }
+}
+
 static int run_gpu(srtp_t ctx, int op, size_t n, const uint8_t *in,
                    const uint64_t *in_off, uint8_t *out,
                    const uint64_t *out_off, const srtp_dev_meta_t *h_meta,
@@ -1998,19 +2412,19 @@ static int run_gpu(srtp_t ctx, int op, size_t n, const uint8_t *in,
     b.meta = ctx->st.d_meta;
     b.auth_ok = ctx->st.d_auth;
     b.uniform_key = uniform_slot(h_meta, n);
-    b.mask = variants_of(h_meta, n);
+    b.mask = variants_of(h_meta, n) & ~(1u << SRTP_VARIANT_V);
     b.stream = stream;
-    if (!b.mask)
-        return 0;
-    if (srtp_gpu_h2d(ctx->gpu, ctx->st.d_meta, h_meta, n * sizeof *h_meta,
-                     stream))
-        return -1;
-    srtp_gpu_set_timing(ctx->gpu, ctx->timing);
-    if (srtp_gpu_run(ctx->gpu, op, &b))
-        return -1;
-    if (ctx->timing)
-        ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
-    return 0;
+    if (b.mask) {
+        if (srtp_gpu_h2d(ctx->gpu, ctx->st.d_meta, h_meta,
+                         n * sizeof *h_meta, stream))
+            return -1;
+        srtp_gpu_set_timing(ctx->gpu, ctx->timing);
+        if (srtp_gpu_run(ctx->gpu, op, &b))
+            return -1;
+        if (ctx->timing)
+            ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
+    }
+    return run_routed(ctx, op, n, in, in_off, out, out_off, h_meta, stream);
 }
 
 static size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -2247,6 +2661,8 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
         xrtp_protect_results(ctx, n, status, HS(ctx))) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         ret = srtp_err_status_fail;
+    } else {
+        routed_status(ctx, n, status);
     }
     for (size_t i = 0; i < n; i++) {
         if (ret) {
@@ -2263,7 +2679,8 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
 }
 
 /* XORs the keystream of each flagged packet's last run back over its
- * output (CTR: that restores the ciphertext) */
+ * output (CTR: that restores the ciphertext); routed packets get the bytes
+ * run_routed() kept */
 static int undo_runs(srtp_t ctx, size_t n, const size_t *list, size_t nl,
                      upkt_t *u, uint8_t *d_out, const uint64_t *d_out_off,
                      void *stream)
@@ -2274,8 +2691,23 @@ static int undo_runs(srtp_t ctx, size_t n, const size_t *list, size_t nl,
         sg->h_meta[i].info = 0xff0000u;
     for (size_t j = 0; j < nl; j++) {
         size_t i = list[j];
-        sg->h_meta[i] = u[i].dm;
         u[i].dirty = 0;
+        if (SRTP_META_VARIANT(u[i].dm.info) == SRTP_VARIANT_V) {
+            uint64_t o;
+            if (i < ctx->vres_cap && ctx->vsave[i] &&
+                (srtp_gpu_d2h(ctx->gpu, &o, d_out_off + i, 8, stream) ||
+                 srtp_gpu_sync(ctx->gpu, stream) ||
+                 srtp_gpu_h2d(ctx->gpu, d_out + o, ctx->vsave[i], u[i].dm.len,
+                              stream) ||
+                 srtp_gpu_sync(ctx->gpu, stream)))
+                return -1;
+            if (i < ctx->vres_cap) {
+                free(ctx->vsave[i]);
+                ctx->vsave[i] = NULL;
+            }
+            continue;
+        }
+        sg->h_meta[i] = u[i].dm;
         k++;
     }
     if (!k)
@@ -2318,6 +2750,7 @@ static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
     size_t npend = n;
     srtp_err_status_t ret = srtp_err_status_ok;
     memset(&ctx->ustat, 0, sizeof ctx->ustat);
+    routed_reset(ctx);
     for (int round = 0; npend; round++) {
         const int mode = round < 2                 ? UNP_OPTIMISTIC
                          : round < UNP_SPEC_ROUNDS ? UNP_CAUTIOUS
@@ -2380,6 +2813,8 @@ static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
                 u[i].dirty = 1;
                 u[i].dm = sg->h_meta[i];
                 u[i].xres = 0;
+                if (SRTP_META_VARIANT(sg->h_meta[i].info) == SRTP_VARIANT_V)
+                    u[i].dirty = u[i].auth; /* run_routed decrypts only then */
                 if (SRTP_META_VARIANT(sg->h_meta[i].info) == SRTP_VARIANT_X) {
                     /* k_xrtp writes only authenticated packets; an undo
                      * needs to know whether cryptex was applied */
@@ -2420,6 +2855,7 @@ static srtp_err_status_t unprotect_core(srtp_t ctx, size_t n,
         if (undo_runs(ctx, n, aux, nb, u, d_out, d_out_off, stream))
             ret = srtp_err_status_fail;
     }
+    routed_reset(ctx);
     free(u);
     free(pend);
     free(aux);
@@ -2627,8 +3063,9 @@ static int dev_build(srtp_t ctx)
         d->key = k->slot;
         d->variant = k->variant;
         d->flags = 0;
-        /* header-extension encryption / cryptex streams: host pre-pass */
-        const int xs = k->variant == SRTP_VARIANT_X;
+        /* header-extension encryption / cryptex streams and routed keys:
+         * host pre-pass */
+        const int xs = k->variant >= SRTP_VARIANT_X;
         if (!st->use_mki && st->rdbx.pending_roc == 0 && !xs &&
             st->direction != DIR_RECEIVER) {
             d->flags |= SRTP_DS_ELIGIBLE;
@@ -2867,6 +3304,7 @@ static srtp_err_status_t protect_device(srtp_t ctx,
         ret = srtp_err_status_fail;
         goto out;
     }
+    routed_status(ctx, n, status);
     ret = dev_results(ctx, b, status, olen, cap);
 out:
     free(sum);

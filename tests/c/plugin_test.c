@@ -11,6 +11,14 @@
  * srtp_aes_gcm_128 / _256 and srtp_hmac objects -- exactly what
  * srtp_replace_cipher_type checks (crypto_kernel.c:300-306).  Only data is
  * read from that library.  Exit status 0 = all checks passed.
+ *
+ * Routing (section 7): once a user type is registered for an id, sessions
+ * using that id run their packet crypto through the registered vtable, as
+ * the reference's do (srtp.c:594-752 allocates the stream's cipher / auth
+ * from the crypto kernel).  The wrappers count their calls; batches
+ * protected before and after the replacement must be bit-identical, and
+ * unprotect must round-trip, refuse a tampered packet without touching it,
+ * and refuse a replay.
  */
 #define _GNU_SOURCE
 #include <dlfcn.h>
@@ -66,9 +74,11 @@ static srtp_err_status_t u_set_iv(void *s, uint8_t *iv,
 {
     return g_icm->set_iv(s, iv, d);
 }
+static long g_cipher_calls, g_auth_calls;
 static srtp_err_status_t u_crypt(void *s, const uint8_t *src, size_t n,
                                  uint8_t *dst, size_t *dn)
 {
+    g_cipher_calls++;
     srtp_err_status_t st = g_icm->encrypt(s, src, n, dst, dn);
     if (!st && g_broken && n)
         dst[0] ^= 1;
@@ -84,6 +94,154 @@ static srtp_err_status_t ua_alloc(srtp_auth_t **a, size_t kl, size_t ol)
     if (!st)
         (*a)->type = &user_hmac;
     return st;
+}
+static srtp_err_status_t ua_compute(void *s, const uint8_t *m, size_t n,
+                                    size_t tl, uint8_t *res)
+{
+    g_auth_calls++;
+    return g_hmac->compute(s, m, n, tl, res);
+}
+
+/* ---- a user AES-GCM-256 type (AEAD: seal / open counted) ---- */
+static const srtp_cipher_type_t *g_gcm;
+static srtp_cipher_type_t user_gcm;
+static long g_gcm_calls;
+static srtp_err_status_t ug_alloc(srtp_cipher_t **c, size_t kl, size_t tl)
+{
+    srtp_err_status_t st = g_gcm->alloc(c, kl, tl);
+    if (!st)
+        (*c)->type = &user_gcm;
+    return st;
+}
+static srtp_err_status_t ug_enc(void *s, const uint8_t *src, size_t n,
+                                uint8_t *dst, size_t *dn)
+{
+    g_gcm_calls++;
+    return g_gcm->encrypt(s, src, n, dst, dn);
+}
+static srtp_err_status_t ug_dec(void *s, const uint8_t *src, size_t n,
+                                uint8_t *dst, size_t *dn)
+{
+    g_gcm_calls++;
+    return g_gcm->decrypt(s, src, n, dst, dn);
+}
+
+/* ---- one session pass: a batch protected, then unprotected in place ---- */
+enum { NB = 96, PK = 320 };
+static uint8_t g_in[NB][PK];
+static size_t g_in_len[NB];
+
+static void make_packets(void)
+{
+    uint64_t x = 0x726f757465643031ULL;
+    for (size_t i = 0; i < NB; i++) {
+        g_in_len[i] = 12 + 1 + (i * 37) % 200;
+        for (size_t j = 0; j < g_in_len[i]; j++) {
+            x ^= x << 13;
+            x ^= x >> 7;
+            x ^= x << 17;
+            g_in[i][j] = (uint8_t)x;
+        }
+        const uint16_t seq = (uint16_t)(0xffd0 + i); /* crosses the ROC */
+        g_in[i][0] = 0x80;
+        g_in[i][1] = 96;
+        g_in[i][2] = (uint8_t)(seq >> 8);
+        g_in[i][3] = (uint8_t)seq;
+        g_in[i][8] = 0xca;
+        g_in[i][9] = 0xfe;
+        g_in[i][10] = 0xba;
+        g_in[i][11] = 0xbe;
+    }
+}
+
+/* gcm: AES-GCM-256 else AES-CM-128 + HMAC-SHA1-80; mki: two master keys
+ * with 4-byte MKIs, packets alternating between them.  out / olen = the
+ * protected batch. */
+static void session_pass(int gcm, int mki, uint8_t out[][PK], size_t *olen)
+{
+    static uint8_t key[2][46], id[2][4];
+    for (int k = 0; k < 2; k++)
+        for (int j = 0; j < 46; j++)
+            key[k][j] = (uint8_t)(0x31 * j + 7 * k + 1);
+    memcpy(id[0], "\x01\x02\x03\x04", 4);
+    memcpy(id[1], "\xa0\xb0\xc0\xd0", 4);
+    srtp_master_key_t mk[2] = { { key[0], id[0] }, { key[1], id[1] } };
+    srtp_master_key_t *mkp[2] = { &mk[0], &mk[1] };
+    srtp_policy_t p;
+    memset(&p, 0, sizeof p);
+    if (gcm) {
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(&p.rtp);
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(&p.rtcp);
+    } else {
+        srtp_crypto_policy_set_rtp_default(&p.rtp);
+        srtp_crypto_policy_set_rtcp_default(&p.rtcp);
+    }
+    p.ssrc.type = ssrc_specific;
+    p.ssrc.value = 0xcafebabe;
+    if (mki) {
+        p.keys = mkp;
+        p.num_master_keys = 2;
+        p.use_mki = true;
+        p.mki_size = 4;
+    } else {
+        p.key = key[0];
+    }
+    p.window_size = 128;
+    srtp_t tx, rx;
+    CHECK(srtp_create(&tx, &p) == 0 && srtp_create(&rx, &p) == 0,
+          "create gcm=%d mki=%d", gcm, mki);
+    const uint8_t *in[NB];
+    uint8_t *op[NB];
+    size_t mi[NB];
+    srtp_err_status_t st[NB];
+    for (size_t i = 0; i < NB; i++) {
+        in[i] = g_in[i];
+        op[i] = out[i];
+        olen[i] = PK;
+        mi[i] = mki ? i & 1 : 0;
+    }
+    CHECK(srtp_protect_batch(tx, NB, in, g_in_len, op, olen, mi, st) == 0,
+          "protect batch");
+    int bad = 0;
+    for (size_t i = 0; i < NB; i++)
+        bad += st[i] != 0 || olen[i] != g_in_len[i] + (mki ? 4 : 0) +
+                                               (gcm ? 16 : 10);
+    CHECK(!bad, "protect statuses / lengths gcm=%d mki=%d: %d bad", gcm, mki,
+          bad);
+    /* receive in place; packet 5 tampered */
+    static uint8_t rxb[NB][PK];
+    uint8_t *rp[NB];
+    size_t rl[NB];
+    for (size_t i = 0; i < NB; i++) {
+        memcpy(rxb[i], out[i], olen[i]);
+        rp[i] = rxb[i];
+        rl[i] = olen[i];
+    }
+    rxb[5][20] ^= 1;
+    uint8_t tampered[PK];
+    memcpy(tampered, rxb[5], olen[5]);
+    CHECK(srtp_unprotect_batch(rx, NB, (const uint8_t *const *)rp, rl, rp, rl,
+                               st) == 0,
+          "unprotect batch");
+    bad = 0;
+    for (size_t i = 0; i < NB; i++) {
+        if (i == 5)
+            continue;
+        bad += st[i] != 0 || rl[i] != g_in_len[i] ||
+               memcmp(rxb[i], g_in[i], g_in_len[i]) != 0;
+    }
+    CHECK(!bad, "round trip gcm=%d mki=%d: %d bad", gcm, mki, bad);
+    CHECK(st[5] == srtp_err_status_auth_fail &&
+              memcmp(rxb[5], tampered, olen[5]) == 0,
+          "tampered packet refused untouched (status %d)", st[5]);
+    uint8_t again[PK];
+    size_t al = olen[7];
+    memcpy(again, out[7], olen[7]);
+    CHECK(srtp_unprotect(rx, again, al, again, &al) ==
+              srtp_err_status_replay_fail,
+          "replay refused");
+    srtp_dealloc(tx);
+    srtp_dealloc(rx);
 }
 
 static void log_cb(srtp_log_level_t level, const char *msg, void *data)
@@ -261,6 +419,14 @@ int main(int argc, char **argv)
               srtp_err_status_bad_param,
           "hmac key 21 rejected");
 
+    /* 6a. batches through the built-in types, before any replacement */
+    static uint8_t gold[3][NB][PK], got[NB][PK];
+    size_t gold_len[3][NB], got_len[NB];
+    make_packets();
+    session_pass(0, 0, gold[0], gold_len[0]);
+    session_pass(0, 1, gold[1], gold_len[1]);
+    session_pass(1, 1, gold[2], gold_len[2]);
+
     /* 6. replacement: a conforming user type is accepted and registered,
      * a broken one and a mismatched id are refused (crypto_kernel.c:270-330) */
     user_icm = *g_icm;
@@ -291,12 +457,22 @@ int main(int argc, char **argv)
           "registered");
     user_hmac = *g_hmac;
     user_hmac.alloc = ua_alloc;
+    user_hmac.compute = ua_compute;
     user_hmac.description = "user HMAC-SHA1";
     CHECK(srtp_replace_auth_type(&user_hmac, SRTP_HMAC_SHA1) ==
               srtp_err_status_ok,
           "auth replacement accepted");
     CHECK(srtp_mi355x_registered_auth_type(SRTP_HMAC_SHA1) == &user_hmac,
           "auth registered");
+    g_gcm = srtp_mi355x_builtin_cipher_type(SRTP_AES_GCM_256);
+    user_gcm = *g_gcm;
+    user_gcm.alloc = ug_alloc;
+    user_gcm.encrypt = ug_enc;
+    user_gcm.decrypt = ug_dec;
+    user_gcm.description = "user AES-256 GCM";
+    CHECK(srtp_replace_cipher_type(&user_gcm, SRTP_AES_GCM_256) ==
+              srtp_err_status_ok,
+          "gcm replacement accepted");
 
     /* 7. the packet path after replacement: srtp_validate's published
      * packet (test/srtp_driver.c:2342-2426) */
@@ -321,6 +497,36 @@ int main(int argc, char **argv)
         CHECK(srtp_octet_string_equal(b3, b1, 38), "srtp_validate KAT: %s",
               srtp_octet_string_hex_string(b3, 38));
         srtp_dealloc(s);
+    }
+
+    /* 7b. routing: the registered types do the packet crypto, and the
+     * batches come out bit-identical to the built-in ones */
+    for (int v = 0; v < 3; v++) {
+        const long c0 = g_cipher_calls, a0 = g_auth_calls, g0 = g_gcm_calls;
+        session_pass(v == 2, v > 0, got, got_len);
+        int bad = 0;
+        for (size_t i = 0; i < NB; i++)
+            bad += got_len[i] != gold_len[v][i] ||
+                   memcmp(got[i], gold[v][i], got_len[i]) != 0;
+        CHECK(!bad, "routed batch %d: %d packets differ from the built-in "
+                    "types'", v, bad);
+        const long dc = g_cipher_calls - c0, da = g_auth_calls - a0,
+                   dg = g_gcm_calls - g0;
+        /* protect NB + unprotect NB - 1 authenticated + 1 tampered (auth
+         * only) + the replay (refused before any crypto) */
+        if (v < 2)
+            CHECK(dc >= 2 * NB - 1 && da >= 2 * NB && dg == 0,
+                  "routed calls %d: cipher %ld auth %ld gcm %ld", v, dc, da,
+                  dg);
+        else
+            CHECK(dg >= 2 * NB && dc == 0 && da == 0,
+                  "routed calls %d: cipher %ld auth %ld gcm %ld", v, dc, da,
+                  dg);
+        printf("routed session %d (%s): bit-exact %s, calls cipher %ld "
+               "auth %ld gcm %ld\n",
+               v, v == 2 ? "AES-GCM-256, MKI" : v ? "AES-CM-128, MKI"
+                                                 : "AES-CM-128",
+               bad ? "NO" : "yes", dc, da, dg);
     }
 
     /* 8. the utilities */
