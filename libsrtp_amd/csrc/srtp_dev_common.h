@@ -588,20 +588,67 @@ DEV u32x4 GhTab<true>::get(uint32_t w, int k) const
     return *(const u32x4 *)(lds + a);
 }
 
-// The 8-copy Shoup table (32 KiB after the four AES tables, 160 KiB in
-// all): entry b of copy c at base + b * 128 + c * 16, c = lane & 7 (two
-// lanes of a ds_read_b128 group share a copy: a 2-way conflict when their
-// entries have the same parity).  The entry offset is a shift of the word
-// plus one full-rate v_bitop3 with the lane template (base | c * 16).
-struct GhTab8 {
+// multiplies a GHASH value by x^8: the byte shifted out of word 3 (x^128..
+// x^135) is folded back by x^128 = 1 + x + x^2 + x^7 (as in ghash_mul)
+DEV u32x4 ghash_mulx8(u32x4 z)
+{
+    const uint32_t o = z.w << 24;
+    u32x4 r;
+    r.w = __builtin_amdgcn_alignbit(z.z, z.w, 8);
+    r.z = __builtin_amdgcn_alignbit(z.y, z.z, 8);
+    r.y = __builtin_amdgcn_alignbit(z.x, z.y, 8);
+    r.x = xor3(xor3(z.x >> 8, o, o >> 1), o >> 2, o >> 7);
+    return r;
+}
+
+// Per-position tables for uniform-key GHASH (32 KiB after the four AES
+// tables, 160 KiB in all): table t holds M_t[b] = M[b] * x^(8t), t = 0..7
+// (M = Shoup's table, byte position 0), entry b of table t at base +
+// (b * 8 + t) * 16.  X * H is then
+//   sum over bytes 0..7 of M_k[X_k]  +  x^64 * sum over bytes 8..15 of
+//   M_(k-8)[X_k]
+// -- 16 lookups and XORs, one multiply by x^64 (a 64-bit fold), instead of
+// Shoup's 16 shift-and-reduce steps.  Bank spread: lane L walks the bytes
+// of each half in the order s ^ r, r = L & 7 (its X halves are byte-permuted
+// once per multiply), so the 16 lanes of a ds_read_b128 group read 8
+// different tables at every step; two lanes share a table and conflict only
+// when their entries have the same parity.
+struct GhPos8 {
     const char *lds;   // LDS base (address 0)
-    uint32_t tmpl;     // table base | (lane & 7) * 16
-    DEV u32x4 get(uint32_t w, int k) const
+    uint32_t tmpl0;    // table base | (r << 4): the table of step 0
+    uint32_t sel;      // v_perm selector: LE byte i <- byte i ^ (r & 3)
+    uint32_t swap;     // r & 4: swap the two words of a half
+    DEV void init(const char *l, uint32_t base, uint32_t lane)
     {
-        // byte k of BE word w (k = 0 the most significant) -> bits 14:7
-        const uint32_t s = k == 3 ? (w << 7) : (w >> (17 - 8 * k));
-        return *(const u32x4 *)(lds + __builtin_amdgcn_bitop3_b32(
-                                          s, 0x7f80u, tmpl, 0xEA));
+        const uint32_t r = lane & 7, q = r & 3;
+        lds = l;
+        tmpl0 = base | (r << 4);
+        sel = (0u ^ q) | ((1u ^ q) << 8) | ((2u ^ q) << 16) | ((3u ^ q) << 24);
+        swap = r & 4;
+    }
+    // the 8 lookups of one half (words a, b = bytes 0..3, 4..7) into acc
+    DEV void half(uint32_t a, uint32_t b, u32x4 &acc) const
+    {
+        a = __builtin_amdgcn_perm(0u, a, sel);
+        b = __builtin_amdgcn_perm(0u, b, sel);
+        const uint32_t w0 = swap ? b : a, w1 = swap ? a : b;
+        u32x4 e[8];
+#pragma unroll
+        for (int st = 0; st < 8; st++) {
+            const uint32_t w = st < 4 ? w0 : w1;
+            const int k = st & 3;   // BE byte of w
+            const uint32_t f = k == 3 ? (w << 7) : (w >> (17 - 8 * k));
+            e[st] = *(const u32x4 *)(lds + __builtin_amdgcn_bitop3_b32(
+                                               f, 0x7f80u,
+                                               tmpl0 ^ ((uint32_t)st << 4), 0xEA));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t t0 = xor3(e[0][u], e[1][u], e[2][u]);
+            const uint32_t t1 = xor3(e[3][u], e[4][u], e[5][u]);
+            const uint32_t t2 = xor3(e[6][u], e[7][u], acc[u]);
+            acc[u] = xor3(t0, t1, t2);
+        }
     }
 };
 
@@ -646,6 +693,23 @@ DEV void ghash_mul(uint32_t x[4], const TAB &T)
     x[1] = z.y;
     x[2] = z.z;
     x[3] = z.w;
+}
+
+DEV void ghash_mul(uint32_t x[4], const GhPos8 &T)
+{
+    u32x4 lo = { 0, 0, 0, 0 }, hi = { 0, 0, 0, 0 };
+    T.half(x[0], x[1], lo);
+    T.half(x[2], x[3], hi);
+    // hi * x^64: words move down two places; the 64 bits leaving word 3
+    // (x^128..x^191, O = hi.z:hi.w at x^0..x^63) fold back as
+    // O * (1 + x + x^2 + x^7), which stays below x^71
+    const uint32_t a = hi.z, b = hi.w;
+    x[0] = xor3(xor3(lo.x, a, a >> 1), a >> 2, a >> 7);
+    x[1] = xor3(xor3(lo.y, b, __builtin_amdgcn_alignbit(a, b, 1)),
+                __builtin_amdgcn_alignbit(a, b, 2),
+                __builtin_amdgcn_alignbit(a, b, 7));
+    x[2] = xor3(xor3(lo.z, hi.x, b << 31), b << 30, b << 25);
+    x[3] = lo.w ^ hi.y;
 }
 
 struct GlobalKey {

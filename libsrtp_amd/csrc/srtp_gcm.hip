@@ -17,8 +17,9 @@ namespace {
 #ifndef GCM_PF
 #define GCM_PF 2   // 64-byte payload chunks loaded ahead of their use
 #endif
-// uniform-key batches: the four AES tables (128 KiB) with an 8-copy GHASH
-// table (32 KiB), instead of (T0, T1) with a 16-copy GHASH table
+// uniform-key batches: the four AES tables (128 KiB) with 8 per-position
+// GHASH tables (32 KiB, GhPos8), instead of (T0, T1) with a 16-copy Shoup
+// table
 #ifndef GCM_TAB4
 #define GCM_TAB4 1
 #endif
@@ -213,7 +214,7 @@ template <int NR, bool PROTECT, bool UNIFORM>
 __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 {
     constexpr bool TAB4 = UNIFORM && GCM_TAB4;
-    constexpr int GH8 = 256 * 16 * 8;   // the 8-copy GHASH table
+    constexpr int GH8 = 256 * 16 * 8;   // the per-position GHASH tables
     __shared__ u32x4 s_tab[(TAB4 ? AES_TAB4_BYTES + GH8
                                  : AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) /
                            16];
@@ -227,8 +228,15 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
         const u32x4 *src =
             (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
         u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB4_BYTES);
-        for (int e = threadIdx.x; e < 256 * 8; e += blockDim.x)
-            dst[e] = src[e >> 3];
+        // per-position tables: entry b of table t = M[b] * x^(8t)
+        for (int b = threadIdx.x; b < 256; b += blockDim.x) {
+            u32x4 z = src[b];
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                dst[b * 8 + t] = z;
+                z = ghash_mulx8(z);
+            }
+        }
     } else {
     load_aes_tables<false>(s_tab);
     }
@@ -248,9 +256,8 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
         rk.load(A.keys + A.uni);
     const uint32_t stride = gridDim.x * blockDim.x;
     if constexpr (TAB4) {
-        GhTab8 G;
-        G.lds = lds;
-        G.tmpl = (uint32_t)AES_TAB4_BYTES | ((threadIdx.x & 7) * 16);
+        GhPos8 G;
+        G.init(lds, (uint32_t)AES_TAB4_BYTES, threadIdx.x);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
              i += stride)
             gcm_packet<NR, PROTECT, UNIFORM, true>(A, i, T, G, rk);
