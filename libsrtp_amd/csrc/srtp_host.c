@@ -599,14 +599,22 @@ static int auth_supported(const srtp_crypto_policy_t *c)
 {
     if (c->auth_type == SRTP_HMAC_SHA1)
         return c->auth_key_len <= 20 && c->auth_tag_len <= 20; /* hmac.c:76 */
-    if (c->auth_type == SRTP_NULL_AUTH) {
-        /* a null auth with a non-zero tag turns into libsrtp's legacy
-         * keystream-prefix mode (srtp.c:2729-2741); not supported here */
-        bool aead = c->cipher_type == SRTP_AES_GCM_128 ||
-                    c->cipher_type == SRTP_AES_GCM_256;
-        return aead || c->auth_tag_len == 0 || !(c->sec_serv & sec_serv_auth);
-    }
+    if (c->auth_type == SRTP_NULL_AUTH) /* a tag: prefix_mode() */
+        return c->auth_tag_len <= SRTP_MAX_TAG_LEN;
     return 0;
+}
+
+/* libsrtp's legacy keystream-prefix mode: a null auth with a non-zero tag
+ * and the auth service on (null_auth.c:80 prefix_len = out_len); the tag is
+ * the first tag_len keystream bytes of the packet and the payload takes the
+ * keystream after them (srtp.c:2729-2741, 3006-3020).  Such RTP sessions run
+ * through the routed path (run_routed), not the kernels. */
+static int prefix_mode(const srtp_crypto_policy_t *c)
+{
+    return c->auth_type == SRTP_NULL_AUTH && c->auth_tag_len > 0 &&
+           (c->sec_serv & sec_serv_auth) &&
+           c->cipher_type != SRTP_AES_GCM_128 &&
+           c->cipher_type != SRTP_AES_GCM_256;
 }
 
 static void kdf_gen(const hc_aes_t *kdf, const uint8_t salt14[14],
@@ -948,7 +956,8 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
                         rtp->cipher_type == SRTP_AES_GCM_256;
     const int rtpr = cipher_routed(rtp->cipher_type) ||
                      (!gcm_rtp && (rtp->sec_serv & sec_serv_auth) &&
-                      auth_routed(rtp->auth_type));
+                      auth_routed(rtp->auth_type)) ||
+                     prefix_mode(rtp);
     if (rtpr && ((p->enc_xtn_hdr && p->enc_xtn_hdr_count > 0) ||
                  p->use_cryptex))
         return srtp_err_status_bad_param; /* not routed: refused, not faked */
@@ -1117,7 +1126,7 @@ static srtp_err_status_t init_key(srtp_t ctx, hkey_t *hk,
     /* replaced RTCP types are not routed: srtp_protect_rtcp then reports
      * no_such_op instead of running the built-in kernel */
     int rtcp_gpu = !cipher_routed(rtcp->cipher_type) &&
-                   !auth_routed(rtcp->auth_type) &&
+                   !auth_routed(rtcp->auth_type) && !prefix_mode(rtcp) &&
                    rtcp_gcm == (hk->family == SRTP_DEV_GCM) &&
                    cipher_supported(rtcp) &&
                    (rtcp->auth_type == SRTP_NULL_AUTH ||
@@ -2240,6 +2249,11 @@ static srtp_err_status_t vt_protect(hkey_t *k, uint8_t *buf, size_t L,
         memcpy(buf + es + outlen, k->mki, k->vmki);   /* MKI after the tag */
         return srtp_err_status_ok;
     }
+    /* keystream prefix (srtp.c:2729-2741): into the tag, before the
+     * payload's keystream */
+    size_t pl = k->vauth ? srtp_auth_get_prefix_length(k->va) : 0;
+    if (pl && srtp_cipher_output(k->vc, buf + L + k->vmki, &pl))
+        return srtp_err_status_cipher_fail;
     if (k->vconf) {
         size_t len = L - es;
         if (srtp_cipher_encrypt(k->vc, buf + es, L - es, buf + es, &len))
@@ -2277,6 +2291,10 @@ static int vt_unprotect(hkey_t *k, uint8_t *buf, size_t srtp_len, size_t L,
     if (k->vauth) {
         uint8_t rb[4], tag[SRTP_MAX_TAG_LEN];
         be32_put(rb, roc);
+        /* keystream prefix (srtp.c:3006-3020): the expected tag */
+        size_t pl = srtp_auth_get_prefix_length(k->va);
+        if (pl && srtp_cipher_output(k->vc, tag, &pl))
+            return 0;
         if (srtp_auth_start(k->va) || srtp_auth_update(k->va, buf, L) ||
             srtp_auth_compute(k->va, rb, 4, tag))
             return 0;

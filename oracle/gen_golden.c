@@ -590,6 +590,27 @@ static void set_gcm_256_8(srtp_crypto_policy_t *p)
     p->auth_tag_len = 8;
 }
 
+/* the legacy keystream-prefix mode (srtp.c:2729-2741, 3006-3020): null
+ * auth with a non-zero tag and the auth service on; the "tag" is the first
+ * tag_len bytes of the packet's keystream, the payload takes the rest */
+static void set_icm128_prefix(srtp_crypto_policy_t *p)
+{
+    srtp_crypto_policy_set_aes_cm_128_null_auth(p);
+    p->sec_serv = sec_serv_conf_and_auth;
+}
+
+static void set_icm256_prefix(srtp_crypto_policy_t *p)
+{
+    srtp_crypto_policy_set_aes_cm_256_null_auth(p);
+    p->sec_serv = sec_serv_conf_and_auth;
+}
+
+static void set_null_prefix(srtp_crypto_policy_t *p)
+{
+    srtp_crypto_policy_set_null_cipher_hmac_null(p);
+    p->sec_serv = sec_serv_auth;
+}
+
 
 /* ---------------------------------------------------------------------- */
 /* Published packet KATs of test/srtp_driver.c.  The reference build must
@@ -965,6 +986,27 @@ int main(int argc, char **argv)
     }
     g_out = fopen(argv[1], "w");
     fputs("{\n", g_out);
+#ifdef PREFIX_CASES
+    /* tests/golden/ref_prefix.json: keystream-prefix sessions only */
+    {
+        static const policy_desc_t pcases[] = {
+            { "prefix_icm128_tag4", set_icm128_prefix, 4, 1, 0, 128, 0,
+              ssrc_specific, ssrc_specific },
+            { "prefix_icm128_tag10", set_icm128_prefix, 10, 1, 0, 128, 0,
+              ssrc_specific, ssrc_specific },
+            { "prefix_icm256_tag7_mki", set_icm256_prefix, 7, 2, 4, 128, 0,
+              ssrc_specific, ssrc_specific },
+            { "prefix_null_tag4", set_null_prefix, 4, 1, 0, 64, 0,
+              ssrc_specific, ssrc_specific },
+        };
+        fputs("  \"backend\": \"internal\",\n  \"cases\": [\n", g_out);
+        for (size_t i = 0; i < sizeof pcases / sizeof pcases[0]; i++)
+            gen_case(&pcases[i], i == 0);
+        fputs("\n  ]\n}\n", g_out);
+        fclose(g_out);
+        return 0;
+    }
+#endif
 #ifndef REF_OSSL
     fputs("  \"backend\": \"internal\",\n", g_out);
     gen_aes();

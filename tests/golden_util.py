@@ -27,6 +27,14 @@ def case_ids():
     return [c["name"] for c in all_cases()]
 
 
+def prefix_cases():
+    """Keystream-prefix sessions (null auth with a tag, srtp.c:2729-2741)
+    from oracle/gen_golden.c -DPREFIX_CASES; the oracle does not restate
+    this legacy mode, so these rows pin the library to the reference
+    directly."""
+    return load("ref_prefix.json")["cases"]
+
+
 def kat_cases():
     """The published packet KATs of test/srtp_driver.c (srtp_validate*,
     srtp_test_empty_payload*), reproduced by the reference build before
@@ -55,3 +63,31 @@ def replay_ops(case, snd, rcv):
         assert st == op["status"], (case["name"], i, kind, st, op["status"])
         if st == 0:
             assert out.hex() == op["out"], (case["name"], i, kind)
+
+
+def replay_ops_batched(case, snd, rcv):
+    """Like replay_ops, but consecutive RTP ops of one session and direction
+    go through ONE protect_batch / unprotect_batch call."""
+    H = bytes.fromhex
+    sess = {"snd": snd, "rcv": rcv}
+    ops = case["ops"]
+    i = 0
+    while i < len(ops):
+        j = i
+        while (j < len(ops) and ops[j]["sess"] == ops[i]["sess"]
+               and ops[j]["op"] == ops[i]["op"]):
+            j += 1
+        grp = ops[i:j]
+        s = sess[ops[i]["sess"]]
+        pk = [H(o["in"]) for o in grp]
+        caps = [o["cap"] for o in grp]
+        if ops[i]["op"] == "protect":
+            st, out = s.protect_batch(pk, caps, [o["mki_index"] for o in grp])
+        else:
+            st, out = s.unprotect_batch(pk, caps)
+        for k, o in enumerate(grp):
+            assert st[k] == o["status"], (case["name"], i + k, o["op"], st[k],
+                                          o["status"])
+            if st[k] == 0:
+                assert out[k].hex() == o["out"], (case["name"], i + k, o["op"])
+        i = j

@@ -2,7 +2,7 @@
 # Two rocprofv3 PMC passes (SQ issue/occupancy counters + clock) over the
 # protect kernel of each exp_build/<name> variant (tools/time_variants.py
 # --one NAME, run in-process), reduced on the box by pmc_reduce.py.
-# usage (on the GPU box): tools/pmc_variants.sh <outdir> name [name...]
+# usage (on the GPU box): [CFG=gcm256] tools/pmc_variants.sh <outdir> name [name...]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=$1; shift
 export TMPDIR=/tmp
@@ -18,7 +18,7 @@ for name in "$@"; do
     d="$out/$name/p$i"; mkdir -p "$out/$name"
     echo "[pmc] $name pass $i"
     timeout -k 10 180 rocprofv3 --kernel-trace --pmc $p --output-format csv -d "$d" -o p \
-        -- python3 tools/time_variants.py --one $name > "$d.log" 2>&1
+        -- python3 tools/time_variants.py --one $name ${CFG:-icm128} > "$d.log" 2>&1
     rc=$?
     echo "[pmc] $name pass $i rc=$rc $(tail -1 $d.log)"
     if [ $rc -ne 0 ]; then tail -5 "$d.log"; exit $rc; fi
