@@ -880,8 +880,14 @@ __global__ void k_pu_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
 // then all of its header loads in flight (256 tiles for 2^20 packets: one
 // round of workgroups on the 256 CUs); the commit kernel uses 256-thread
 // blocks
-constexpr int CH_THREADS = 1024;
-constexpr int CH_ITEMS = 4;
+#ifndef CH_THREADS_N
+#define CH_THREADS_N 1024
+#endif
+#ifndef CH_ITEMS_N
+#define CH_ITEMS_N 4
+#endif
+constexpr int CH_THREADS = CH_THREADS_N;
+constexpr int CH_ITEMS = CH_ITEMS_N;
 constexpr int CH_TILE = CH_THREADS * CH_ITEMS;
 constexpr int CH_COMMIT_THREADS = 256;
 // look-back word: [63:62] 1 = tile aggregate, 2 = inclusive prefix; [61] a
