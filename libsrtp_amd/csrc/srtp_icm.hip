@@ -547,22 +547,28 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
     }
 }
 
-// KM_UNI / KM_WAVE: all four T-tables (128 KiB of LDS, one 512-lane
-// workgroup per CU), the AES schedule in SGPRs.  KM_LANE: (T0, T1) only,
-// two 512-lane workgroups per CU, the schedule in VGPRs.  Persistent: the
-// grid is sized to the CUs and each workgroup walks the batch, so the
-// tables are loaded once per CU.
+// All four T-tables (128 KiB of LDS, one 512-lane workgroup per CU).  The
+// AES schedule sits in SGPRs (KM_UNI / KM_WAVE) or VGPRs (KM_LANE).  With
+// per-lane keys the kernel needs 230-256 VGPRs, so two waves per SIMD is
+// all a CU holds whatever the table size: (T0, T1) + rotations (64 KiB)
+// bought no occupancy and cost 8 VALU per round (configs[3] kernel 2.31 ->
+// 2.24 ms with four tables, MI355X A/B).  Persistent: the grid is sized to
+// the CUs and each workgroup walks the batch, so the tables are loaded once
+// per CU.
 constexpr int ICM_THREADS_UNI = 512;
-constexpr int ICM_THREADS_LANE = 512;
+#ifndef ICM_LANE_THREADS
+#define ICM_LANE_THREADS 512
+#endif
+constexpr int ICM_THREADS_LANE = ICM_LANE_THREADS;
 constexpr uint32_t ICM_SKIP = 0xffffffffu;
 
 template <int NR, bool AUTH, bool PROTECT, int KM>
 __global__ __launch_bounds__(KM == KM_LANE ? ICM_THREADS_LANE : ICM_THREADS_UNI)
 void k_icm_hmac(IcmArgs A)
 {
-    constexpr bool TAB4 = KM != KM_LANE;
+    constexpr bool TAB4 = true;
     constexpr int NRK = NR ? NR : 1;
-    constexpr int LDSB = NR ? (TAB4 ? AES_TAB4_BYTES : AES_TAB2_BYTES) : 16;
+    constexpr int LDSB = NR ? AES_TAB4_BYTES : 16;
     __shared__ u32x4 s_tab[LDSB / 16];
     __shared__ uint32_t s_t0[256];   // the S-box row during the table build
     if (A.abort && *A.abort)
@@ -631,11 +637,10 @@ void k_icm_hmac(IcmArgs A)
 template <int NR, int KM, bool AU, bool PR>
 static void icm_go(const IcmArgs &A, int ncu, hipStream_t st)
 {
-    // persistent grid: one workgroup per CU (128 KiB of tables) for SGPR
-    // keys, two 512-lane workgroups per CU for per-lane keys
+    // persistent grid: one workgroup per CU (128 KiB of tables)
     const size_t T = KM == KM_LANE ? ICM_THREADS_LANE : ICM_THREADS_UNI;
     size_t wgs = A.rec ? (size_t)-1 : (A.n + T - 1) / T;
-    const size_t cap = (size_t)ncu * (KM == KM_LANE ? 2 : 1);
+    const size_t cap = (size_t)ncu;
     if (wgs > cap)
         wgs = cap;
     hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM>), dim3((unsigned)wgs),
