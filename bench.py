@@ -120,6 +120,12 @@ def parse():
     return ap.parse_args()
 
 
+def note(msg):
+    """progress on stderr (stdout carries only the JSON line): a GPU box
+    takes a run that writes nothing for minutes to be hung"""
+    print("bench: " + msg, file=sys.stderr, flush=True)
+
+
 def pmc_counter(path, kernel_substr, counter):
     """mean per-dispatch value of one rocprofv3 --pmc counter of the
     kernels whose name contains kernel_substr, from counter_collection.csv"""
@@ -159,6 +165,7 @@ def measure_pmc(a, kname):
     base = tempfile.mkdtemp(prefix="srtp_pmc_", dir="/tmp")
     got = {}
     for k, ctrs in enumerate(PMC_PASSES):
+        note("PMC pass %d/%d: %s" % (k + 1, len(PMC_PASSES), " ".join(ctrs)))
         d = os.path.join(base, "p%d" % k)
         cmd = [prof, "--pmc"] + list(ctrs) + [
                "--output-format", "csv", "-d", d, "-o",
@@ -169,8 +176,8 @@ def measure_pmc(a, kname):
         if a.packets:
             cmd += ["--packets", str(a.packets)]
         try:
-            subprocess.run(cmd, stdout=subprocess.DEVNULL,
-                           stderr=subprocess.DEVNULL, timeout=150,
+            # the child's stderr (its progress notes) stays visible
+            subprocess.run(cmd, stdout=subprocess.DEVNULL, timeout=150,
                            env=dict(os.environ, TMPDIR="/tmp"))
         except subprocess.TimeoutExpired:
             break
@@ -249,6 +256,45 @@ def timed_steps(step, steps, warmup, world, sync=None):
 HOST_SHARE = 16
 
 
+def _bounded(fn, *args, limit=120):
+    """bench.<fn>(*args) in a child process with a time limit (the parent
+    has initialised the GPU, so the child is a fresh interpreter, not a
+    fork); None when it fails or runs past the limit"""
+    import subprocess
+    code = ("import json, sys; sys.path.insert(0, %r); import bench; "
+            "print(json.dumps(bench.%s(*json.loads(sys.argv[1]))))"
+            % (ROOT, fn))
+    try:
+        r = subprocess.run([sys.executable, "-c", code, json.dumps(args)],
+                           capture_output=True, text=True, timeout=limit)
+        return tuple(json.loads(r.stdout.strip().splitlines()[-1]))
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        note("cpu baseline %s%r: no result within %d s" % (fn, args, limit))
+        return None
+
+
+def cgroup_cpus():
+    """the cgroup CPU quota in whole CPUs (cgroup v2 cpu.max or v1
+    cfs_quota_us / cfs_period_us), None when there is none"""
+    import math
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+        if q != "max":
+            return max(1, math.ceil(int(q) / int(p)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            p = int(f.read())
+        return max(1, math.ceil(q / p)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
 def _ref_rate(lib_path, op, payload, gcm, threads, seconds):
     """packets/s of the reference build at lib_path: calibrate on one thread,
     then ~`seconds` of work on `threads` threads (sized for HOST_SHARE
@@ -265,10 +311,11 @@ def _ref_rate(lib_path, op, payload, gcm, threads, seconds):
     return done / secs.value, done
 
 
-def _ref_rate_streams(lib_path, payload, nstreams, threads, cycles=2):
+def _ref_rate_streams(lib_path, payload, nstreams, threads, cycles=1):
     """the reference with nstreams specific-SSRC streams per srtp_t, packets
     round-robin (BASELINE configs[3]; every srtp_protect() scans the
-    reference's stream list): `cycles` passes over the streams per thread"""
+    reference's stream list): `cycles` passes over the streams per thread
+    (one pass of 65,536 packets per thread takes ~10-30 s of linear scans)"""
     L = C.CDLL(lib_path)
     fn = L.ref_bench_streams
     fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
@@ -297,16 +344,30 @@ def cpu_baseline(cfg, op, payload, seconds):
     ossl = os.path.join(ref, "bench_ref_ossl.so")
     intk = os.path.join(ref, "bench_ref_int.so")
     affinity = len(os.sched_getaffinity(0))
-    threads = max(1, min(256, affinity))
+    quota = cgroup_cpus()
+    # the CPUs this process can actually use: its affinity mask, capped by
+    # its cgroup's CPU quota (the one-GPU box shows the whole host's 256
+    # CPUs in the mask and grants a 16-CPU quota; 256 threads on that quota
+    # collapse OpenSSL 3 into lock contention)
+    threads = max(1, min(256, affinity, quota or affinity))
     call = "srtp_%s()" % op
     res, res16 = {}, {}
     for k, path in (("ossl", ossl), ("int", intk)):
         if not os.path.exists(path) or (k == "int" and gcm):
             continue
-        res[k] = _ref_rate(path, op, payload, gcm, threads, seconds)
-        res16[k] = _ref_rate(path, op, payload, gcm, 16, seconds / 2) \
-            if threads != 16 else res[k]
-    if not res:
+        note("cpu baseline %s, %d threads" % (k, threads))
+        r = _bounded("_ref_rate", path, op, payload, gcm, threads, seconds)
+        if threads != 16:
+            note("cpu baseline %s, 16 threads" % k)
+            r16 = _bounded("_ref_rate", path, op, payload, gcm, 16,
+                           seconds / 2)
+        else:
+            r16 = r
+        if r:
+            res[k] = r
+        if r16:
+            res16[k] = r16
+    if not res or not res16:
         return None
     # `value` is the faster backend (the stronger baseline: OpenSSL wins on
     # large payloads, the built-in kernel on small ones, where OpenSSL's
@@ -331,6 +392,7 @@ def cpu_baseline(cfg, op, payload, seconds):
            "value_affinity": rate, "threads_affinity": threads,
            "value_16": res16[k16][0],
            "host_cpus": os.cpu_count(), "affinity_cpus": affinity,
+           "cgroup_cpus": quota,
            "backends": {"openssl": res["ossl"][0] if "ossl" in res else None,
                         "internal_kernel": res["int"][0] if "int" in res
                         else None}}
@@ -340,7 +402,9 @@ def cpu_baseline(cfg, op, payload, seconds):
         ms = {}
         th = min(threads, HOST_SHARE)   # 65,536 stream contexts per thread
         for k, path in (("ossl", ossl), ("int", intk)):
-            r = _ref_rate_streams(path, payload, STREAMS[cfg], th) \
+            note("cpu baseline %s, %d streams per srtp_t, %d threads"
+                 % (k, STREAMS[cfg], th))
+            r = _bounded("_ref_rate_streams", path, payload, STREAMS[cfg], th) \
                 if os.path.exists(path) else None
             if r:
                 ms[k] = r
@@ -525,8 +589,10 @@ def run_gpu(a, world, rank, local, json_out):
         policies = [dict(pol, ssrc_type=1, ssrc=base + k, window_size=128,
                          allow_repeat_tx=0, keys=[key])
                     for k, key in enumerate(keys)]
+    note("session: %d streams (GPU KDF)" % len(policies))
     sess = L.Session(policies)
 
+    note("building %d batches of %d packets in HBM" % (a.warmup + a.steps, n))
     # packet arenas in HBM, one per step: slot = roundup16(rtp_len + tag)
     rtp_len = 12 + payload
     slot = (rtp_len + tag + 15) & ~15
@@ -615,8 +681,10 @@ def run_gpu(a, world, rank, local, json_out):
         return None if pipelined else sess.last_kernel_ms()
 
     dev_b0, host_b0 = sess.prepass_stats()
+    note("%d warmup + %d timed steps" % (a.warmup, a.steps))
     dt, kms = timed_steps(step, a.steps, a.warmup, world,
                           sync=torch.cuda.synchronize)
+    note("timed steps done: %.3f ms per step" % (dt * 1e3 / a.steps))
     if pipelined:
         # the warmup launches, synchronous with timing on; the first one
         # also pays the cold start, so it is left out when there are more
