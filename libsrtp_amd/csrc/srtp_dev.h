@@ -32,18 +32,22 @@ enum {
 enum { SRTP_XF_XTN = 1, SRTP_XF_CRYPTEX = 2,
        SRTP_XF_CONF = 4 /* the stream's RTP services include confidentiality */ };
 
+/* The words a packet reads come first: with an AES-128 schedule the whole
+ * per-packet part of a record is its first 256 bytes (two 128-byte cache
+ * lines), which per-lane-key batches gather once per packet. */
 typedef struct srtp_dev_key {
-    uint32_t rk[60];    /* AES round keys, little-endian words of the bytes */
     uint32_t salt[4];   /* ICM: 14-byte salt || 00 00; GCM: 12-byte salt   */
     uint32_t ipad[5];   /* SHA-1 state after (K ^ ipad)                      */
     uint32_t opad[5];   /* SHA-1 state after (K ^ opad)                      */
-    uint32_t rounds;    /* 10 / 12 / 14, 0 for the null cipher              */
-    uint32_t family;    /* SRTP_DEV_*                                        */
-    uint32_t auth;      /* 1 = HMAC-SHA1 computed, 0 = none                  */
     uint32_t tag_len;   /* bytes of tag on the wire                          */
     uint32_t mki_size;  /* bytes of MKI on the wire (0 if not used)          */
     uint32_t conf;      /* 1 = payload encrypted (sec_serv_conf)             */
     uint32_t ghash_slot;/* index into the GHASH table arena (GCM only)       */
+    uint32_t rounds;    /* 10 / 12 / 14, 0 for the null cipher              */
+    uint32_t family;    /* SRTP_DEV_*                                        */
+    uint32_t rk[60];    /* AES round keys, little-endian words of the bytes
+                           (byte offset 80: 16-byte aligned)                 */
+    uint32_t auth;      /* 1 = HMAC-SHA1 computed, 0 = none                  */
     uint32_t xslot;     /* slot of the header-extension ICM key (SRTP_XF_XTN) */
     uint32_t h[4];      /* GCM hash subkey E_K(0^128), big-endian words      */
     uint8_t mki[128];
@@ -51,6 +55,13 @@ typedef struct srtp_dev_key {
     uint32_t xflags;    /* SRTP_XF_*                                         */
     uint32_t pad1;
 } srtp_dev_key_t;
+#ifdef __cplusplus
+static_assert(sizeof(srtp_dev_key_t) == 512, "one 512-byte key slot");
+static_assert(offsetof(srtp_dev_key_t, rk) == 80, "rk 16-byte aligned");
+#else
+_Static_assert(sizeof(srtp_dev_key_t) == 512, "one 512-byte key slot");
+_Static_assert(offsetof(srtp_dev_key_t, rk) == 80, "rk 16-byte aligned");
+#endif
 
 /* per-packet work descriptor written by the pre-pass */
 typedef struct srtp_dev_meta {

@@ -11,8 +11,9 @@
 //    ds_read_b32 wave instruction is conflict-free for ANY byte values.
 //    The LDS address of a lookup is formed by ONE v_perm_b32 (byte k of the
 //    state word -> bits 15:8, the lane's copy offset -> bits 7:0).
-//  * GHASH (GCM) uses Shoup's 8-bit table M[b] = b*H, 16 B per entry, in LDS
-//    replicated 16 times (ds_read_b128 lane groups are 16 lanes).
+//  * GHASH (GCM) uses Shoup's 8-bit table M[b] = b*H, 16 B per entry: for
+//    uniform keys as 8 per-position tables M[b]*x^(8t) in LDS (GhPos8), for
+//    per-lane keys each key's table in global memory (GhGlobal).
 //  * v_bitop3_b32 (gfx950) gives 3-input XOR and majority in one op.
 #pragma once
 
@@ -59,7 +60,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 //                 T2/T3 are rotations: xor3(T0,T1,rk) ^ rotl16(T0' ^ T1')
 constexpr int AES_TAB2_BYTES = 256 * 32 * 8;           // 64 KiB
 constexpr int AES_TAB4_BYTES = 2 * AES_TAB2_BYTES;     // 128 KiB
-constexpr int GH_LDS_BYTES = 256 * 16 * 16;            // 64 KiB
 
 // T0[x] = (2s, s, s, 3s) bytes little-endian, s = S[x]: the FIPS-197 5.1.1
 // S-box (inverse in GF(2^8), then the affine map) computed on the device, so
@@ -136,13 +136,10 @@ DEV AesLds make_aes_lds(const void *lds)
 // v_bitop3_b32, a full-rate VALU op on gfx950, where v_perm_b32 is
 // half-rate (tools/valu_rate.hip: 1.15 vs 1.9 ns per wave-instruction per
 // SIMD); the other bytes need the permute.
-#ifndef AES_BITOP3_B1
-#define AES_BITOP3_B1 1
-#endif
 template <int TAB, int K>
 DEV uint32_t ta(const AesLds &T, uint32_t w)
 {
-    if constexpr (K == 1 && AES_BITOP3_B1)
+    if constexpr (K == 1)
         return __builtin_amdgcn_bitop3_b32(w, 0x0000ff00u, T.L[TAB >> 1], 0xEA);
     return __builtin_amdgcn_perm(w, T.L[TAB >> 1], 0x0c020000u | ((4u + K) << 8));
 }
@@ -565,28 +562,15 @@ struct CoopPtr {
 };
 
 // ---------------------------------------------------------------------------
-// GHASH: Shoup 8-bit table, X held as big-endian words (x^0 = bit 31 of x0)
-template <bool LDSM>
-struct GhTab {
-    const char *lds;          // LDS base of the replicated table (+64K)
-    uint32_t lane16;          // (lane & 15) * 16 | 0x10000
-    const u32x4 *g;           // global table (per-lane key variant)
-    DEV u32x4 get(uint32_t w, int k) const;
+// GHASH: X held as big-endian words (x^0 = bit 31 of x0).  Per-lane keys
+// read their key's Shoup 8-bit table M[b] = b * H from global memory.
+struct GhGlobal {
+    const u32x4 *g;
+    DEV u32x4 get(uint32_t w, int k) const   // byte k of BE word w
+    {
+        return g[(w >> (24 - 8 * k)) & 0xffu];
+    }
 };
-
-template <>
-DEV u32x4 GhTab<true>::get(uint32_t w, int k) const
-{
-    // byte k of BE word w (k = 0 is the most significant byte) at address
-    // bits 15:8; byte 2 is there already: one full-rate v_bitop3 instead of
-    // the half-rate v_perm
-    if (k == 2)
-        return *(const u32x4 *)(lds + __builtin_amdgcn_bitop3_b32(
-                                          w, 0x0000ff00u, lane16, 0xEA));
-    uint32_t sel = 0x0c020000u | ((4u + 3u - (uint32_t)k) << 8);
-    uint32_t a = __builtin_amdgcn_perm(w, lane16, sel);
-    return *(const u32x4 *)(lds + a);
-}
 
 // multiplies a GHASH value by x^8: the byte shifted out of word 3 (x^128..
 // x^135) is folded back by x^128 = 1 + x + x^2 + x^7 (as in ghash_mul)
@@ -651,13 +635,6 @@ struct GhPos8 {
         }
     }
 };
-
-template <>
-DEV u32x4 GhTab<false>::get(uint32_t w, int k) const
-{
-    uint32_t idx = (w >> (24 - 8 * k)) & 0xffu;
-    return g[idx];
-}
 
 // Z = X * H by Horner over the bytes of X, last byte first (Shoup's 8-bit
 // table M[b] = b * H).  Each step multiplies Z by x^8: the byte leaving Z

@@ -18,11 +18,8 @@ namespace {
 #define GCM_PF 2   // 64-byte payload chunks loaded ahead of their use
 #endif
 // uniform-key batches: the four AES tables (128 KiB) with 8 per-position
-// GHASH tables (32 KiB, GhPos8), instead of (T0, T1) with a 16-copy Shoup
-// table
-#ifndef GCM_TAB4
-#define GCM_TAB4 1
-#endif
+// GHASH tables (32 KiB, GhPos8); per-lane keys: (T0, T1) and each key's
+// Shoup table in global memory
 
 DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
 {
@@ -115,10 +112,6 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
             if (c + GCM_PF < nfc)
                 load_chunk4(ring[GCM_PF - 1], pin + 64 * (c + GCM_PF));
             uint32_t ks[4][4];
-#ifdef GCM_EXP_NOAES   // timing experiment only: no keystream
-            for (int t = 0; t < 4; t++)
-                ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = t;
-#else
 #pragma unroll
             for (int g = 0; g < 4; g += 2) {
                 const uint32_t jb[2] = { (4 * c + g + 2) << 8,
@@ -126,7 +119,6 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
                 aes_ctr<2, NR, TAB4>(
                     *reinterpret_cast<uint32_t(*)[2][4]>(&ks[g]), jb, C, rk, T);
             }
-#endif
 #pragma unroll
             for (int t = 0; t < 4; t++) {
                 const u32x4 o = { cur[t].x ^ ks[t][0], cur[t].y ^ ks[t][1],
@@ -137,11 +129,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
                 x[1] ^= bswap(ctv.y);
                 x[2] ^= bswap(ctv.z);
                 x[3] ^= bswap(ctv.w);
-#ifdef GCM_EXP_NOGHASH   // timing experiment only: fold instead of multiply
-                x[0] ^= x[3] >> 1;
-#else
                 ghash_mul(x, G);
-#endif
             }
         }
         j = 4 * nfc;
@@ -203,8 +191,9 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
     }
 }
 
-// (T0, T1) in LDS plus, for uniform keys, the GHASH table replicated 16x
-// (128 KiB: one 512-lane workgroup per CU); persistent grid.
+// Uniform keys: four AES tables + per-position GHASH tables (160 KiB, one
+// 512-lane workgroup per CU); per-lane keys: (T0, T1) (64 KiB, two per CU).
+// Persistent grid.
 #ifndef GCM_THREADS_N
 #define GCM_THREADS_N 512
 #endif
@@ -213,10 +202,9 @@ constexpr int GCM_THREADS = GCM_THREADS_N;
 template <int NR, bool PROTECT, bool UNIFORM>
 __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 {
-    constexpr bool TAB4 = UNIFORM && GCM_TAB4;
+    constexpr bool TAB4 = UNIFORM;
     constexpr int GH8 = 256 * 16 * 8;   // the per-position GHASH tables
-    __shared__ u32x4 s_tab[(TAB4 ? AES_TAB4_BYTES + GH8
-                                 : AES_TAB2_BYTES + (UNIFORM ? GH_LDS_BYTES : 0)) /
+    __shared__ u32x4 s_tab[(TAB4 ? AES_TAB4_BYTES + GH8 : AES_TAB2_BYTES) /
                            16];
     if (A.abort && *A.abort)
         return;
@@ -238,14 +226,7 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
             }
         }
     } else {
-    load_aes_tables<false>(s_tab);
-    }
-    if (UNIFORM && !TAB4) {
-        const u32x4 *src =
-            (const u32x4 *)(A.ghash + 1024 * A.keys[A.uni].ghash_slot);
-        u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB2_BYTES);
-        for (int e = threadIdx.x; e < 256 * 16; e += blockDim.x)
-            dst[e] = src[e >> 4];
+        load_aes_tables<false>(s_tab);
     }
     __syncthreads();
     const char *lds = (const char *)s_tab;
@@ -263,9 +244,7 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
             gcm_packet<NR, PROTECT, UNIFORM, true>(A, i, T, G, rk);
         return;
     }
-    GhTab<UNIFORM> G;
-    G.lds = lds + AES_TAB2_BYTES - 0x10000;   // the 0x10000 comes from lane16
-    G.lane16 = ((threadIdx.x & 15) * 16) | 0x10000u;
+    GhGlobal G;   // set per packet from its key
     G.g = nullptr;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
          i += stride)

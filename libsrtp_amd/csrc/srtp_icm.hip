@@ -556,10 +556,7 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
 // the CUs and each workgroup walks the batch, so the tables are loaded once
 // per CU.
 constexpr int ICM_THREADS_UNI = 512;
-#ifndef ICM_LANE_THREADS
-#define ICM_LANE_THREADS 512
-#endif
-constexpr int ICM_THREADS_LANE = ICM_LANE_THREADS;
+constexpr int ICM_THREADS_LANE = 512;
 constexpr uint32_t ICM_SKIP = 0xffffffffu;
 
 template <int NR, bool AUTH, bool PROTECT, int KM>
