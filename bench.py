@@ -273,12 +273,12 @@ def _bounded(fn, *args, limit=120):
         return None
 
 
-def cgroup_cpus():
+def cgroup_cpus(root="/sys/fs/cgroup"):
     """the cgroup CPU quota in whole CPUs (cgroup v2 cpu.max or v1
     cfs_quota_us / cfs_period_us), None when there is none"""
     import math
     try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
+        with open(os.path.join(root, "cpu.max")) as f:
             q, p = f.read().split()[:2]
         if q != "max":
             return max(1, math.ceil(int(q) / int(p)))
@@ -286,9 +286,9 @@ def cgroup_cpus():
     except (OSError, ValueError):
         pass
     try:
-        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+        with open(os.path.join(root, "cpu", "cpu.cfs_quota_us")) as f:
             q = int(f.read())
-        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+        with open(os.path.join(root, "cpu", "cpu.cfs_period_us")) as f:
             p = int(f.read())
         return max(1, math.ceil(q / p)) if q > 0 else None
     except (OSError, ValueError):

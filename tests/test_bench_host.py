@@ -1,0 +1,37 @@
+"""bench.py's host-side helpers (no GPU): the CPU-baseline thread count from
+the cgroup quota, and the time-bounded reference legs."""
+import os
+
+import pytest
+
+import bench
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_cgroup_cpus_v2_and_v1(tmp_path):
+    (tmp_path / "cpu.max").write_text("1600000 100000\n")
+    assert bench.cgroup_cpus(str(tmp_path)) == 16
+    (tmp_path / "cpu.max").write_text("150000 100000\n")
+    assert bench.cgroup_cpus(str(tmp_path)) == 2      # 1.5 CPUs -> 2 threads
+    (tmp_path / "cpu.max").write_text("max 100000\n")
+    assert bench.cgroup_cpus(str(tmp_path)) is None
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("800000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert bench.cgroup_cpus(str(v1)) == 8
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    assert bench.cgroup_cpus(str(v1)) is None
+    assert bench.cgroup_cpus(str(tmp_path / "none")) is None
+
+
+def test_bounded_leg_result_and_limit():
+    lib = os.path.join(ROOT, "oracle", "_ref", "bench_ref_int.so")
+    if not os.path.exists(lib):
+        pytest.skip("oracle/_ref not built")
+    r = bench._bounded("_ref_rate", lib, "protect", 160, False, 2, 0.5)
+    assert r is not None and r[0] > 0 and r[1] > 0
+    # a leg past its limit reports nothing instead of stalling the bench
+    assert bench._bounded("_ref_rate", lib, "protect", 160, False, 2, 60.0,
+                          limit=1) is None
