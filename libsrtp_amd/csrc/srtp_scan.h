@@ -78,26 +78,51 @@ __device__ __forceinline__ Agg agg_none()
     return r;
 }
 
-// exclusive scan of one Agg per thread over the block (Hillis-Steele in
-// LDS); returns the thread's exclusive prefix, *total = the block's
 template <int OP>
+__device__ __forceinline__ Agg agg_shfl_up(const Agg &a, int d)
+{
+    Agg r;
+    r.fk = (uint32_t)__shfl_up((int)a.fk, d);
+    r.lk = (uint32_t)__shfl_up((int)a.lk, d);
+    r.single = (uint32_t)__shfl_up((int)a.single, d);
+    r.has = (uint32_t)__shfl_up((int)a.has, d);
+    r.v = (uint64_t)__shfl_up((long long)a.v, d);
+    return r;
+}
+
+// exclusive scan of one Agg per thread over the block: inclusive scans of
+// the four waves by shuffles, the wave totals through LDS (two barriers;
+// a Hillis-Steele pass over 256 threads in LDS took 16); returns the
+// thread's exclusive prefix, *total = the block's
+template <int OP, int NT = TILE_THREADS>
 __device__ Agg block_exclusive(Agg mine, Agg *total)
 {
-    __shared__ Agg s_a[TILE_THREADS];
-    const int t = threadIdx.x;
-    s_a[t] = mine;
-    __syncthreads();
-    for (int d = 1; d < TILE_THREADS; d <<= 1) {
-        Agg o = t >= d ? s_a[t - d] : agg_none();
-        __syncthreads();
-        if (t >= d)
-            s_a[t] = combine<OP>(o, s_a[t]);
-        __syncthreads();
+    constexpr int NW = NT / 64;
+    __shared__ Agg s_w[NW];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    Agg incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const Agg o = agg_shfl_up<OP>(incl, d);   // an earlier lane
+        if (lane >= d)
+            incl = combine<OP>(o, incl);
     }
-    Agg ex = t ? s_a[t - 1] : agg_none();
-    *total = s_a[TILE_THREADS - 1];
+    Agg lex = agg_shfl_up<OP>(incl, 1);
+    if (lane == 0)
+        lex = agg_none();
+    if (lane == 63)
+        s_w[wv] = incl;
     __syncthreads();
-    return ex;
+    Agg wex = agg_none(), tot = agg_none();
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        if (w == wv)
+            wex = tot;
+        tot = combine<OP>(tot, s_w[w]);
+    }
+    *total = tot;
+    __syncthreads();   // s_w is free again
+    return combine<OP>(wex, lex);
 }
 
 // Traits: key(i) (NOKEY-free; unsegmented scans return 0), val(i),
@@ -122,24 +147,16 @@ __global__ __launch_bounds__(TILE_THREADS) void k_scan_up(S s, uint32_t n,
 template <int OP>
 __global__ __launch_bounds__(1024) void k_scan_mid(Agg *agg, uint32_t ntiles)
 {
-    __shared__ Agg s_a[1024];
-    const uint32_t t = threadIdx.x, T = blockDim.x;
+    constexpr uint32_t T = 1024;   // the launch's block size
+    const uint32_t t = threadIdx.x;
     const uint32_t per = (ntiles + T - 1) / T;
     const uint32_t a0 = t * per < ntiles ? t * per : ntiles;
     const uint32_t a1 = a0 + per < ntiles ? a0 + per : ntiles;
     Agg run = agg_none();
     for (uint32_t i = a0; i < a1; i++)
         run = combine<OP>(run, agg[i]);
-    s_a[t] = run;
-    __syncthreads();
-    for (uint32_t d = 1; d < T; d <<= 1) {
-        Agg o = t >= d ? s_a[t - d] : agg_none();
-        __syncthreads();
-        if (t >= d)
-            s_a[t] = combine<OP>(o, s_a[t]);
-        __syncthreads();
-    }
-    Agg c = t ? s_a[t - 1] : agg_none();
+    Agg tot;
+    Agg c = block_exclusive<OP, T>(run, &tot);
     for (uint32_t i = a0; i < a1; i++) {
         const Agg me = agg[i];
         agg[i] = c;   // exclusive carry of tile i
