@@ -785,7 +785,7 @@ __global__ void k_pu_top_check(const uint32_t *skey2, const uint32_t *perm2,
 // per-stream count and highest index; the meta of authenticated packets
 // is cleared so that the undo pass restores only the rejected ones (after
 // an abort nothing is cleared: the undo restores every packet for the host)
-__global__ void k_pu_accept(const uint32_t *skey, const uint32_t *perm,
+__global__ __launch_bounds__(1024) void k_pu_accept(const uint32_t *skey, const uint32_t *perm,
                             const uint64_t *est, const uint32_t *pstat,
                             const srtp_dev_hdr_t *hdr,
                             const srtp_dev_stream_t *st, uint32_t ns,
@@ -2104,7 +2104,10 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                            P->perm2, P->hdr, P->est, P->top, P->st, ns, N,
                            P->abort);
     }
-    hipLaunchKernelGGL(k_pu_accept, gp, blk, 0, stream, ks, kp, P->est,
+    // 1024-thread blocks: agg_stream merges a block's waves, so one stream's
+    // batch costs one same-address atomic pair per 1024 packets
+    hipLaunchKernelGGL(k_pu_accept, dim3((N + 1023) / 1024), dim3(1024), 0,
+                       stream, ks, kp, P->est,
                        P->pstat, P->hdr, P->st, ns, N, P->abort, P->auth,
                        P->meta, b->status, b->out_len, P->bcount2,
                        (unsigned long long *)P->new_index2);
