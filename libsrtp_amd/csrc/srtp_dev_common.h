@@ -421,6 +421,55 @@ DEV void store_bytes(uint8_t *p, uint32_t w, int n)
         p[i] = (uint8_t)(w >> (8 * i));
 }
 
+// The first n bytes of the little-endian words w at p (an authentication
+// tag): whole words as dword stores when p is 4-byte aligned (the usual
+// case: a tag follows a 4-byte-aligned RTP payload end), the rest byte by
+// byte.  A 10-byte HMAC-SHA1-80 tag is then 3 store instructions instead of
+// 10 partial-line stores per lane.
+template <int NW>
+DEV void store_tag(uint8_t *p, const uint32_t (&w)[NW], uint32_t n)
+{
+    const bool al = ((uintptr_t)p & 3) == 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const int r = (int)n - 4 * j;
+        if (r <= 0)
+            break;
+        if (r >= 4 && al) {
+            *(uint32_t *)(p + 4 * j) = w[j];
+            continue;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (b < r)
+                p[4 * j + b] = (uint8_t)(w[j] >> (8 * b));
+    }
+}
+
+// OR of the differences between the n tag bytes at p and those of w (zero
+// when equal; every byte is read, constant time in the data)
+template <int NW>
+DEV uint32_t tag_diff(const uint8_t *p, const uint32_t (&w)[NW], uint32_t n)
+{
+    const bool al = ((uintptr_t)p & 3) == 0;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < NW; j++) {
+        const int r = (int)n - 4 * j;
+        if (r <= 0)
+            break;
+        if (r >= 4 && al) {
+            diff |= *(const uint32_t *)(p + 4 * j) ^ w[j];
+            continue;
+        }
+#pragma unroll
+        for (int b = 0; b < 4; b++)
+            if (b < r)
+                diff |= (uint32_t)(p[4 * j + b] ^ (uint8_t)(w[j] >> (8 * b)));
+    }
+    return diff;
+}
+
 DEV void store_words_partial(uint8_t *p, const uint32_t *w, int nbytes)
 {
     // store the first nbytes (0..16) of 4 LE words at p (p 4-byte aligned)

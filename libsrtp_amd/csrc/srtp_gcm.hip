@@ -178,16 +178,11 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
                          bswap(x[3]) ^ e3 };   // little-endian words of tag
     if (PROTECT) {
         uint8_t *tp = pout + P;
-        for (uint32_t u = 0; u < tag_len; u++)
-            tp[u] = (uint8_t)(tagw[u >> 2] >> (8 * (u & 3)));
+        store_tag(tp, tagw, tag_len);
         for (uint32_t u = 0; u < mki_size; u++)
             tp[tag_len + u] = key->mki[u];
     } else {
-        const uint8_t *tp = pin + P;
-        uint32_t diff = 0;
-        for (uint32_t u = 0; u < tag_len; u++)
-            diff |= (uint32_t)(tp[u] ^ (uint8_t)(tagw[u >> 2] >> (8 * (u & 3))));
-        A.auth_ok[i] = diff == 0;
+        A.auth_ok[i] = tag_diff(pin + P, tagw, tag_len) == 0;
     }
 }
 

@@ -532,18 +532,17 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
         oh[k] = key->opad[k];
     sha1_compress(oh, ow);
 
+    // the tag: the first tag_len bytes of the digest (big-endian words)
+    uint32_t tw[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        tw[k] = bswap(oh[k]);
     if (PROTECT) {
         for (uint32_t u = 0; u < mki_size; u++)
             out[L + u] = key->mki[u];
-        uint8_t *tp = out + L + mki_size;
-        for (uint32_t u = 0; u < tag_len; u++)
-            tp[u] = (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3)));
+        store_tag(out + L + mki_size, tw, tag_len);
     } else {
-        const uint8_t *tp = p.in + L + mki_size;
-        uint32_t diff = 0;
-        for (uint32_t u = 0; u < tag_len; u++)
-            diff |= (uint32_t)(tp[u] ^ (uint8_t)(oh[u >> 2] >> (24 - 8 * (u & 3))));
-        A.auth_ok[i] = diff == 0;
+        A.auth_ok[i] = tag_diff(p.in + L + mki_size, tw, tag_len) == 0;
     }
 }
 
