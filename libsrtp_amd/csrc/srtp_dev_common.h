@@ -470,16 +470,29 @@ DEV uint32_t tag_diff(const uint8_t *p, const uint32_t (&w)[NW], uint32_t n)
     return diff;
 }
 
+typedef uint32_t u32x2a4 __attribute__((ext_vector_type(2), aligned(4)));
+typedef uint32_t u32x3a4 __attribute__((ext_vector_type(3), aligned(4)));
+
 DEV void store_words_partial(uint8_t *p, const uint32_t *w, int nbytes)
 {
-    // store the first nbytes (0..16) of 4 LE words at p (p 4-byte aligned)
+    // store the first nbytes (0..16) of 4 LE words at p (p 4-byte aligned):
+    // the whole words in one store instruction, then the bytes left
+    const int nw = nbytes >> 2;
+    if (nw == 4)
+        *(u32x4a4 *)p = u32x4a4{ w[0], w[1], w[2], w[3] };
+    else if (nw == 3)
+        *(u32x3a4 *)p = u32x3a4{ w[0], w[1], w[2] };
+    else if (nw == 2)
+        *(u32x2a4 *)p = u32x2a4{ w[0], w[1] };
+    else if (nw == 1)
+        *(uint32_t *)p = w[0];
+    if ((nbytes & 3) == 0 || nw == 4)
+        return;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        int n = nbytes - 4 * i;
-        if (n >= 4)
-            *(uint32_t *)(p + 4 * i) = w[i];
-        else if (n > 0)
-            store_bytes(p + 4 * i, w[i], n);
+        if (i != nw)
+            continue;
+        store_bytes(p + 4 * i, w[i], nbytes & 3);
     }
 }
 
