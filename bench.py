@@ -146,7 +146,14 @@ PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
               ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES"))
 
 
-def measure_pmc(a, kname):
+DIST_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
+             "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE", "GROUP_WORLD_SIZE",
+             "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID",
+             "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS",
+             "SRTP_FORCE_DIST")
+
+
+def measure_pmc(a, kname, device=0):
     """per-launch PMC counters of the dominant kernel over a short run of
     this same workload, one rocprofv3 --pmc pass per entry of PMC_PASSES,
     each a child process started before this process touches the GPU.
@@ -175,10 +182,14 @@ def measure_pmc(a, kname):
                "--no-cpu-baseline", "--traffic", "off"]
         if a.packets:
             cmd += ["--packets", str(a.packets)]
+        # a one-rank child on this rank's device (at N > 1 rank 0 measures
+        # before the process group forms; the other ranks wait in it)
+        env = {k: v for k, v in os.environ.items() if k not in DIST_VARS}
+        env.update(TMPDIR="/tmp", SRTP_BENCH_DEVICE=str(device))
         try:
             # the child's stderr (its progress notes) stays visible
             subprocess.run(cmd, stdout=subprocess.DEVNULL, timeout=150,
-                           env=dict(os.environ, TMPDIR="/tmp"))
+                           env=env)
         except subprocess.TimeoutExpired:
             break
         csvs = glob.glob(os.path.join(d, "**", "*counter_collection.csv"),
@@ -438,6 +449,56 @@ def distribute_keys(keys_hex, world, dev):
     return [raw[i * w:(i + 1) * w].hex() for i in range(len(keys_hex))]
 
 
+def replicate_session(L, policies, world, rank, dev, backend):
+    """Session replication (north_star "RCCL broadcast of
+    session keys over xGMI"): rank 0 creates the session -- its KDF derives
+    the session keys on its GPU -- and every other rank receives a replica
+    (streams, derived key records, stream state) through the library's C
+    ABI.  With RCCL (backend nccl) that is srtp_mi355x_session_broadcast on
+    torch's own communicator: ncclBroadcast of the exported blob from device
+    memory over xGMI.  Otherwise (gloo, or no communicator handle) the
+    exported blob (srtp_mi355x_session_export) goes through the process
+    group and srtp_mi355x_session_import rebuilds it.  Returns (session,
+    how)."""
+    import torch
+    import torch.distributed as dist
+    on = world > 1 or (dist.is_available() and dist.is_initialized())
+    if not on:
+        return L.Session(policies), "none (one rank)"
+    sess = L.Session(policies) if rank == 0 else None
+    tdev = dev if backend == "nccl" else torch.device("cpu")
+    comm = None
+    if backend == "nccl":
+        try:
+            dist.barrier()   # the communicator exists after a collective
+            pg = dist.distributed_c10d._get_default_group()
+            comm = pg._get_backend(torch.device("cuda", dev.index))._comm_ptr()
+        except Exception as e:   # noqa: BLE001 - torch-version dependent
+            note("no RCCL communicator handle (%s): blob over the group" % e)
+            comm = None
+    # every rank takes the same path
+    ok = torch.tensor([1 if comm else 0], dtype=torch.int32, device=tdev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok[0]):
+        stream = torch.cuda.current_stream().cuda_stream
+        return (L.session_broadcast(sess, comm, 0, stream),
+                "srtp_mi355x_session_broadcast (ncclBroadcast on the "
+                "process group's RCCL communicator)")
+    blob = sess.export_blob() if rank == 0 else b""
+    n = torch.tensor([len(blob)], dtype=torch.int64, device=tdev)
+    dist.broadcast(n, src=0)
+    if rank == 0:
+        buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(tdev)
+    else:
+        buf = torch.empty(int(n[0]), dtype=torch.uint8, device=tdev)
+    dist.broadcast(buf, src=0)
+    how = ("srtp_mi355x_session_export / _import, blob broadcast over %s"
+           % backend)
+    if rank == 0:
+        return sess, how
+    return L.Session.from_blob(buf.cpu().numpy().tobytes()), how
+
+
 def _free_port():
     import socket
     with socket.socket() as s:
@@ -554,9 +615,13 @@ def run_gpu(a, world, rank, local, json_out):
     pol, payload, npk, tag = CONFIGS[a.config]
     kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
     # PMC passes first: child processes, before this one touches the GPU
+    # SRTP_BENCH_DEVICE: every rank of this process on that device (the
+    # N > 1 path exercised on a one-GPU box, with gloo: RCCL refuses two
+    # ranks on one device)
+    devno = int(os.environ.get("SRTP_BENCH_DEVICE", local))
     pmc = {}
-    if world == 1 and a.traffic == "auto":
-        pmc = measure_pmc(a, kname)
+    if rank == 0 and a.traffic == "auto":
+        pmc = measure_pmc(a, kname, devno)
     traffic = None
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         traffic = (pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
@@ -564,33 +629,49 @@ def run_gpu(a, world, rank, local, json_out):
     import torch.distributed as dist
     # SRTP_FORCE_DIST=1: a one-rank process group, so the RCCL barrier,
     # key broadcast and max-over-ranks reduction run on a one-GPU box too
+    backend = None
+    torch.cuda.set_device(devno)
     if world > 1 or os.environ.get("SRTP_FORCE_DIST") == "1":
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group(
-            os.environ.get("SRTP_DIST_BACKEND", "nccl"),
-            device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+        backend = os.environ.get("SRTP_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group(backend,
+                                    device_id=torch.device("cuda", devno))
+        else:
+            dist.init_process_group(backend)
     import libsrtp_amd as L
     dev = torch.device("cuda", torch.cuda.current_device())
 
     n = a.packets or npk
     nstreams = STREAMS[a.config]
     ssrc = rank_ssrc(rank)
-    # rank 0's master key(s), broadcast to every rank
-    keys = distribute_keys([TEST_KEY] if nstreams == 1 else
-                           stream_keys(nstreams), world, dev)
     if nstreams == 1:
-        policies = [dict(pol, ssrc_type=1, ssrc=ssrc, window_size=128,
-                         allow_repeat_tx=0, keys=keys)]
+        # one stream per rank (SSRC-affine shards): rank 0's
+        # session holds every rank's stream; each rank keeps its own shard
+        # of the replica
+        policies = [dict(pol, ssrc_type=1, ssrc=rank_ssrc(r), window_size=128,
+                         allow_repeat_tx=0, keys=[TEST_KEY])
+                    for r in range(world)]
+        note("session: %d streams (GPU KDF on rank 0), replicated"
+             % len(policies))
+        sess, replication = replicate_session(L, policies, world, rank, dev,
+                                              backend)
+        for r in range(world):
+            if r != rank and sess.remove_stream(rank_ssrc(r)) != 0:
+                raise RuntimeError("bench: removing stream of rank %d" % r)
     else:
+        # 64k streams per rank: the master keys (rank 0's) are broadcast and
+        # every rank derives its own streams' session keys
+        keys = distribute_keys(stream_keys(nstreams), world,
+                               dev if backend == "nccl" else "cpu")
         base = (0x10000000 + (rank << 20)) & 0xffffffff
         policies = [dict(pol, ssrc_type=1, ssrc=base + k, window_size=128,
                          allow_repeat_tx=0, keys=[key])
                     for k, key in enumerate(keys)]
-    note("session: %d streams (GPU KDF)" % len(policies))
-    sess = L.Session(policies)
+        note("session: %d streams (GPU KDF)" % len(policies))
+        sess = L.Session(policies)
+        replication = "master keys broadcast, KDF per rank" \
+            if backend else "none (one rank)"
 
     note("building %d batches of %d packets in HBM" % (a.warmup + a.steps, n))
     # packet arenas in HBM, one per step: slot = roundup16(rtp_len + tag)
@@ -700,9 +781,12 @@ def run_gpu(a, world, rank, local, json_out):
     algo_bytes = n * (rtp_len + rtp_len + tag)   # rtp + srtp, read + write
     achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
     if rank != 0:
+        if backend:
+            dist.barrier()   # rank 0's CPU baseline and line, then teardown
         return
     cpu = None
-    if world == 1 and not a.no_cpu_baseline:
+    if not a.no_cpu_baseline:
+        # the host cores beside rank 0's GPU, after the timed region
         cpu = cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
     roofline = {"bound": "hbm", "achieved": achieved,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -715,7 +799,10 @@ def run_gpu(a, world, rank, local, json_out):
                "host_batches": host_b - host_b0,
                "last_abort": sess.prepass_last_abort()}
     out = result_line(a, world, n, payload, tag, dt, roofline, cpu, prepass)
+    out["session_replication"] = replication
     print(json.dumps(out), file=json_out, flush=True)
+    if backend:
+        dist.barrier()
 
 
 if __name__ == "__main__":

@@ -373,6 +373,41 @@ srtp_err_status_t srtp_protect_device_async(srtp_t ctx,
 srtp_err_status_t srtp_unprotect_device(srtp_t ctx,
                                         const srtp_device_batch_t *b);
 
+/* ======================================================================
+ * Session replication across GPUs (new; north_star "RCCL broadcast of
+ * session keys over xGMI").  The reference has no
+ * counterpart: its session is one process's srtp_create
+ * (include/srtp.h:512, srtp/srtp.c:1233-1607 derives the session keys).
+ * A replica is a session on another device (or process) with the same
+ * streams, template, derived session keys (the device key records: AES
+ * schedules, salts, HMAC midstates, GCM H; GHASH tables are rebuilt from H)
+ * and per-stream state (index / ROC, replay windows, SRTCP index window,
+ * key-usage counters).  Master keys are not part of it: they are not kept
+ * after srtp_create.  Sessions whose streams use replaced crypto types
+ * (srtp_replace_cipher_type / _auth_type) cannot be exported
+ * (srtp_err_status_bad_param): their keys live in host vtable objects.
+ * ====================================================================== */
+/* Serialise `ctx` into buf (cap bytes).  *len receives the blob size; with
+ * buf == NULL (or cap too small: srtp_err_status_bad_param) nothing is
+ * written but *len.  The blob holds secret key material. */
+srtp_err_status_t srtp_mi355x_session_export(srtp_t ctx, void *buf,
+                                             size_t cap, size_t *len);
+/* A new session on the calling thread's current HIP device from a blob of
+ * srtp_mi355x_session_export (same library build and host byte order). */
+srtp_err_status_t srtp_mi355x_session_import(srtp_t *session, const void *blob,
+                                             size_t len);
+/* Collective over a caller's RCCL communicator (ncclComm_t passed as
+ * void *): on the communicator's rank `root`, *session is an existing
+ * session whose blob is broadcast from device memory with ncclBroadcast
+ * (RCCL over xGMI); on every other rank *session receives the imported
+ * replica.  `stream` is the hipStream_t the broadcast is enqueued on (NULL:
+ * the null stream); the call returns once the replica exists.  RCCL is
+ * resolved at run time from the process (dlsym RTLD_DEFAULT, then
+ * librccl.so.1): srtp_err_status_init_fail when it is absent. */
+srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
+                                                void *nccl_comm, int root,
+                                                void *stream);
+
 /* Instrumentation for bench.py: device time (ms) of the crypto kernels of
  * the last batch, measured with HIP events on the stream they ran on. */
 void srtp_mi355x_set_timing(srtp_t ctx, int on);

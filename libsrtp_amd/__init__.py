@@ -14,6 +14,7 @@ from .srtp import (  # noqa: F401
     LIB_PATH, lib, build, Status, Policy, CryptoPolicy, MasterKey,
     SSRC_SPECIFIC, SSRC_ANY_INBOUND, SSRC_ANY_OUTBOUND, Session,
     policy_setter, DeviceBatch, EventData, install_event_handler,
+    session_broadcast,
 )
 
 # fail loudly at import when the HIP library is absent: there is no fallback
@@ -23,4 +24,5 @@ __all__ = [
     "LIB_PATH", "lib", "build", "Status", "Policy", "CryptoPolicy",
     "MasterKey", "Session", "policy_setter", "DeviceBatch",
     "SSRC_SPECIFIC", "SSRC_ANY_INBOUND", "SSRC_ANY_OUTBOUND",
+    "session_broadcast",
 ]

@@ -150,6 +150,14 @@ const char *srtp_gpu_last_error(void);
 int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
                      const uint32_t *ghash_tab /* 1024 words or NULL */);
 
+/* the key table as a whole (session replication, srtp_mi355x_session_*):
+ * get copies slots [0, n) to dst; put writes slots [0, n) from src and
+ * builds the GHASH table of every slot i with ghash_flag[i] != 0 from its
+ * record's H (k_ghash_build).  Synchronous. */
+int srtp_gpu_get_keys(srtp_gpu_t *g, uint32_t n, srtp_dev_key_t *dst);
+int srtp_gpu_put_keys(srtp_gpu_t *g, uint32_t n, const srtp_dev_key_t *src,
+                      const uint8_t *ghash_flag);
+
 /* derive n session keys on the GPU (k_kdf) straight into the key table;
  * synchronous */
 int srtp_gpu_kdf(srtp_gpu_t *g, const srtp_kdf_job_t *jobs, size_t n);

@@ -1034,6 +1034,31 @@ DEV void kdf_prf(const ArrKey<NR> &K, const uint8_t *salt, uint32_t label,
     }
 }
 
+// Shoup's table M[b] = b * H of the big-endian H words v (clobbered): powers
+// by halving (v * x = v >> 1, ^ 0xe1 on carry), then sums
+// (host_crypto.c hc_ghash_table, same layout)
+DEV void ghash_shoup(uint32_t v[4], uint32_t *tab)
+{
+    for (int w = 0; w < 4; w++)
+        tab[w] = 0;
+    for (uint32_t bit = 0x80; bit; bit >>= 1) {
+        for (int w = 0; w < 4; w++)
+            tab[4 * bit + w] = v[w];
+        const uint32_t lsb = v[3] & 1u;
+        v[3] = (v[3] >> 1) | (v[2] << 31);
+        v[2] = (v[2] >> 1) | (v[1] << 31);
+        v[1] = (v[1] >> 1) | (v[0] << 31);
+        v[0] = (v[0] >> 1) ^ ((0u - lsb) & 0xe1000000u);
+    }
+    for (uint32_t b = 1; b < 256; b++) {
+        const uint32_t low = b & (0u - b);
+        if (b == low)
+            continue;
+        for (int w = 0; w < 4; w++)
+            tab[4 * b + w] = tab[4 * low + w] ^ tab[4 * (b ^ low) + w];
+    }
+}
+
 // the cipher half of the record: schedule of the derived key, H, GHASH
 template <int NR>
 DEV void kdf_cipher(const srtp_kdf_job_t &J, const uint8_t *ek,
@@ -1056,27 +1081,7 @@ DEV void kdf_cipher(const srtp_kdf_job_t &J, const uint8_t *ek,
     }
     if (!(J.flags & SRTP_KDF_GHASH))
         return;
-    // Shoup's table M[b] = b * H: powers by halving (v * x = v >> 1, ^ 0xe1
-    // on carry), then sums (host_crypto.c hc_ghash_table, same layout)
-    uint32_t *tab = ghash + 1024 * (size_t)J.key.ghash_slot;
-    for (int w = 0; w < 4; w++)
-        tab[w] = 0;
-    for (uint32_t bit = 0x80; bit; bit >>= 1) {
-        for (int w = 0; w < 4; w++)
-            tab[4 * bit + w] = v[w];
-        const uint32_t lsb = v[3] & 1u;
-        v[3] = (v[3] >> 1) | (v[2] << 31);
-        v[2] = (v[2] >> 1) | (v[1] << 31);
-        v[1] = (v[1] >> 1) | (v[0] << 31);
-        v[0] = (v[0] >> 1) ^ ((0u - lsb) & 0xe1000000u);
-    }
-    for (uint32_t b = 1; b < 256; b++) {
-        const uint32_t low = b & (0u - b);
-        if (b == low)
-            continue;
-        for (int w = 0; w < 4; w++)
-            tab[4 * b + w] = tab[4 * low + w] ^ tab[4 * (b ^ low) + w];
-    }
+    ghash_shoup(v, ghash + 1024 * (size_t)J.key.ghash_slot);
 }
 
 template <int NRK>
@@ -1134,6 +1139,19 @@ DEV void kdf_one(const srtp_kdf_job_t &J, srtp_dev_key_t *keys,
             }
         }
     }
+}
+
+// GHASH tables of imported key records (srtp_gpu_put_keys): one lane per
+// slot whose flag is set, from the record's H
+__global__ __launch_bounds__(256) void k_ghash_build(const srtp_dev_key_t *keys,
+                                                     const uint8_t *flag,
+                                                     uint32_t n, uint32_t *ghash)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i])
+        return;
+    uint32_t v[4] = { keys[i].h[0], keys[i].h[1], keys[i].h[2], keys[i].h[3] };
+    ghash_shoup(v, ghash + 1024 * (size_t)keys[i].ghash_slot);
 }
 
 __global__ __launch_bounds__(256) void k_kdf(const srtp_kdf_job_t *jobs,
@@ -1342,6 +1360,59 @@ int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
         HIPCHK(hipMemcpyAsync(g->d_ghash + 1024 * (size_t)k->ghash_slot,
                               ghash_tab, 4096, hipMemcpyHostToDevice,
                               g->stream));
+    }
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return 0;
+}
+
+int srtp_gpu_get_keys(srtp_gpu_t *g, uint32_t n, srtp_dev_key_t *dst)
+{
+    if (!n)
+        return 0;
+    if (n > g->key_cap) {
+        snprintf(g_err, sizeof g_err, "srtp_gpu_get_keys: %u slots of %u",
+                 n, g->key_cap);
+        return -1;
+    }
+    HIPCHK(hipMemcpyAsync(dst, g->d_keys, (size_t)n * sizeof *dst,
+                          hipMemcpyDeviceToHost, g->stream));
+    HIPCHK(hipStreamSynchronize(g->stream));
+    return 0;
+}
+
+int srtp_gpu_put_keys(srtp_gpu_t *g, uint32_t n, const srtp_dev_key_t *src,
+                      const uint8_t *ghash_flag)
+{
+    if (!n)
+        return 0;
+    if (grow((void **)&g->d_keys, &g->key_cap, n, sizeof(srtp_dev_key_t)))
+        return -1;
+    HIPCHK(hipMemcpyAsync(g->d_keys, src, (size_t)n * sizeof *src,
+                          hipMemcpyHostToDevice, g->stream));
+    uint32_t gmax = 0;
+    for (uint32_t i = 0; i < n; i++)
+        if (ghash_flag[i] && src[i].ghash_slot + 1 > gmax)
+            gmax = src[i].ghash_slot + 1;
+    if (gmax) {
+        if (grow((void **)&g->d_ghash, &g->ghash_cap, gmax,
+                 1024 * sizeof(uint32_t)))
+            return -1;
+        uint8_t *d = NULL;
+        HIPCHK(hipMalloc((void **)&d, n));
+        hipError_t e = hipMemcpyAsync(d, ghash_flag, n, hipMemcpyHostToDevice,
+                                      g->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(k_ghash_build, dim3((n + 255) / 256), dim3(256),
+                               0, g->stream, g->d_keys, d, n,
+                               (uint32_t *)g->d_ghash);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(g->stream);
+        (void)hipFree(d);
+        if (e != hipSuccess)
+            return srtp_gpu_fail(e, "k_ghash_build");
+        return 0;
     }
     HIPCHK(hipStreamSynchronize(g->stream));
     return 0;

@@ -26,8 +26,10 @@
  * rejected packet holds its ciphertext, as with the reference (which
  * verifies before decrypting).
  */
+#define _GNU_SOURCE /* dlsym RTLD_DEFAULT (session broadcast) */
 #include "srtp_mi355x.h"
 
+#include <dlfcn.h>
 #include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -2326,12 +2328,18 @@ static void routed_reset(srtp_t ctx)
  * to the device arenas.  Protect: ctx->vres[i] = the status of a packet
  * whose cipher / auth call failed (its output untouched).  Unprotect:
  * auth_ok[i] = the verdict; only an authenticated packet is decrypted, its
- * original bytes kept in ctx->vsave[i] for undo_runs. */
+ * original bytes kept in ctx->vsave[i] for undo_runs.  The routed packets
+ * move as one gather and one scatter (every copy queued, one synchronize
+ * each way): the vtable calls themselves are the host's per-packet work. */
 static int run_routed(srtp_t ctx, int op, size_t n, const uint8_t *in,
                       const uint64_t *in_off, uint8_t *out,
                       const uint64_t *out_off, const srtp_dev_meta_t *h_meta,
                       void *stream)
 {
+    /* no status of an earlier (possibly failed) pass may survive into this
+     * one's routed_status */
+    if (ctx->vres_cap)
+        memset(ctx->vres, 0, n < ctx->vres_cap ? n : ctx->vres_cap);
     size_t nv = 0;
     for (size_t i = 0; i < n; i++)
         if (!SRTP_META_STATUS(h_meta[i].info) &&
@@ -2350,13 +2358,19 @@ static int run_routed(srtp_t ctx, int op, size_t n, const uint8_t *in,
             return -1;
     }
     uint64_t *io = (uint64_t *)malloc(n * 8), *oo = (uint64_t *)malloc(n * 8);
-    uint8_t *buf = (uint8_t *)malloc(65536 + 2 * SRTP_MAX_TRAILER_LEN);
+    size_t *list = (size_t *)malloc(nv * sizeof(size_t));
+    size_t *pos = (size_t *)malloc(nv * sizeof(size_t));
+    uint8_t *okv = (uint8_t *)calloc(nv, 1);
+    uint8_t *buf = NULL;
     int rc = -1;
-    if (!io || !oo || !buf || srtp_gpu_sync(ctx->gpu, stream) ||
+    if (!io || !oo || !list || !pos || !okv || srtp_gpu_sync(ctx->gpu, stream) ||
         srtp_gpu_d2h(ctx->gpu, io, in_off, n * 8, stream) ||
         srtp_gpu_d2h(ctx->gpu, oo, out_off, n * 8, stream) ||
         srtp_gpu_sync(ctx->gpu, stream))
         goto out;
+    /* gather: each routed packet's bytes (protect: the RTP packet, unprotect:
+     * packet + MKI + tag) into one host buffer with room for the trailer */
+    size_t tot = 0, j = 0;
     for (size_t i = 0; i < n; i++) {
         const srtp_dev_meta_t m = h_meta[i];
         if (SRTP_META_STATUS(m.info) ||
@@ -2365,42 +2379,64 @@ static int run_routed(srtp_t ctx, int op, size_t n, const uint8_t *in,
         hkey_t *k = m.key < ctx->vkeys_cap ? ctx->vkeys[m.key] : NULL;
         if (!k || m.len > 65535)
             goto out;
+        list[j] = i;
+        pos[j++] = tot;
+        tot += m.len + k->vmki + k->tag_len + SRTP_MAX_TRAILER_LEN;
+    }
+    buf = (uint8_t *)malloc(tot + 1);
+    if (!buf)
+        goto out;
+    for (j = 0; j < nv; j++) {
+        const size_t i = list[j];
+        const hkey_t *k = ctx->vkeys[h_meta[i].key];
+        const size_t L = h_meta[i].len;
+        if (srtp_gpu_d2h(ctx->gpu, buf + pos[j], in + io[i],
+                         op == 0 ? L : L + k->vmki + k->tag_len, stream))
+            goto out;
+    }
+    if (srtp_gpu_sync(ctx->gpu, stream))
+        goto out;
+    /* the registered types' calls, then the scatter */
+    for (j = 0; j < nv; j++) {
+        const size_t i = list[j];
+        const srtp_dev_meta_t m = h_meta[i];
+        hkey_t *k = ctx->vkeys[m.key];
+        uint8_t *b = buf + pos[j];
         const size_t L = m.len, es = SRTP_META_ENC_START(m.info);
         const size_t total = L + k->vmki + k->tag_len;
         if (op == 0) {
-            if (srtp_gpu_d2h(ctx->gpu, buf, in + io[i], L, stream) ||
-                srtp_gpu_sync(ctx->gpu, stream))
-                goto out;
-            srtp_err_status_t st = vt_protect(k, buf, L, es, m.roc);
+            srtp_err_status_t st = vt_protect(k, b, L, es, m.roc);
             ctx->vres[i] = (uint8_t)st;
-            if (!st && (srtp_gpu_h2d(ctx->gpu, out + oo[i], buf, total, stream) ||
-                        srtp_gpu_sync(ctx->gpu, stream)))
+            if (!st && srtp_gpu_h2d(ctx->gpu, out + oo[i], b, total, stream))
                 goto out;
         } else {
-            if (srtp_gpu_d2h(ctx->gpu, buf, in + io[i], total, stream) ||
-                srtp_gpu_sync(ctx->gpu, stream))
-                goto out;
             uint8_t *orig = (uint8_t *)malloc(L ? L : 1);
             if (!orig)
                 goto out;
-            memcpy(orig, buf, L);
-            uint8_t ok = (uint8_t)vt_unprotect(k, buf, total, L, es, m.roc);
-            if (srtp_gpu_h2d(ctx->gpu, ctx->st.d_auth + i, &ok, 1, stream) ||
-                (ok && srtp_gpu_h2d(ctx->gpu, out + oo[i], buf, L, stream)) ||
-                srtp_gpu_sync(ctx->gpu, stream)) {
+            memcpy(orig, b, L);
+            okv[j] = (uint8_t)vt_unprotect(k, b, total, L, es, m.roc);
+            if (srtp_gpu_h2d(ctx->gpu, ctx->st.d_auth + i, &okv[j], 1, stream) ||
+                (okv[j] && srtp_gpu_h2d(ctx->gpu, out + oo[i], b, L, stream))) {
                 free(orig);
                 goto out;
             }
             free(ctx->vsave[i]);
-            ctx->vsave[i] = ok ? orig : NULL;
-            if (!ok)
+            ctx->vsave[i] = okv[j] ? orig : NULL;
+            if (!okv[j])
                 free(orig);
         }
     }
     rc = 0;
 out:
+    /* the queued copies read buf / okv: both stay until the stream is past
+     * them */
+    if (srtp_gpu_sync(ctx->gpu, stream))
+        rc = -1;
     free(io);
     free(oo);
+    free(list);
+    free(pos);
+    free(okv);
     free(buf);
     return rc;
 }
@@ -4238,4 +4274,453 @@ int srtp_mi355x_debug_index(size_t window, int allow_repeat_tx,
     }
     free(r.w);
     return 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Session replication (srtp_mi355x_session_export / _import / _broadcast):
+ * the multi-GPU sender of SURVEY.md §8(e) keeps one session per GPU; rank
+ * root derives the session keys once (srtp_create, srtp.c:1233-1607 on the
+ * GPU), every other rank receives them -- the device key records, not the
+ * master keys -- with the stream table over RCCL.
+ *
+ * Blob: header, key sets (the hkey_t fields that are not pointers), streams
+ * (policy fields, rdbx index + window words, SRTCP window), then the key
+ * records of slots [0, nslots).  Fixed-width little-endian host layout: a
+ * blob is read by the same build on the same kind of host.
+ * ---------------------------------------------------------------------- */
+#define REP_MAGIC "SRTPREP1"
+
+typedef struct {
+    char magic[8];
+    uint32_t nslots, nkeysets, nstreams, has_templ;
+    uint64_t total;
+} rep_hdr_t;
+
+typedef struct {
+    uint32_t slot, cipher_type, family, rounds, variant, tag_len;
+    uint32_t rslot, rtag_len, rgcm, xslot, limit_state, pad;
+    uint64_t num_left;
+    uint8_t mki[SRTP_MAX_MKI_LEN];
+} rep_key_t;
+
+typedef struct {
+    uint32_t ssrc, keyset, direction, rtp_services, rtcp_services;
+    uint32_t allow_repeat_tx, use_mki, mki_size, window_size, bits;
+    uint32_t pending_roc, rtcp_start, rtcp_bm[4];
+    uint64_t index;
+} rep_stream_t;
+
+typedef struct {
+    const keyset_t *ks;
+    uint32_t idx;
+} rep_kref_t;
+
+static int rep_kref_cmp(const void *a, const void *b)
+{
+    const uintptr_t x = (uintptr_t)((const rep_kref_t *)a)->ks,
+                    y = (uintptr_t)((const rep_kref_t *)b)->ks;
+    return x < y ? -1 : x > y;
+}
+
+/* the streams in blob order: the list (insertion order), then the template */
+static srtp_stream_ctx_t *rep_stream_at(srtp_t ctx, size_t i)
+{
+    return i < ctx->n ? ctx->list[i] : ctx->templ;
+}
+
+srtp_err_status_t srtp_mi355x_session_export(srtp_t ctx, void *buf, size_t cap,
+                                             size_t *len)
+{
+    if (!ctx || !len)
+        return srtp_err_status_bad_param;
+    ASYNC_DRAIN_CHECK(ctx);
+    dev_pull(ctx);
+    if (kq_flush(ctx))
+        return srtp_err_status_fail;
+    const size_t ns = ctx->n + (ctx->templ ? 1 : 0);
+    /* key sets, each once (template clones share theirs) */
+    rep_kref_t *ref = (rep_kref_t *)malloc((ns + 1) * sizeof *ref);
+    if (!ref)
+        return srtp_err_status_alloc_fail;
+    for (size_t i = 0; i < ns; i++)
+        ref[i].ks = rep_stream_at(ctx, i)->keys;
+    qsort(ref, ns, sizeof *ref, rep_kref_cmp);
+    size_t nk = 0;
+    for (size_t i = 0; i < ns; i++)
+        if (!nk || ref[nk - 1].ks != ref[i].ks)
+            ref[nk++].ks = ref[i].ks;
+    size_t total = sizeof(rep_hdr_t), nkeys = 0;
+    srtp_err_status_t rc = srtp_err_status_ok;
+    for (size_t k = 0; k < nk; k++) {
+        ref[k].idx = (uint32_t)k;
+        const keyset_t *ks = ref[k].ks;
+        for (size_t j = 0; j < ks->n; j++)
+            if (ks->k[j].variant == SRTP_VARIANT_V)
+                rc = srtp_err_status_bad_param; /* keys in host vtables */
+        nkeys += ks->n;
+    }
+    total += nk * 2 * sizeof(uint32_t) + nkeys * sizeof(rep_key_t);
+    for (size_t i = 0; i < ns; i++)
+        total += sizeof(rep_stream_t) + rep_stream_at(ctx, i)->rdbx.bits / 8;
+    const uint32_t nslots = ctx->next_slot;
+    total += (size_t)nslots * sizeof(srtp_dev_key_t);
+    *len = total;
+    if (rc || !buf || cap < total) {
+        free(ref);
+        return rc ? rc : (buf ? srtp_err_status_bad_param : srtp_err_status_ok);
+    }
+    uint8_t *p = (uint8_t *)buf;
+    rep_hdr_t h;
+    memset(&h, 0, sizeof h);
+    memcpy(h.magic, REP_MAGIC, 8);
+    h.nslots = nslots;
+    h.nkeysets = (uint32_t)nk;
+    h.nstreams = (uint32_t)ns;
+    h.has_templ = ctx->templ != NULL;
+    h.total = total;
+    memcpy(p, &h, sizeof h);
+    p += sizeof h;
+    for (size_t k = 0; k < nk; k++) {
+        const keyset_t *ks = ref[k].ks;
+        uint32_t w[2] = { (uint32_t)ks->n, (uint32_t)ks->cryptex };
+        memcpy(p, w, sizeof w);
+        p += sizeof w;
+        for (size_t j = 0; j < ks->n; j++) {
+            const hkey_t *hk = &ks->k[j];
+            rep_key_t r;
+            memset(&r, 0, sizeof r);
+            r.slot = hk->slot;
+            r.cipher_type = hk->cipher_type;
+            r.family = hk->family;
+            r.rounds = hk->rounds;
+            r.variant = hk->variant;
+            r.tag_len = (uint32_t)hk->tag_len;
+            r.rslot = hk->rslot;
+            r.rtag_len = (uint32_t)hk->rtag_len;
+            r.rgcm = (uint32_t)hk->rgcm;
+            r.xslot = hk->xslot;
+            r.limit_state = (uint32_t)hk->limit_state;
+            r.num_left = hk->num_left;
+            memcpy(r.mki, hk->mki, sizeof r.mki);
+            memcpy(p, &r, sizeof r);
+            p += sizeof r;
+        }
+    }
+    for (size_t i = 0; i < ns; i++) {
+        const srtp_stream_ctx_t *s = rep_stream_at(ctx, i);
+        rep_kref_t key = { s->keys, 0 };
+        const rep_kref_t *f =
+            (const rep_kref_t *)bsearch(&key, ref, nk, sizeof *ref, rep_kref_cmp);
+        rep_stream_t r;
+        memset(&r, 0, sizeof r);
+        r.ssrc = s->ssrc;
+        r.keyset = f->idx;
+        r.direction = (uint32_t)s->direction;
+        r.rtp_services = (uint32_t)s->rtp_services;
+        r.rtcp_services = (uint32_t)s->rtcp_services;
+        r.allow_repeat_tx = s->allow_repeat_tx;
+        r.use_mki = s->use_mki;
+        r.mki_size = (uint32_t)s->mki_size;
+        r.window_size = (uint32_t)s->window_size;
+        r.bits = (uint32_t)s->rdbx.bits;
+        r.pending_roc = s->rdbx.pending_roc;
+        r.rtcp_start = s->rtcp_start;
+        memcpy(r.rtcp_bm, s->rtcp_bm, sizeof r.rtcp_bm);
+        r.index = s->rdbx.index;
+        memcpy(p, &r, sizeof r);
+        p += sizeof r;
+        memcpy(p, s->rdbx.w, s->rdbx.bits / 8);
+        p += s->rdbx.bits / 8;
+    }
+    free(ref);
+    if (srtp_gpu_get_keys(ctx->gpu, nslots, (srtp_dev_key_t *)p)) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        return srtp_err_status_fail;
+    }
+    return srtp_err_status_ok;
+}
+
+/* bounds-checked reader over the blob */
+typedef struct {
+    const uint8_t *p, *end;
+} rep_rd_t;
+
+static int rep_take(rep_rd_t *r, void *dst, size_t n)
+{
+    if ((size_t)(r->end - r->p) < n)
+        return -1;
+    memcpy(dst, r->p, n);
+    r->p += n;
+    return 0;
+}
+
+static srtp_err_status_t rep_fill(srtp_t ctx, rep_rd_t *rd)
+{
+    rep_hdr_t h;
+    if (rep_take(rd, &h, sizeof h) || memcmp(h.magic, REP_MAGIC, 8) ||
+        h.total != (uint64_t)(rd->end - rd->p) + sizeof h ||
+        h.nstreams < (h.has_templ ? 1u : 0u))
+        return srtp_err_status_bad_param;
+    keyset_t **ks = (keyset_t **)calloc(h.nkeysets + 1, sizeof *ks);
+    uint8_t *used = (uint8_t *)calloc(h.nslots + 1, 1);
+    uint8_t *gh = (uint8_t *)calloc(h.nslots + 1, 1);
+    srtp_dev_key_t *recs = NULL;
+    srtp_err_status_t rc = srtp_err_status_bad_param;
+    if (!ks || !used || !gh)
+        goto out_alloc;
+    for (uint32_t k = 0; k < h.nkeysets; k++) {
+        uint32_t w[2];
+        if (rep_take(rd, w, sizeof w) || w[0] == 0 ||
+            w[0] > SRTP_MAX_NUM_MASTER_KEYS)
+            goto out;
+        ks[k] = (keyset_t *)calloc(1, sizeof(keyset_t));
+        if (!ks[k])
+            goto out_alloc;
+        ks[k]->n = w[0];
+        ks[k]->cryptex = (int)w[1];
+        for (uint32_t j = 0; j < w[0]; j++) {
+            rep_key_t r;
+            if (rep_take(rd, &r, sizeof r) || r.slot >= h.nslots ||
+                (r.rslot != 0xffffffffu && r.rslot >= h.nslots) ||
+                (r.xslot != 0xffffffffu && r.xslot >= h.nslots) ||
+                r.variant >= SRTP_VARIANT_V)
+                goto out;
+            hkey_t *hk = &ks[k]->k[j];
+            hk->slot = r.slot;
+            hk->cipher_type = r.cipher_type;
+            hk->family = r.family;
+            hk->rounds = r.rounds;
+            hk->variant = r.variant;
+            hk->tag_len = r.tag_len;
+            hk->rslot = r.rslot;
+            hk->rtag_len = r.rtag_len;
+            hk->rgcm = (int)r.rgcm;
+            hk->xslot = r.xslot;
+            hk->limit_state = (int)r.limit_state;
+            hk->num_left = r.num_left;
+            memcpy(hk->mki, r.mki, sizeof hk->mki);
+            used[r.slot] = 1;
+            gh[r.slot] = r.family == SRTP_DEV_GCM;
+            if (r.rslot != 0xffffffffu)
+                used[r.rslot] = 1;
+            if (r.xslot != 0xffffffffu)
+                used[r.xslot] = 1;
+            ctx->variant_mask |= 1u << r.variant;
+        }
+    }
+    /* the key records keep their slot numbers: the session's next_slot is
+     * the exporter's, the slots no key set uses are free */
+    ctx->next_slot = h.nslots;
+    for (uint32_t s = 0; s < h.nslots; s++)
+        if (!used[s])
+            free_slot_now(ctx, s);
+    for (uint32_t i = 0; i < h.nstreams; i++) {
+        rep_stream_t r;
+        if (rep_take(rd, &r, sizeof r) || r.keyset >= h.nkeysets ||
+            r.bits == 0 || (r.bits & 31) || r.bits > 0x8000 ||
+            r.mki_size > SRTP_MAX_MKI_LEN)
+            goto out;
+        srtp_stream_ctx_t *s = (srtp_stream_ctx_t *)calloc(1, sizeof *s);
+        if (!s || rdbx_init(&s->rdbx, r.bits)) {
+            free(s);
+            rc = srtp_err_status_alloc_fail;
+            goto out;
+        }
+        s->ssrc = r.ssrc;
+        s->direction = (int)r.direction;
+        s->rtp_services = (int)r.rtp_services;
+        s->rtcp_services = (int)r.rtcp_services;
+        s->allow_repeat_tx = r.allow_repeat_tx != 0;
+        s->use_mki = r.use_mki != 0;
+        s->mki_size = r.mki_size;
+        s->window_size = r.window_size;
+        s->rdbx.index = r.index;
+        s->rdbx.pending_roc = r.pending_roc;
+        s->rtcp_start = r.rtcp_start;
+        memcpy(s->rtcp_bm, r.rtcp_bm, sizeof s->rtcp_bm);
+        s->keys = ks[r.keyset];
+        s->keys->refs++;
+        if (rep_take(rd, s->rdbx.w, r.bits / 8)) {
+            stream_free(ctx, s);
+            goto out;
+        }
+        if (h.has_templ && i + 1 == h.nstreams) {
+            ctx->templ = s;
+        } else if (list_insert(ctx, s)) {
+            stream_free(ctx, s);
+            rc = srtp_err_status_alloc_fail;
+            goto out;
+        }
+    }
+    /* key sets no stream references would leak: a blob never holds one */
+    for (uint32_t k = 0; k < h.nkeysets; k++)
+        if (ks[k]->refs == 0)
+            goto out;
+    recs = (srtp_dev_key_t *)malloc((size_t)h.nslots * sizeof *recs + 1);
+    if (!recs) {
+        rc = srtp_err_status_alloc_fail;
+        goto out;
+    }
+    if (rep_take(rd, recs, (size_t)h.nslots * sizeof *recs) || rd->p != rd->end)
+        goto out;
+    for (uint32_t s = 0; s < h.nslots; s++)
+        if (gh[s] && recs[s].ghash_slot != s)
+            goto out;
+    if (srtp_gpu_put_keys(ctx->gpu, h.nslots, recs, gh)) {
+        log_msg(srtp_log_level_error, srtp_gpu_last_error());
+        rc = srtp_err_status_init_fail;
+        goto out;
+    }
+    rc = srtp_err_status_ok;
+    goto done;
+out:
+out_alloc:
+    if (rc == srtp_err_status_ok)
+        rc = srtp_err_status_alloc_fail;
+    /* key sets without a stream are freed here, the rest with the streams */
+    for (uint32_t k = 0; ks && k < h.nkeysets; k++)
+        if (ks[k] && ks[k]->refs == 0)
+            free(ks[k]);
+done:
+    free(recs);
+    free(ks);
+    free(used);
+    free(gh);
+    return rc;
+}
+
+srtp_err_status_t srtp_mi355x_session_import(srtp_t *session, const void *blob,
+                                             size_t len)
+{
+    if (!session || !blob)
+        return srtp_err_status_bad_param;
+    *session = NULL;
+    srtp_t ctx;
+    srtp_err_status_t st = srtp_create(&ctx, NULL);
+    if (st)
+        return st;
+    rep_rd_t rd = { (const uint8_t *)blob, (const uint8_t *)blob + len };
+    st = rep_fill(ctx, &rd);
+    if (st) {
+        srtp_dealloc(ctx);
+        return st;
+    }
+    *session = ctx;
+    return srtp_err_status_ok;
+}
+
+/* RCCL, resolved at run time: whatever the process already links (the
+ * caller's communicator must come from that library), else librccl.so.1 */
+
+typedef int (*rccl_bcast_fn)(const void *, void *, size_t, int, int, void *,
+                             void *);
+typedef int (*rccl_rank_fn)(void *, int *);
+typedef const char *(*rccl_err_fn)(int);
+
+static void *rccl_sym(const char *name)
+{
+    void *f = dlsym(RTLD_DEFAULT, name);
+    if (f)
+        return f;
+    /* a copy already loaded privately (PyTorch's bundled librccl.so, the
+     * one its communicators come from), else ROCm's */
+    static void *h;
+    if (!h)
+        h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (!h)
+        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h)
+        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    return h ? dlsym(h, name) : NULL;
+}
+
+srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
+                                                void *nccl_comm, int root,
+                                                void *stream)
+{
+    enum { NCCL_UINT8 = 1 }; /* rccl.h ncclDataType_t ncclUint8 */
+    if (!session || !nccl_comm)
+        return srtp_err_status_bad_param;
+    rccl_bcast_fn bcast = (rccl_bcast_fn)rccl_sym("ncclBroadcast");
+    rccl_rank_fn urank = (rccl_rank_fn)rccl_sym("ncclCommUserRank");
+    rccl_err_fn estr = (rccl_err_fn)rccl_sym("ncclGetErrorString");
+    if (!bcast || !urank) {
+        log_msg(srtp_log_level_error, "session broadcast: RCCL not found\n");
+        return srtp_err_status_init_fail;
+    }
+    int rank = -1;
+    if (urank(nccl_comm, &rank))
+        return srtp_err_status_bad_param;
+    const int is_root = rank == root;
+    if (is_root && !*session)
+        return srtp_err_status_bad_param;
+    srtp_err_status_t st = srtp_err_status_ok;
+    uint64_t hlen = 0;
+    size_t blen = 0;   /* bytes of blob to wipe */
+    uint8_t *blob = NULL, *dblob = NULL;
+    uint64_t *dlen = (uint64_t *)srtp_gpu_malloc(sizeof(uint64_t));
+    if (!dlen)
+        return srtp_err_status_alloc_fail;
+    if (is_root) {
+        size_t n = 0;
+        st = srtp_mi355x_session_export(*session, NULL, 0, &n);
+        blob = st ? NULL : (uint8_t *)malloc(n);
+        blen = blob ? n : 0;
+        if (!st && !blob)
+            st = srtp_err_status_alloc_fail;
+        if (!st)
+            st = srtp_mi355x_session_export(*session, blob, n, &n);
+        /* a failed export still broadcasts (length 0) so that no rank is
+         * left waiting in the collective */
+        hlen = st ? 0 : n;
+    }
+    int nr = 0;
+    if (srtp_gpu_h2d(NULL, dlen, &hlen, sizeof hlen, stream) ||
+        (nr = bcast(dlen, dlen, sizeof hlen, NCCL_UINT8, root, nccl_comm,
+                    stream)) ||
+        srtp_gpu_d2h(NULL, &hlen, dlen, sizeof hlen, stream) ||
+        srtp_gpu_sync(NULL, stream)) {
+        st = srtp_err_status_fail;
+        goto out;
+    }
+    if (!hlen) {
+        if (!st)
+            st = srtp_err_status_fail;   /* the root's export failed */
+        goto out;
+    }
+    dblob = (uint8_t *)srtp_gpu_malloc(hlen);
+    if (!is_root) {
+        blob = (uint8_t *)malloc(hlen);
+        blen = blob ? hlen : 0;
+    }
+    if (!dblob || !blob) {
+        /* every rank must still take part: a rank that cannot allocate
+         * leaves the others in the collective, so this is fatal for the
+         * communicator, as any RCCL allocation failure is */
+        st = srtp_err_status_alloc_fail;
+        goto out;
+    }
+    if ((is_root && srtp_gpu_h2d(NULL, dblob, blob, hlen, stream)) ||
+        (nr = bcast(dblob, dblob, hlen, NCCL_UINT8, root, nccl_comm, stream)) ||
+        (!is_root && srtp_gpu_d2h(NULL, blob, dblob, hlen, stream)) ||
+        srtp_gpu_sync(NULL, stream)) {
+        st = srtp_err_status_fail;
+        goto out;
+    }
+    if (!is_root)
+        st = srtp_mi355x_session_import(session, blob, hlen);
+out:
+    if (nr && estr) {
+        char m[160];
+        snprintf(m, sizeof m, "session broadcast: ncclBroadcast: %s\n",
+                 estr(nr));
+        log_msg(srtp_log_level_error, m);
+    }
+    if (blob) {
+        memset(blob, 0, blen);
+        free(blob);
+    }
+    srtp_gpu_free(dblob);
+    srtp_gpu_free(dlen);
+    return st;
 }

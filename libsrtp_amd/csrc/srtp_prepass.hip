@@ -897,10 +897,17 @@ constexpr uint64_t CH_AGG = 1ull << 62, CH_PRE = 2ull << 62,
                    CH_HAS = 1ull << 61, CH_FLAGS = 3ull << 62;
 // chain aggregate of a run of packets: has a chain packet, the first and
 // last chain packets' sequence numbers, the sum of the advances between
-// consecutive chain packets inside the run
+// consecutive chain packets inside the run.  The sum is 64-bit: one tile's
+// is below 2^27 (4095 advances < 2^15, the 29-bit field of a published
+// aggregate), but the look-back combines any number of tiles, and a valid
+// sender chain of large advances passes 2^32 after ~32 tiles.
 struct ChAgg {
-    uint32_t has, first, last, internal;
+    uint32_t has, first, last;
+    uint64_t internal;
 };
+static_assert(CH_TILE - 1 < (1 << 14), "a tile's advance sum fits 29 bits");
+// k_pp_chain1's look-back words are allocated per srtp_scan::TILE packets
+static_assert(CH_TILE >= srtp_scan::TILE, "ch_tile sized by srtp_scan::TILE");
 
 __device__ __forceinline__ ChAgg ch_none() { return ChAgg{ 0, 0, 0, 0 }; }
 
@@ -960,7 +967,7 @@ __device__ __forceinline__ uint64_t ch_pack_agg(const ChAgg &a)
 __device__ __forceinline__ ChAgg ch_unpack_agg(uint64_t v)
 {
     return ChAgg{ (v & CH_HAS) ? 1u : 0u, (uint32_t)(v >> 45) & 0xffffu,
-                  (uint32_t)(v >> 29) & 0xffffu, (uint32_t)v & 0x1fffffffu };
+                  (uint32_t)(v >> 29) & 0xffffu, v & 0x1fffffffull };
 }
 
 __device__ __forceinline__ ChAgg ch_shfl_down(const ChAgg &a, int d)
@@ -968,7 +975,7 @@ __device__ __forceinline__ ChAgg ch_shfl_down(const ChAgg &a, int d)
     return ChAgg{ (uint32_t)__shfl_down((int)a.has, d),
                   (uint32_t)__shfl_down((int)a.first, d),
                   (uint32_t)__shfl_down((int)a.last, d),
-                  (uint32_t)__shfl_down((int)a.internal, d) };
+                  (uint64_t)__shfl_down((long long)a.internal, d) };
 }
 
 // wave 0 of a tile: the published state of the tiles before it, 64 at a
@@ -1003,7 +1010,7 @@ __device__ void ch_lookback(const uint64_t *tile, uint32_t t, uint64_t stored,
         const ChAgg w{ (uint32_t)__shfl((int)a.has, 0),
                        (uint32_t)__shfl((int)a.first, 0),
                        (uint32_t)__shfl((int)a.last, 0),
-                       (uint32_t)__shfl((int)a.internal, 0) };
+                       (uint64_t)__shfl((long long)a.internal, 0) };
         suf = ch_combine(w, suf, bad);
         if (pm) {
             const uint64_t pv = (uint64_t)__shfl((long long)v, fl);
@@ -1020,7 +1027,7 @@ __device__ __forceinline__ ChAgg ch_shfl_up(const ChAgg &a, int d)
     return ChAgg{ (uint32_t)__shfl_up((int)a.has, d),
                   (uint32_t)__shfl_up((int)a.first, d),
                   (uint32_t)__shfl_up((int)a.last, d),
-                  (uint32_t)__shfl_up((int)a.internal, d) };
+                  (uint64_t)__shfl_up((long long)a.internal, d) };
 }
 
 // inclusive scan over the wave's lanes in lane order
@@ -1736,6 +1743,19 @@ static bool fused_on()
     return on;
 }
 
+// An error after k_pp_chain1 was queued: only k_pp_chain1_commit zeroes the
+// look-back words, the tile ticket / key-use counters and the next batch's
+// abort word, so they are zeroed here (else the next one-stream batch would
+// start from stale prefixes and a nonzero ticket).
+static int chain1_fail(PpState *P, hipStream_t stream)
+{
+    (void)hipMemsetAsync(P->ch_tile, 0, (P->ch_tiles_cap + 1) * 8, stream);
+    (void)hipMemsetAsync(P->ch_ctl, 0, 8, stream);
+    (void)hipMemsetAsync(P->ch_abort, 0, 8, stream);
+    (void)hipStreamSynchronize(stream);
+    return -1;
+}
+
 // the one-stream chain form in two launches (k_pp_chain1 + commit), then
 // the crypto kernels; see k_pp_chain1
 static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
@@ -1772,9 +1792,12 @@ static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     A.abort = ab;
     A.ntiles = nt;
     hipLaunchKernelGGL(k_pp_chain1, dim3(nt), dim3(CH_THREADS), 0, stream, A);
-    PPCHK(hipGetLastError());
+    if (const hipError_t le = hipGetLastError(); le != hipSuccess) {
+        pp_fail(le, "k_pp_chain1");
+        return chain1_fail(P, stream);
+    }
     if (pp_step(stream, "chain1"))
-        return -1;
+        return chain1_fail(P, stream);
     Chain1Commit K;
     K.pstat = P->pstat;
     K.olen = P->skey2;
@@ -1793,9 +1816,12 @@ static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     hipLaunchKernelGGL(k_pp_chain1_commit,
                        dim3((N + CH_COMMIT_THREADS - 1) / CH_COMMIT_THREADS),
                        dim3(CH_COMMIT_THREADS), 0, stream, K);
-    PPCHK(hipGetLastError());
+    if (const hipError_t le = hipGetLastError(); le != hipSuccess) {
+        pp_fail(le, "k_pp_chain1_commit");
+        return chain1_fail(P, stream);
+    }
     if (pp_step(stream, "chain1_commit"))
-        return -1;
+        return chain1_fail(P, stream);
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
     cb.in = b->in;

@@ -155,6 +155,11 @@ def lib():
         "srtp_mi355x_set_key_buckets": ([C.c_int], None),
         "srtp_mi355x_unprotect_stats": ([P] + [C.POINTER(C.c_uint32)] * 3,
                                         None),
+        "srtp_mi355x_session_export": ([P, P, S, SP], C.c_int),
+        "srtp_mi355x_session_import": ([C.POINTER(C.c_void_p), P, S],
+                                       C.c_int),
+        "srtp_mi355x_session_broadcast": ([C.POINTER(C.c_void_p), P, C.c_int,
+                                           P], C.c_int),
 
         "srtp_get_version_string": ([], C.c_char_p),
     }
@@ -236,6 +241,28 @@ class _PolicyHolder:
         self.policy = p
 
 
+def session_broadcast(sess, comm_ptr, root, stream=0):
+    """srtp_mi355x_session_broadcast over an RCCL communicator (ncclComm_t
+    address, e.g. torch's ProcessGroupNCCL._comm_ptr()): on rank `root`
+    `sess` is the session to replicate (returned as is), elsewhere pass None
+    and get the replica."""
+    L = lib()
+    st = L.srtp_init()
+    if st:
+        raise RuntimeError("srtp_init failed: %s" % Status(st).name)
+    h = C.c_void_p(sess.h.value if sess is not None else None)
+    st = L.srtp_mi355x_session_broadcast(C.byref(h), C.c_void_p(comm_ptr),
+                                         root, C.c_void_p(stream or None))
+    if st:
+        raise RuntimeError("session broadcast: %s" % Status(st).name)
+    if sess is not None:
+        return sess
+    out = Session.__new__(Session)
+    out.L = L
+    out.h = h
+    return out
+
+
 class EventData(C.Structure):
     """srtp_event_data_t (include/srtp.h:1690-1700)"""
     _fields_ = [("session", C.c_void_p), ("ssrc", C.c_uint32),
@@ -279,6 +306,38 @@ class Session:
                            C.byref(holders[0].policy) if holders else None)
         if st:
             raise RuntimeError("srtp_create failed: %s" % Status(st).name)
+
+    def export_blob(self):
+        """srtp_mi355x_session_export: the session's streams, derived
+        session keys and stream state as bytes (secret material)"""
+        n = C.c_size_t()
+        st = self.L.srtp_mi355x_session_export(self.h, None, 0, C.byref(n))
+        if st:
+            raise RuntimeError("session export: %s" % Status(st).name)
+        buf = C.create_string_buffer(n.value)
+        st = self.L.srtp_mi355x_session_export(self.h, buf, n.value,
+                                               C.byref(n))
+        if st:
+            raise RuntimeError("session export: %s" % Status(st).name)
+        return buf.raw[:n.value]
+
+    @classmethod
+    def from_blob(cls, blob):
+        """srtp_mi355x_session_import: a replica of the exported session on
+        the current HIP device"""
+        L = lib()
+        st = L.srtp_init()
+        if st:
+            raise RuntimeError("srtp_init failed: %s" % Status(st).name)
+        self = cls.__new__(cls)
+        self.L = L
+        self.h = C.c_void_p()
+        buf = C.create_string_buffer(bytes(blob), len(blob))
+        st = L.srtp_mi355x_session_import(C.byref(self.h), buf, len(blob))
+        if st:
+            self.h = C.c_void_p()
+            raise RuntimeError("session import: %s" % Status(st).name)
+        return self
 
     def add_stream(self, policy):
         h = _PolicyHolder(policy)

@@ -319,6 +319,42 @@ def test_device_api_vs_oracle(name):
             assert host2[offs2[i]:offs2[i] + olen2[i]] == ref, i
 
 
+def oracle_chunks(pol, orig, prot, rtp_len, trailer, seq0, chunk=65536):
+    """Compare every packet of a one-stream batch (rows of orig / prot, the
+    stream's packets in order from sequence number seq0, ROC 0) with the C
+    oracle: chunks of 2^16 packets run on host threads, each on an oracle
+    session whose stream is seated at the chunk's ROC by
+    srtp_stream_set_roc (the sender's pending ROC, srtp.c:2069-2071) -- a
+    chunk starting at sequence number seq0 with ROC >= 1.  Returns the
+    mismatching packet numbers."""
+    import concurrent.futures as cf
+    import numpy as np
+    n, slot = orig.shape
+    assert chunk % 65536 == 0 and n % chunk == 0
+    out_len = rtp_len + trailer
+    sessions = []
+    for c in range(n // chunk):
+        o = O.Session([pol])
+        roc = (seq0 + c * chunk) >> 16
+        if roc:
+            assert o.set_roc(pol["ssrc"], roc) == 0
+        sessions.append(o)
+
+    def one(c):
+        lo = c * chunk
+        part = np.ascontiguousarray(orig[lo:lo + chunk])
+        offs = np.arange(chunk, dtype=np.uint64) * np.uint64(slot)
+        lens = np.full(chunk, rtp_len, dtype=np.uint32)
+        nbad, exp, olen = sessions[c].protect_many(part.reshape(-1), offs,
+                                                   lens, slot)
+        assert nbad == 0 and (olen == out_len).all()
+        diff = (exp[:, :out_len] != prot[lo:lo + chunk, :out_len]).any(axis=1)
+        return [lo + int(i) for i in np.nonzero(diff)[0]]
+
+    with cf.ThreadPoolExecutor(max_workers=16) as ex:
+        return sum(ex.map(one, range(len(sessions))), [])
+
+
 @pytest.mark.parametrize("name,n,trailer", [
     ("icm128_hmac80", 65536, 10),
     ("icm128_hmac80", 1 << 20, 10),   # configs[1] at its own size
@@ -326,9 +362,10 @@ def test_device_api_vs_oracle(name):
     ("gcm256_16", 1 << 20, 16),       # configs[2] at its own size
 ])
 def test_large_uniform_batch_roundtrip(name, n, trailer):
-    """n x 1400 B through the device API (the bench shape): protect ->
-    unprotect must restore every packet; a prefix is compared byte-for-byte
-    with the oracle."""
+    """n x 1400 B through the device API (the bench shape): every protected
+    packet is compared byte-for-byte with the C oracle (at 2^20 packets ROC
+    0 .. 16 across every CU's waves), and protect -> unprotect must restore
+    every packet."""
     _gpu()
     import torch
     payload = 1400
@@ -358,11 +395,10 @@ def test_large_uniform_batch_roundtrip(name, n, trailer):
     assert int(st.abs().sum()) == 0
     assert bool((cap == 12 + payload + trailer).all())
     prot = d.cpu().reshape(n, slot)
-    # the oracle, in order, on a prefix
-    orc2 = O.Session([pol])
-    for i in range(2000):
-        rc, ref = orc2.protect(bytes(orig[i, :12 + payload].numpy()), slot)
-        assert rc == 0 and bytes(prot[i, :len(ref)].numpy()) == ref, i
+    # every packet against the oracle (ROC 0 .. 16 at n = 2^20)
+    bad = oracle_chunks(pol, orig.numpy(), prot.numpy(), 12 + payload,
+                        trailer, 0x1234)
+    assert bad == [], bad[:5]
     # ciphertext differs from the plaintext everywhere but the header
     assert not torch.equal(prot[:, 12:12 + payload], orig[:, 12:12 + payload])
     del prot
