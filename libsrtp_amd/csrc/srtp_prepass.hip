@@ -42,6 +42,7 @@
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "srtp_dev.h"
 #include "srtp_rtp_hdr.h"
@@ -105,6 +106,15 @@ struct PpState {
     uint32_t *ch_abort = nullptr;
     uint32_t ch_par = 0;
     size_t ch_tiles_cap = 0;
+    // one-stream unprotect (k_pu_chain1 .. k_pu_commit1): two control blocks
+    // used in turn, the look-back words of its two scans, the generation-
+    // tagged first-authenticated-position array and its generation
+    struct PuCtl *pu_ctl = nullptr;
+    uint32_t pu_par = 0;
+    uint64_t *pu_tile = nullptr;   // 2 x (ch_tiles_cap + 1) words
+    unsigned long long *pu_first = nullptr;
+    uint64_t pu_first_cap = 0;
+    uint32_t pu_gen = 0;
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -1291,6 +1301,624 @@ __global__ __launch_bounds__(CH_COMMIT_THREADS) void k_pp_chain1_commit(Chain1Co
 }
 
 // ---------------------------------------------------------------------------
+// Unprotect of ONE stream in order or not: the receiver's batch with network
+// reordering, duplicates, late and forged packets stays on the device.  The
+// reference walks the packets in order (srtp.c:2884-2903 estimate and
+// replay check, 3157-3167 replay add after the tag check; rdbx.c:112-145,
+// 227-270):
+//   est_k  = index_guess(T_{k-1}, seq_k), T = highest ACCEPTED index so far
+//            (the stored index before the batch)
+//   replay = est_k <= T_{k-1} and (T_{k-1} - est_k >= window bits: old, or
+//            est_k's bit set: an earlier accepted packet had that index)
+// In batch form:
+//   k_pu_chain1    parse, classify (k_pu_classify's checks), and u_k for
+//                  every candidate: the stored index's guess for the first
+//                  one plus the SIGNED 16-bit advances (-2^15, 2^15) between
+//                  consecutive candidates -- k_pp_chain1's single-pass
+//                  look-back scan with signed sums
+//   crypto         every candidate's tag verdict, speculative decryption
+//   k_pu_first     (only when some advance was <= 0) the first authenticated
+//                  position of every index: duplicates
+//   k_pu_verdict1  a second look-back scan, max over the AUTHENTICATED u,
+//                  gives T_{k-1} (a replayed or old packet never raises it:
+//                  its index is at most T); the reference's estimate
+//                  index_guess(T_{k-1}, seq_k) must equal u_k -- else the
+//                  host decides -- and the verdict follows: replay_old,
+//                  replay_fail (stored window bit, or an earlier accepted
+//                  duplicate), auth_fail, accepted
+//   k_pu_commit1   statuses / lengths; block 0 the stream: index, window
+//                  (the stored one shifted, one bit per accepted packet in
+//                  it), key uses, direction; accepted packets leave the undo
+//                  set (meta cleared), the look-back state is reset
+//   undo           every other candidate's decryption is taken back
+// The first authenticated position uses a generation-tagged array (no reset
+// between batches): entry = (~gen << 32) | position, atomicMin keeps the
+// current batch's smallest position.
+constexpr uint32_t ST_AUTH_FAIL = 7, ST_REPLAY_FAIL = 9, ST_REPLAY_OLD = 10;
+
+// per-batch counters, two used in turn: a batch's commit kernel resets the
+// next batch's (every block of it still reads its own)
+struct PuCtl {
+    uint32_t t_chain, t_verdict;   // tile tickets (dispatch order)
+    uint32_t nonmono;              // some candidate advance was <= 0
+    uint32_t cand, replays, accepted;
+    uint32_t abort1;               // abort bits raised before the crypto
+    uint32_t abort2;               // ... and after it
+    unsigned long long umin, umax; // candidate indices of the batch
+};
+
+__device__ __forceinline__ void pu_ctl_reset(PuCtl &c)
+{
+    c.t_chain = c.t_verdict = 0;
+    c.nonmono = c.cand = c.replays = c.accepted = c.abort1 = c.abort2 = 0;
+    c.umin = ~0ull;
+    c.umax = 0;
+}
+
+// the signed advance between consecutive candidates, in [-2^15, 2^15)
+__device__ __forceinline__ uint64_t cs_adv(uint32_t from, uint32_t to,
+                                           uint32_t *nm)
+{
+    const int32_t d = (int32_t)((to - from + 32768u) & 0xffffu) - 32768;
+    if (d <= 0)
+        *nm = 1;
+    return (uint64_t)(int64_t)d;
+}
+
+__device__ __forceinline__ ChAgg cs_combine(const ChAgg &a, const ChAgg &b,
+                                            uint32_t *nm)
+{
+    if (!a.has)
+        return b;
+    if (!b.has)
+        return a;
+    return ChAgg{ 1, a.first, b.last,
+                  a.internal + cs_adv(a.last, b.first, nm) + b.internal };
+}
+
+// a tile aggregate's signed sum: |sum| < 4095 * 2^15 < 2^28 (29-bit field)
+__device__ __forceinline__ ChAgg cs_unpack_agg(uint64_t v)
+{
+    ChAgg a = ch_unpack_agg(v);
+    a.internal = (uint64_t)(((int64_t)(v << 35)) >> 35);
+    return a;
+}
+
+// prefix (has, u of the last candidate) followed by a run; u is kept in
+// 48 bits (an index below zero or past 2^48 sends the batch to the host)
+__device__ __forceinline__ void cs_apply(uint32_t &has, uint64_t &idx,
+                                         const ChAgg &a, uint64_t stored,
+                                         uint32_t *nm, uint32_t *bad)
+{
+    if (!a.has)
+        return;
+    if (has) {
+        idx += cs_adv((uint32_t)idx & 0xffffu, a.first, nm) + a.internal;
+    } else {
+        uint64_t e;
+        guess_index(stored, a.first, &e);
+        idx = e + a.internal;
+        has = 1;
+    }
+    if (idx >> 48)
+        *bad = 1;
+}
+
+__device__ __forceinline__ ChAgg cs_wave_scan(ChAgg a, uint32_t *nm)
+{
+    const int lane = threadIdx.x & 63;
+    for (int d = 1; d < 64; d <<= 1) {
+        const ChAgg o = ch_shfl_up(a, d);
+        if (lane >= d)
+            a = cs_combine(o, a, nm);
+    }
+    return a;
+}
+
+__device__ void cs_lookback(const uint64_t *tile, uint32_t t, uint64_t stored,
+                            uint32_t &has, uint64_t &idx, uint32_t *nm,
+                            uint32_t *bad)
+{
+    const int lane = threadIdx.x & 63;
+    ChAgg suf = ch_none();
+    has = 0;
+    idx = 0;
+    for (int64_t j0 = (int64_t)t - 1; j0 >= 0; j0 -= 64) {
+        const int64_t j = j0 - lane;
+        uint64_t v = CH_PRE;
+        if (j >= 0)
+            while (!((v = __hip_atomic_load(&tile[j], __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)) &
+                     CH_FLAGS))
+                __builtin_amdgcn_s_sleep(1);
+        const uint64_t pm = __ballot((v & CH_FLAGS) == CH_PRE);
+        const int fl = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
+        ChAgg a = lane < fl ? cs_unpack_agg(v) : ch_none();
+        for (int d = 1; d < 64; d <<= 1) {
+            const ChAgg o = ch_shfl_down(a, d);
+            if (lane + d < 64)
+                a = cs_combine(o, a, nm);
+        }
+        const ChAgg w{ (uint32_t)__shfl((int)a.has, 0),
+                       (uint32_t)__shfl((int)a.first, 0),
+                       (uint32_t)__shfl((int)a.last, 0),
+                       (uint64_t)__shfl((long long)a.internal, 0) };
+        suf = cs_combine(w, suf, nm);
+        if (pm) {
+            const uint64_t pv = (uint64_t)__shfl((long long)v, fl);
+            has = (pv & CH_HAS) ? 1u : 0u;
+            idx = pv & 0xffffffffffffull;
+            break;
+        }
+    }
+    cs_apply(has, idx, suf, stored, nm, bad);
+}
+
+struct PuChainArgs {
+    ClassifyArgs C;       // in, offsets, lengths, capacities, stream 0, map
+    uint8_t *auth;
+    uint64_t *tile;       // look-back words, zero at entry
+    PuCtl *ctl;           // this batch's, reset
+};
+
+__global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
+{
+    const ClassifyArgs &C = A.C;
+    __shared__ uint32_t s_tile, s_has, s_cand, s_abort, s_nm;
+    __shared__ uint64_t s_idx, s_min, s_max;
+    __shared__ ChAgg s_w[CH_THREADS / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) {
+        s_tile = atomicAdd(&A.ctl->t_chain, 1u);
+        s_cand = 0;
+        s_abort = 0;
+        s_nm = 0;
+        s_min = ~0ull;
+        s_max = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const srtp_dev_stream_t S = C.st[0];
+    const uint64_t stored = S.index;
+    const uint32_t tag = S.trailer;   // no MKI on this path
+    const uint32_t base = tile * CH_TILE + t * CH_ITEMS;
+    uint32_t bad = 0, nm = 0, abort = 0, chain = 0, cand = 0;
+    uint64_t off[CH_ITEMS];
+    uint32_t len[CH_ITEMS], cap[CH_ITEMS], code[CH_ITEMS], seq[CH_ITEMS];
+    srtp_dev_hdr_t hh[CH_ITEMS];
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        const uint32_t i = base + k < C.n ? base + k : C.n - 1;
+        off[k] = C.in_off[i];
+        len[k] = C.in_len[i];
+        cap[k] = C.cap[i];
+    }
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++)
+        hh[k] = srtp_parse_rtp(C.in + off[k], off[k], len[k]);
+    ChAgg mine = ch_none();
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        code[k] = 0;
+        seq[k] = 0;
+        if (base + k >= C.n)
+            continue;
+        const srtp_dev_hdr_t &h = hh[k];
+        // k_pu_classify's checks (srtp_host.c un_static; srtp.c:2905-2990)
+        if (h.enc_start >> 24) {
+            code[k] = h.enc_start >> 24;
+        } else if (h.ssrc != S.ssrc) {
+            abort |= AB_UNKNOWN_SSRC;
+        } else {
+            if (!(S.flags & SRTP_DS_RX_ELIGIBLE) || (S.dir & SRTP_DIR_TX))
+                abort |= AB_INELIGIBLE;
+            const uint32_t L = len[k];
+            if (L < tag || h.enc_start > L - tag ||
+                ((S.flags & SRTP_DS_AEAD) && L - h.enc_start < tag) ||
+                cap[k] < L - tag ||
+                ((S.flags & SRTP_DS_ICM_CONF) &&
+                 (L - tag - h.enc_start + 15) / 16 > 0xffffu)) {
+                abort |= AB_STATIC;
+            } else {
+                chain |= 1u << k;
+                cand++;
+                seq[k] = h.seq_len & 0xffffu;
+                mine = cs_combine(mine, ChAgg{ 1, seq[k], seq[k], 0 }, &nm);
+            }
+        }
+    }
+    const ChAgg incl = cs_wave_scan(mine, &nm);
+    ChAgg lex = ch_shfl_up(incl, 1);
+    if (lane == 0)
+        lex = ch_none();
+    if (lane == 63)
+        s_w[wv] = incl;
+    __syncthreads();
+    if (t < 64) {
+        ChAgg a = t < CH_THREADS / 64 ? s_w[t] : ch_none();
+        a = cs_wave_scan(a, &nm);
+        if (t < CH_THREADS / 64)
+            s_w[t] = a;
+    }
+    __syncthreads();
+    const ChAgg wex = wv ? s_w[wv - 1] : ch_none();
+    const ChAgg excl = cs_combine(wex, lex, &nm);
+    const ChAgg tot = s_w[CH_THREADS / 64 - 1];
+    if (t == 0 && tile > 0)
+        __hip_atomic_store(&A.tile[tile], ch_pack_agg(tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (t < 64) {
+        uint32_t has = 0;
+        uint64_t idx = 0;
+        if (tile > 0)
+            cs_lookback(A.tile, tile, stored, has, idx, &nm, &bad);
+        if (t == 0) {
+            s_has = has;
+            s_idx = idx;
+            cs_apply(has, idx, tot, stored, &nm, &bad);
+            __hip_atomic_store(&A.tile[tile],
+                               CH_PRE | (has ? CH_HAS : 0) |
+                                   (idx & 0xffffffffffffull),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    uint32_t has = s_has;
+    uint64_t idx = s_idx;
+    cs_apply(has, idx, excl, stored, &nm, &bad);
+    uint64_t umin = ~0ull, umax = 0;
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        const uint32_t i = base + k;
+        if (i >= C.n)
+            break;
+        srtp_dev_meta_t m;
+        m.key = 0;
+        m.roc = 0;
+        m.len = 0;
+        m.info = 0xff0000u;   // no crypto
+        uint64_t e = 0;
+        if (chain >> k & 1) {
+            cs_apply(has, idx, ChAgg{ 1, seq[k], seq[k], 0 }, stored, &nm, &bad);
+            e = idx;
+            umin = e < umin ? e : umin;
+            umax = e > umax ? e : umax;
+            m.key = S.key;
+            m.roc = (uint32_t)(e >> 16);
+            m.info = hh[k].enc_start | (S.variant << 24);
+            m.len = hh[k].len - tag;
+        }
+        C.est[i] = e;
+        C.skey[i] = (chain >> k & 1) ? 0u : NOCHAIN;
+        C.pstat[i] = code[k];
+        C.meta[i] = m;
+        A.auth[i] = 1;   // kernels without a tag check leave it: accepted
+    }
+    if (bad)
+        abort |= AB_SEQUENCE;
+    if (abort)
+        atomicOr(&s_abort, abort);
+    if (nm)
+        s_nm = 1;
+    if (cand) {
+        atomicAdd(&s_cand, cand);
+        atomicMin((unsigned long long *)&s_min, (unsigned long long)umin);
+        atomicMax((unsigned long long *)&s_max, (unsigned long long)umax);
+    }
+    __syncthreads();
+    if (t == 0) {
+        if (s_abort)
+            atomicOr(&A.ctl->abort1, s_abort);
+        if (s_nm)
+            atomicOr(&A.ctl->nonmono, 1u);
+        if (s_cand) {
+            atomicAdd(&A.ctl->cand, s_cand);
+            atomicMin(&A.ctl->umin, (unsigned long long)s_min);
+            atomicMax(&A.ctl->umax, (unsigned long long)s_max);
+        }
+    }
+}
+
+// duplicates (non-monotone batches only): the first authenticated position
+// of every candidate index, generation-tagged (no reset between batches)
+__global__ void k_pu_first(const uint32_t *skey, const uint64_t *est,
+                           const uint8_t *auth, uint32_t n, PuCtl *ctl,
+                           unsigned long long *first, uint64_t cap,
+                           uint32_t gen)
+{
+    if (!ctl->nonmono || ctl->abort1)
+        return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t lo = ctl->umin, span = ctl->umax - ctl->umin + 1;
+    if (span > cap) {
+        if (i == 0)
+            atomicOr(&ctl->abort2, AB_ORDER);   // indices too spread: host
+        return;
+    }
+    if (i >= n || skey[i] != 0u || !auth[i])
+        return;
+    const unsigned long long tagv = ((unsigned long long)(~gen) << 32) | i;
+    atomicMin(&first[est[i] - lo], tagv);
+}
+
+struct PuVerdictArgs {
+    const uint32_t *skey;
+    const uint64_t *est;
+    const uint8_t *auth;
+    const unsigned long long *first;
+    const srtp_dev_stream_t *st;
+    const uint32_t *win;
+    uint32_t n;
+    uint64_t *tile;       // look-back words, zero at entry
+    PuCtl *ctl;
+    uint32_t *pstat;      // out: the verdict code of every candidate
+    uint64_t *top;        // out: T_k inclusive (highest authenticated)
+    uint32_t gen;         // k_pu_first's generation of this batch
+};
+
+__global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
+{
+    __shared__ uint32_t s_tile, s_rep, s_acc;
+    __shared__ uint64_t s_w[CH_THREADS / 64], s_pre;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    if (t == 0) {
+        s_tile = atomicAdd(&A.ctl->t_verdict, 1u);
+        s_rep = 0;
+        s_acc = 0;
+    }
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const srtp_dev_stream_t S = A.st[0];
+    const uint64_t stored = S.index;
+    const uint32_t bits = S.win_bits;
+    const bool nonmono = A.ctl->nonmono != 0;
+    const uint64_t lo = A.ctl->umin;
+    const uint32_t gen = A.gen;
+    const uint32_t base = tile * CH_TILE + t * CH_ITEMS;
+    uint64_t u[CH_ITEMS];
+    uint32_t cand = 0, au = 0;
+    // values are index + 1 so that 0 means "no authenticated packet"
+    uint64_t mx = 0;
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        const uint32_t i = base + k;
+        u[k] = 0;
+        if (i < A.n && A.skey[i] == 0u) {
+            cand |= 1u << k;
+            u[k] = A.est[i];
+            if (A.auth[i]) {
+                au |= 1u << k;
+                mx = u[k] + 1 > mx ? u[k] + 1 : mx;
+            }
+        }
+    }
+    // block max-scan: inclusive over lanes, waves through LDS
+    uint64_t incl = mx;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t o = (uint64_t)__shfl_up((long long)incl, d);
+        if (lane >= d)
+            incl = o > incl ? o : incl;
+    }
+    uint64_t lex = (uint64_t)__shfl_up((long long)incl, 1);
+    if (lane == 0)
+        lex = 0;
+    if (lane == 63)
+        s_w[wv] = incl;
+    __syncthreads();
+    uint64_t wex = 0, tot = 0;
+    for (int w = 0; w < CH_THREADS / 64; w++) {
+        if (w == wv)
+            wex = tot;
+        tot = s_w[w] > tot ? s_w[w] : tot;
+    }
+    // look-back words: [63:62] 1 aggregate / 2 inclusive prefix, [48:0]
+    // max authenticated index + 1 (0: none)
+    if (t == 0 && tile > 0)
+        __hip_atomic_store(&A.tile[tile], CH_AGG | tot, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (t < 64) {
+        uint64_t pre = 0;
+        for (int64_t j0 = (int64_t)tile - 1; j0 >= 0; j0 -= 64) {
+            const int64_t j = j0 - lane;
+            uint64_t v = CH_PRE;
+            if (j >= 0)
+                while (!((v = __hip_atomic_load(&A.tile[j], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT)) &
+                         CH_FLAGS))
+                    __builtin_amdgcn_s_sleep(1);
+            const uint64_t pm = __ballot((v & CH_FLAGS) == CH_PRE);
+            const int fl = pm ? __ffsll((unsigned long long)pm) - 1 : 64;
+            uint64_t a = lane <= fl ? (v & ~CH_FLAGS) : 0;
+            for (int m = 1; m < 64; m <<= 1) {
+                const uint64_t o = (uint64_t)__shfl_xor((long long)a, m);
+                a = o > a ? o : a;
+            }
+            pre = a > pre ? a : pre;
+            if (pm)
+                break;
+        }
+        if (t == 0) {
+            s_pre = pre;
+            __hip_atomic_store(&A.tile[tile], CH_PRE | (pre > tot ? pre : tot),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    __syncthreads();
+    uint64_t run = s_pre > wex ? s_pre : wex;
+    run = lex > run ? lex : run;
+    uint32_t bad = 0, rep = 0, acc = 0;
+#pragma unroll
+    for (int k = 0; k < CH_ITEMS; k++) {
+        const uint32_t i = base + k;
+        if (!(cand >> k & 1))
+            continue;
+        // T_{k-1}: the stored index or the highest authenticated before
+        const uint64_t T = run > stored + 1 ? run - 1 : stored;
+        uint64_t g;
+        guess_index(T, (uint32_t)u[k] & 0xffffu, &g);
+        if (g != u[k])
+            bad = 1;   // the reference estimates this packet differently
+        uint32_t v;
+        if (u[k] > T) {
+            v = (au >> k & 1) ? 0u : ST_AUTH_FAIL;
+        } else if (T - u[k] >= bits) {
+            v = ST_REPLAY_OLD;
+        } else {
+            bool seen = false;
+            if (u[k] <= stored) {
+                // the stored window (rdbx.c:227-243): bit (bits-1) = stored
+                const uint32_t bit = bits - 1 - (uint32_t)(stored - u[k]);
+                seen = (A.win[S.win_off + (bit >> 5)] >> (bit & 31)) & 1u;
+            }
+            if (!seen && nonmono) {
+                const unsigned long long f = A.first[u[k] - lo];
+                seen = (uint32_t)(f >> 32) == ~gen && (uint32_t)f < i;
+            }
+            v = seen ? ST_REPLAY_FAIL : (au >> k & 1) ? 0u : ST_AUTH_FAIL;
+        }
+        if (v == ST_REPLAY_FAIL || v == ST_REPLAY_OLD)
+            rep++;
+        if (v == 0)
+            acc++;
+        if (au >> k & 1)
+            run = u[k] + 1 > run ? u[k] + 1 : run;
+        A.pstat[i] = v;
+        A.top[i] = run > stored + 1 ? run - 1 : stored;
+    }
+    if (bad)
+        atomicOr(&A.ctl->abort2, AB_ORDER);
+    if (rep)
+        atomicAdd(&s_rep, rep);
+    if (acc)
+        atomicAdd(&s_acc, acc);
+    __syncthreads();
+    if (t == 0) {
+        if (s_rep)
+            atomicAdd(&A.ctl->replays, s_rep);
+        if (s_acc)
+            atomicAdd(&A.ctl->accepted, s_acc);
+    }
+}
+
+struct PuCommitArgs {
+    const uint32_t *skey, *pstat, *in_len;
+    const uint64_t *est, *top;
+    uint32_t n;
+    srtp_dev_stream_t *st;
+    uint32_t *win;
+    uint64_t *tile, *vtile;
+    uint32_t ntiles;
+    PuCtl *ctl, *ctl_next;
+    uint32_t *pub;
+    srtp_dev_meta_t *meta;
+    int32_t *status;
+    uint32_t *out_len;
+};
+
+__global__ __launch_bounds__(CH_COMMIT_THREADS) void k_pu_commit1(PuCommitArgs A)
+{
+    // ab1: before the crypto (it ran on nothing), ab2: after it (every
+    // candidate's decryption is undone)
+    const uint32_t ab1 = A.ctl->abort1, ab2 = A.ctl->abort2, ab = ab1 | ab2;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const srtp_dev_stream_t S0 = A.st[0];
+    if (i < A.n && ab1)
+        A.meta[i].info = 0xff0000u;   // nothing ran: nothing to undo
+    if (i < A.n && !ab) {
+        if (A.skey[i] != 0u) {
+            A.status[i] = (int32_t)A.pstat[i];   // header errors: no stream
+        } else {
+            const uint32_t v = A.pstat[i];
+            A.status[i] = (int32_t)v;
+            if (v == 0) {
+                A.out_len[i] = A.in_len[i] - S0.trailer;
+                A.meta[i].info = 0xff0000u;      // accepted: nothing to undo
+            }
+        }
+    }
+    if (blockIdx.x != 0)
+        return;
+    __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
+    __shared__ uint32_t s_stop;
+    srtp_dev_stream_t &S = A.st[0];
+    const uint64_t old = S.index;
+    const uint32_t words = S.win_bits >> 5;
+    uint64_t hi = old;
+    if (A.ntiles) {
+        const uint64_t last = A.vtile[A.ntiles - 1] & ~CH_FLAGS;
+        if (last && last - 1 > hi)
+            hi = last - 1;
+    }
+    const uint32_t acc = A.ctl->accepted;
+    if (!ab && acc) {
+        // the stored window shifted to the new top (rdbx_add), then the
+        // accepted packets' bits inside it; the highest authenticated index
+        // T_k never decreases along the batch, so the walk back from the
+        // end stops at the first packet with T_k below the window
+        const uint64_t adv = hi - old;
+        const uint32_t *w = A.win + S.win_off;
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x) {
+            uint32_t v = 0;
+            if (adv < S.win_bits) {
+                const uint32_t b0 = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+                const uint32_t a = x + b0 < words ? w[x + b0] : 0u;
+                const uint32_t b = x + b0 + 1 < words ? w[x + b0 + 1] : 0u;
+                v = bi ? (a >> bi) | (b << (32 - bi)) : a;
+            }
+            s_win[x] = v;
+        }
+        if (threadIdx.x == 0)
+            s_stop = 0;
+        __syncthreads();
+        for (int64_t c = (int64_t)A.n - 1; c >= 0; c -= blockDim.x) {
+            const int64_t j = c - (int64_t)threadIdx.x;
+            if (j >= 0 && A.skey[j] == 0u) {
+                if (hi - A.top[j] >= S.win_bits) {
+                    s_stop = 1;
+                } else if (A.pstat[j] == 0) {
+                    const uint64_t e = A.est[j];
+                    if (hi - e < S.win_bits) {
+                        const uint32_t bit =
+                            S.win_bits - 1 - (uint32_t)(hi - e);
+                        atomicOr(&s_win[bit >> 5], 1u << (bit & 31));
+                    }
+                }
+            }
+            __syncthreads();
+            const uint32_t stop = s_stop;
+            __syncthreads();
+            if (stop)
+                break;
+        }
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x)
+            A.win[S.win_off + x] = s_win[x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!ab) {
+            // key usage: AES-GCM every candidate that passed the replay
+            // check (srtp_unprotect_aead counts before the tag), AES-ICM /
+            // HMAC the accepted ones
+            S.uses += (S.flags & SRTP_DS_AEAD)
+                          ? A.ctl->cand - A.ctl->replays
+                          : acc;
+            if (acc) {
+                S.dir |= SRTP_DIR_RX;
+                S.index = hi;
+            }
+        }
+        if (A.pub)
+            __hip_atomic_store(A.pub, ab, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        pu_ctl_reset(*A.ctl_next);
+    }
+    for (uint32_t x = threadIdx.x; x < A.ntiles; x += blockDim.x) {
+        A.tile[x] = 0;
+        A.vtile[x] = 0;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Key buckets: a batch of many streams with distinct keys
 // is laid out for the crypto kernel as one bucket of records per stream, so
 // that a wave's 64 packets share one key (SGPR round keys, the four-table
@@ -1522,6 +2150,10 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
         PPCHK(hipFree(P->ch_tile));
     PPCHK(hipMalloc((void **)&P->ch_tile, (nt + 1) * 8));
     PPCHK(hipMemsetAsync(P->ch_tile, 0, (nt + 1) * 8, stream));
+    if (P->pu_tile)
+        PPCHK(hipFree(P->pu_tile));
+    PPCHK(hipMalloc((void **)&P->pu_tile, 2 * (nt + 1) * 8));
+    PPCHK(hipMemsetAsync(P->pu_tile, 0, 2 * (nt + 1) * 8, stream));
     PPCHK(hipStreamSynchronize(stream));
     P->ch_tiles_cap = nt;
     P->n_cap = c;
@@ -1543,7 +2175,8 @@ void srtp_gpu_pp_free(void *p)
                      P->perm, P->perm2, P->val, P->est, P->meta, P->agg,
                      P->hist, P->auth, P->top, P->abort, P->bk_off, P->bk_cur,
                      P->rec, P->rec_idx, P->bk_range, P->ch_tile,
-                     P->ch_ctl, P->ch_abort };
+                     P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
+                     P->pu_first };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -1583,6 +2216,11 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
         PPCHK(hipMalloc((void **)&P->ch_abort, 8));
         PPCHK(hipMemset(P->ch_ctl, 0, 8));
         PPCHK(hipMemset(P->ch_abort, 0, 8));
+        PPCHK(hipMalloc((void **)&P->pu_ctl, 2 * sizeof(PuCtl)));
+        PuCtl h[2];
+        memset(h, 0, sizeof h);
+        h[0].umin = h[1].umin = ~0ull;
+        PPCHK(hipMemcpy(P->pu_ctl, h, sizeof h, hipMemcpyHostToDevice));
         PPCHK(hipHostMalloc((void **)&P->h_abort, 4,
                             hipHostMallocMapped | hipHostMallocCoherent));
         PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
@@ -2022,6 +2660,150 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     }
 }
 
+// an error after k_pu_chain1 was queued: both control blocks and the
+// look-back words back to their reset state (normally the commit's job)
+static int pu1_fail(PpState *P, hipStream_t stream)
+{
+    PuCtl h[2];
+    memset(h, 0, sizeof h);
+    h[0].umin = h[1].umin = ~0ull;
+    (void)hipMemcpyAsync(P->pu_ctl, h, sizeof h, hipMemcpyHostToDevice, stream);
+    (void)hipMemsetAsync(P->pu_tile, 0, 2 * (P->ch_tiles_cap + 1) * 8, stream);
+    (void)hipStreamSynchronize(stream);
+    return -1;
+}
+
+#define PU1CHK(x, what)                                                        \
+    do {                                                                       \
+        const hipError_t e_ = (x);                                             \
+        if (e_ != hipSuccess) {                                                \
+            pp_fail(e_, what);                                                 \
+            return pu1_fail(P, stream);                                        \
+        }                                                                      \
+    } while (0)
+
+// one stream: k_pu_chain1 -> crypto -> k_pu_first -> k_pu_verdict1 ->
+// k_pu_commit1 -> undo (see k_pu_chain1)
+static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
+                               srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                               int *fallback)
+{
+    const uint32_t N = (uint32_t)b->n;
+    const uint32_t nt = (N + CH_TILE - 1) / CH_TILE;
+    // duplicates' index range: up to 4 indices per packet plus a window
+    const uint64_t fcap = 4ull * N + 65536;
+    if (fcap > P->pu_first_cap) {
+        if (P->pu_first)
+            PPCHK(hipFree(P->pu_first));
+        P->pu_first = nullptr;
+        PPCHK(hipMalloc((void **)&P->pu_first, fcap * 8));
+        PPCHK(hipMemsetAsync(P->pu_first, 0xff, fcap * 8, stream));
+        P->pu_first_cap = fcap;
+    }
+    if (++P->pu_gen == 0) {   // generations wrapped: forget every entry
+        PPCHK(hipMemsetAsync(P->pu_first, 0xff, P->pu_first_cap * 8, stream));
+        P->pu_gen = 1;
+    }
+    PuCtl *ctl = P->pu_ctl + P->pu_par, *nxt = P->pu_ctl + (P->pu_par ^ 1);
+    P->pu_par ^= 1;
+    uint64_t *tile = P->pu_tile, *vtile = P->pu_tile + P->ch_tiles_cap + 1;
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    PuChainArgs A;
+    A.C.in = b->in;
+    A.C.in_off = b->in_off;
+    A.C.in_len = b->in_len;
+    A.C.cap = b->out_len;
+    A.C.st = P->st;
+    A.C.hkey = P->hkey;
+    A.C.hval = P->hval;
+    A.C.hmask = P->hcap - 1;
+    A.C.n = N;
+    A.C.hdr = P->hdr;
+    A.C.pstat = P->pstat;
+    A.C.skey = P->skey;
+    A.C.perm = P->perm;
+    A.C.bcount = P->bcount;
+    A.C.abort = nullptr;
+    A.C.est = P->est;
+    A.C.new_index = nullptr;
+    A.C.meta = P->meta;
+    A.C.olen = nullptr;
+    A.auth = P->auth;
+    A.tile = tile;
+    A.ctl = ctl;
+    hipLaunchKernelGGL(k_pu_chain1, dim3(nt), dim3(CH_THREADS), 0, stream, A);
+    PU1CHK(hipGetLastError(), "k_pu_chain1");
+    if (pp_step(stream, "pu_chain1"))
+        return pu1_fail(P, stream);
+    srtp_gpu_batch_t cb = {};
+    cb.n = b->n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;
+    cb.auth_ok = P->auth;
+    cb.uniform_key = b->uniform_key;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = &ctl->abort1;
+    if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "pu_crypto"))
+        return pu1_fail(P, stream);
+    const dim3 blk(256), gp((N + 255) / 256);
+    hipLaunchKernelGGL(k_pu_first, gp, blk, 0, stream, P->skey, P->est,
+                       P->auth, N, ctl, P->pu_first, P->pu_first_cap,
+                       P->pu_gen);
+    PuVerdictArgs V;
+    V.skey = P->skey;
+    V.est = P->est;
+    V.auth = P->auth;
+    V.first = P->pu_first;
+    V.st = P->st;
+    V.win = P->win;
+    V.n = N;
+    V.tile = vtile;
+    V.ctl = ctl;
+    V.pstat = P->pstat;
+    V.top = P->top;
+    V.gen = P->pu_gen;
+    hipLaunchKernelGGL(k_pu_verdict1, dim3(nt), dim3(CH_THREADS), 0, stream, V);
+    PU1CHK(hipGetLastError(), "k_pu_verdict1");
+    if (pp_step(stream, "pu_verdict1"))
+        return pu1_fail(P, stream);
+    PuCommitArgs K;
+    K.skey = P->skey;
+    K.pstat = P->pstat;
+    K.in_len = b->in_len;
+    K.est = P->est;
+    K.top = P->top;
+    K.n = N;
+    K.st = P->st;
+    K.win = P->win;
+    K.tile = tile;
+    K.vtile = vtile;
+    K.ntiles = nt;
+    K.ctl = ctl;
+    K.ctl_next = nxt;
+    K.pub = P->h_abort_dev;
+    K.meta = P->meta;
+    K.status = b->status;
+    K.out_len = b->out_len;
+    hipLaunchKernelGGL(k_pu_commit1,
+                       dim3((N + CH_COMMIT_THREADS - 1) / CH_COMMIT_THREADS),
+                       dim3(CH_COMMIT_THREADS), 0, stream, K);
+    PU1CHK(hipGetLastError(), "k_pu_commit1");
+    if (pp_step(stream, "pu_commit1"))
+        return pu1_fail(P, stream);
+    // rejected packets (every candidate after a post-crypto abort): their
+    // speculative decryption is undone
+    if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
+        return -1;
+    PPCHK(hipStreamSynchronize(stream));
+    *fallback = (int)*(volatile uint32_t *)P->h_abort;
+    b->sorted = 1;
+    return 0;
+}
+
 int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                           int *fallback)
 {
@@ -2044,8 +2826,10 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         const char *e = getenv("SRTP_PP_SORTED");
         return e && *e == '1';
     }();
-    // one stream: the chain form directly (a sender's batch usually holds
-    // more packets than the replay window); several: order-free first
+    // one stream: the fused chain form, in order or not (k_pu_chain1);
+    // several: order-free first, then the sorted chain form
+    if (ns == 1 && fused_on())
+        return pp_unprotect_chain1(g, P, b, stream, fallback);
     bool unordered = ns > 1 && !force_sorted;
     for (;;) {
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;

@@ -60,6 +60,11 @@ def lib():
         L.orc_get_roc.argtypes = [C.c_void_p, C.c_uint32,
                                   C.POINTER(C.c_uint32)]
         L.orc_set_roc.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        L.orc_unprotect_many.restype = None
+        L.orc_unprotect_many.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_void_p, C.c_void_p, C.c_uint32,
+                                         C.c_void_p]
         L.orc_protect_many.restype = C.c_size_t
         L.orc_protect_many.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p,
                                        C.c_void_p, C.c_void_p, C.c_void_p,
@@ -170,6 +175,25 @@ class Session:
             lens.ctypes.data, out.ctypes.data, ooff.ctypes.data,
             olen.ctypes.data, out_cap)
         return bad, out.reshape(len(lens), out_cap), olen
+
+    def unprotect_many(self, arena, offs, lens, out_cap):
+        """orc_unprotect_many: every packet at arena[offs[i]:+lens[i]], in
+        order; returns (statuses, outputs as an (n, out_cap) array, plaintext
+        lengths)"""
+        import numpy as np
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        offs = np.ascontiguousarray(offs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = len(lens)
+        ooff = np.arange(n, dtype=np.uint64) * np.uint64(out_cap)
+        out = np.zeros(n * out_cap, dtype=np.uint8)
+        olen = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.int32)
+        lib().orc_unprotect_many(self.h, n, arena.ctypes.data, offs.ctypes.data,
+                                 lens.ctypes.data, out.ctypes.data,
+                                 ooff.ctypes.data, olen.ctypes.data, out_cap,
+                                 st.ctypes.data)
+        return st, out.reshape(n, out_cap), olen
 
     def unprotect(self, srtp, cap):
         out = C.create_string_buffer(max(cap, len(srtp)) + 64)

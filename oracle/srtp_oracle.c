@@ -1323,3 +1323,20 @@ size_t orc_protect_many(orc_session_t *s, size_t n, const uint8_t *in,
     }
     return bad;
 }
+
+/* orc_unprotect over n packets in order (test infrastructure: the reference
+ * receive loop of test/rtp.c:104-149, one srtp_unprotect per packet):
+ * status[i] per packet, out_len[i] the plaintext length (0 on error) */
+void orc_unprotect_many(orc_session_t *s, size_t n, const uint8_t *in,
+                        const uint64_t *in_off, const uint32_t *in_len,
+                        uint8_t *out, const uint64_t *out_off,
+                        uint32_t *out_len, uint32_t out_cap, int32_t *status)
+{
+    for (size_t i = 0; i < n; i++) {
+        size_t len = out_cap;
+        int rc = orc_unprotect(s, in + in_off[i], in_len[i], out + out_off[i],
+                               &len);
+        status[i] = rc;
+        out_len[i] = rc ? 0 : (uint32_t)len;
+    }
+}

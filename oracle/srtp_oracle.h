@@ -111,6 +111,10 @@ size_t orc_protect_many(orc_session_t *s, size_t n, const uint8_t *in,
                         const uint64_t *in_off, const uint32_t *in_len,
                         uint8_t *out, const uint64_t *out_off,
                         uint32_t *out_len, uint32_t out_cap);
+void orc_unprotect_many(orc_session_t *s, size_t n, const uint8_t *in,
+                        const uint64_t *in_off, const uint32_t *in_len,
+                        uint8_t *out, const uint64_t *out_off,
+                        uint32_t *out_len, uint32_t out_cap, int32_t *status);
 
 #ifdef __cplusplus
 }
