@@ -22,7 +22,10 @@ namespace {
 
 // ---------------------------------------------------------------------------
 // AES-ICM + HMAC-SHA1 protect / unprotect: one lane per packet.
-constexpr int ICM_NB = 2;   // AES blocks interleaved per round in the steady state
+#ifndef ICM_NB_N
+#define ICM_NB_N 2
+#endif
+constexpr int ICM_NB = ICM_NB_N;   // AES blocks interleaved per round (steady state)
 constexpr int ICM_PF = 1;   // chunks of packet data loaded ahead (per-lane path)
 
 // per-packet constants of the chunk loop
@@ -42,28 +45,19 @@ struct IcmPkt {
     uint32_t cb[4];    // counter block, block counter (bytes 14..15) zero
 };
 
-// One 64-byte chunk b of a packet in its general form: header words that
-// are not encrypted, quads past the end of the data, the partial last quad
-// (kept in tailq, stored once after the chunk loop: a byte-wise store here,
-// unrolled per quad, costs ~65 VGPRs), and the ROC / terminator / length
-// words of the SHA-1 message tail (sha1.c srtp_sha1_final).  The keystream
-// blocks that any payload byte uses come from the counter cache inside the
-// first epoch (blocks 0..255), from full AES past it.
+// One 64-byte chunk b of a packet in its general form, given its four
+// input quads v (zero past the data): header words that are not encrypted,
+// the ROC / terminator / length words of the SHA-1 message tail (sha1.c
+// srtp_sha1_final); the output quads go to oq.  The keystream blocks that
+// any payload byte uses come from the counter cache inside the first epoch
+// (blocks 0..255), from full AES past it.
 template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
-DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
-                   const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
-                   uint32_t hst[5], uint32_t tailq[4], u32x4 (&oq)[4])
+DEV void icm_chunk_core(uint32_t b, const IcmPkt &p, const CtrCache &C,
+                        const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
+                        uint32_t hst[5], const u32x4 (&v)[4],
+                        u32x4 (&oq)[4])
 {
     const uint32_t q0 = 4 * b;
-    const uint8_t *ip = p.in + 16 * q0;
-    uint8_t *op = p.out + 16 * q0;
-    u32x4 v[4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        v[t] = u32x4{ 0, 0, 0, 0 };
-        if (q0 + t < p.nq)
-            v[t] = *(const u32x4 *)(ip + 16 * t);
-    }
     uint32_t ks[4][4];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
@@ -110,20 +104,11 @@ DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
                 if (4 * q + u < p.hw)
                     kk[u] = 0;   // header words are never encrypted
         }
-        uint32_t o[4] = { v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
-                          v[t].w ^ kk[3] };
-        oq[t] = u32x4{ o[0], o[1], o[2], o[3] };
-        if (16 * q + 16 <= p.L) {
-            *(u32x4 *)(op + 16 * t) = u32x4{ o[0], o[1], o[2], o[3] };
-        } else if (16 * q < p.L) {
-            // the one partial quad: stored after the loop
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                tailq[u] = o[u];
-        }
+        oq[t] = u32x4{ v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
+                       v[t].w ^ kk[3] };
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
+            wv[4 * t + u] = bswap(PROTECT ? oq[t][u] : v[t][u]);
             ks_prev[u] = ks[t][u];
         }
     }
@@ -141,6 +126,103 @@ DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
             }
         }
         sha1_compress(hst, wv);
+    }
+}
+
+// chunk b, one lane per packet: 16-byte loads and stores of the lane's own
+// packet.  The partial last quad is kept in tailq and stored once after the
+// chunk loop (a byte-wise store here, unrolled per quad, costs ~65 VGPRs).
+template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
+                   const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
+                   uint32_t hst[5], uint32_t tailq[4], u32x4 (&oq)[4])
+{
+    const uint32_t q0 = 4 * b;
+    const uint8_t *ip = p.in + 16 * q0;
+    uint8_t *op = p.out + 16 * q0;
+    u32x4 v[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        v[t] = u32x4{ 0, 0, 0, 0 };
+        if (q0 + t < p.nq)
+            v[t] = *(const u32x4 *)(ip + 16 * t);
+    }
+    icm_chunk_core<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, v,
+                                            oq);
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t q = q0 + t;
+        if (16 * q + 16 <= p.L) {
+            *(u32x4 *)(op + 16 * t) = oq[t];
+        } else if (16 * q < p.L) {
+            // the one partial quad: stored after the loop
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                tailq[u] = oq[t][u];
+        }
+    }
+}
+
+template <int J>
+DEV uint32_t qbcast32(uint32_t v)   // value of lane (L & ~3) + J
+{
+    return qperm<J | (J << 2) | (J << 4) | (J << 6)>(v);
+}
+
+// chunk b of a wave whose 64 packets all start 64-byte aligned (in and out)
+// and have the same number of chunks -- BASELINE configs[3]'s 172-byte
+// packets in 192-byte slots: every chunk of every packet moves in lane
+// quads.  Load instruction j: lanes 4m..4m+3 read chunk b of packet 16j+m
+// (64 contiguous bytes; quads past a packet's readable end, roundup16(len),
+// are not read); the 4x4 transpose hands each lane its own chunk; after the
+// crypto the output is transposed back and instruction j stores chunk b of
+// packet 16j+m: whole aligned 64-byte segments up to the packet's last full
+// quad, the partial quad as one dwordx1..3 store plus its odd bytes.
+template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
+DEV void icm_chunk_coop64(uint32_t b, const IcmPkt &p, const CtrCache &C,
+                          const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
+                          uint32_t hst[5])
+{
+    const uint32_t lq = threadIdx.x & 3, q = 4 * b + lq;
+    const uint64_t pin = (uint64_t)(uintptr_t)p.in;
+    const uint64_t pout = (uint64_t)(uintptr_t)p.out;
+    uint32_t Lj[4];
+    Lj[0] = qbcast32<0>(p.L);
+    Lj[1] = qbcast32<1>(p.L);
+    Lj[2] = qbcast32<2>(p.L);
+    Lj[3] = qbcast32<3>(p.L);
+    uint64_t ij[4];
+    ij[0] = qbcast64<0>(pin);
+    ij[1] = qbcast64<1>(pin);
+    ij[2] = qbcast64<2>(pin);
+    ij[3] = qbcast64<3>(pin);
+    u32x4 v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        v[j] = u32x4{ 0, 0, 0, 0 };
+        if (16 * q < Lj[j])
+            v[j] = *(gcptr)(uintptr_t)(ij[j] + 16 * q);
+    }
+    quad_transpose(v);
+    u32x4 o[4];
+    icm_chunk_core<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, v,
+                                            o);
+    quad_transpose(o);
+    uint64_t oj[4];
+    oj[0] = qbcast64<0>(pout);
+    oj[1] = qbcast64<1>(pout);
+    oj[2] = qbcast64<2>(pout);
+    oj[3] = qbcast64<3>(pout);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int rem = (int)Lj[j] - (int)(16 * q);
+        uint8_t *dst = (uint8_t *)(uintptr_t)(oj[j] + 16 * q);
+        if (rem >= 16) {
+            *(gptr)dst = o[j];
+        } else if (rem > 0) {
+            const uint32_t w[4] = { o[j].x, o[j].y, o[j].z, o[j].w };
+            store_words_partial(dst, w, rem);
+        }
     }
 }
 
@@ -424,83 +506,100 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
             C = ctr_cache<NR, TAB4>(p.cb, rk, T);
     }
     uint32_t b = 0;
-    for (; b < p.bclean && b < p.nb; b++)
-        icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst,
-                                           tailq, prev);
-
-    // steady chunks: full chunks whose blocks j = 4b+t-qoff stay in counter
-    // epoch 0 (j <= 255, 4 KiB of payload)
-    uint32_t se = p.L >> 6;
-    se = se < ((256 + p.qoff) >> 2) ? se : ((256 + p.qoff) >> 2);
-    if (b < se) {
-        bool coop = false;
-        if constexpr (KM != KM_LANE) {
-            // every lane of the wave active, 16-B aligned and in the same
-            // steady range / keystream shift: the cooperative path
-            const uint32_t al =
-                (uint32_t)(((uintptr_t)p.in | (uintptr_t)p.out) & 15);
-            coop = wave_uniform(b) && wave_uniform(se) && wave_uniform(p.s) &&
-                   wave_uniform(p.conf ? 1u : 0u) &&
-                   __builtin_amdgcn_ballot_w64(al == 0) == ~0ull;
-        }
-        if (coop) {
-            const uint64_t lq = 16 * (threadIdx.x & 3);
-            const uint64_t pin = (uint64_t)(uintptr_t)p.in;
-            const uint64_t seg0 = (uint64_t)(uintptr_t)p.out & ~63ull;
-            const uint32_t r0 = (uint32_t)(((uintptr_t)p.out >> 4) & 3);
-            CoopPtr cp;
-            cp.in[0] = (const uint8_t *)(uintptr_t)(qbcast64<0>(pin) + lq);
-            cp.in[1] = (const uint8_t *)(uintptr_t)(qbcast64<1>(pin) + lq);
-            cp.in[2] = (const uint8_t *)(uintptr_t)(qbcast64<2>(pin) + lq);
-            cp.in[3] = (const uint8_t *)(uintptr_t)(qbcast64<3>(pin) + lq);
-            cp.seg[0] = (uint8_t *)(uintptr_t)(qbcast64<0>(seg0) + lq);
-            cp.seg[1] = (uint8_t *)(uintptr_t)(qbcast64<1>(seg0) + lq);
-            cp.seg[2] = (uint8_t *)(uintptr_t)(qbcast64<2>(seg0) + lq);
-            cp.seg[3] = (uint8_t *)(uintptr_t)(qbcast64<3>(seg0) + lq);
-            switch (p.s) {
-            case 0:
-                icm_coop_run<0, NR, TAB4, AUTH, PROTECT>(
-                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
-                break;
-            case 1:
-                icm_coop_run<1, NR, TAB4, AUTH, PROTECT>(
-                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
-                break;
-            case 2:
-                icm_coop_run<2, NR, TAB4, AUTH, PROTECT>(
-                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
-                break;
-            default:
-                icm_coop_run<3, NR, TAB4, AUTH, PROTECT>(
-                    b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
-                break;
-            }
-        } else {
-            switch (p.s) {
-            case 0:
-                icm_steady_run<0, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
-                                                           ks_prev, hst);
-                break;
-            case 1:
-                icm_steady_run<1, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
-                                                           ks_prev, hst);
-                break;
-            case 2:
-                icm_steady_run<2, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
-                                                           ks_prev, hst);
-                break;
-            default:
-                icm_steady_run<3, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
-                                                           ks_prev, hst);
-                break;
-            }
-        }
+    // per-lane keys (many short packets: BASELINE configs[3]), every packet
+    // of the wave 64-byte aligned with as many chunks: the whole packet in
+    // lane quads (icm_chunk_coop64).  Not in the uniform-key kernels: the
+    // extra path costs them 13 spilled VGPRs.
+    bool all64 = false;
+    if constexpr (KM == KM_LANE) {
+        const uint32_t al64 =
+            (uint32_t)(((uintptr_t)p.in | (uintptr_t)p.out) & 63);
+        all64 = __builtin_amdgcn_ballot_w64(al64 == 0) == ~0ull &&
+                wave_uniform(p.nb);
     }
-    for (; b < p.nb; b++)
-        icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst,
-                                           tailq, prev);
-    if (p.L & 15)
-        store_words_partial(p.out + (p.L & ~15u), tailq, (int)(p.L & 15));
+    if (all64) {
+        for (; b < p.nb; b++)
+            icm_chunk_coop64<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev,
+                                                      hst);
+    } else {
+        for (; b < p.bclean && b < p.nb; b++)
+            icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst,
+                                               tailq, prev);
+
+        // steady chunks: full chunks whose blocks j = 4b+t-qoff stay in counter
+        // epoch 0 (j <= 255, 4 KiB of payload)
+        uint32_t se = p.L >> 6;
+        se = se < ((256 + p.qoff) >> 2) ? se : ((256 + p.qoff) >> 2);
+        if (b < se) {
+            bool coop = false;
+            if constexpr (KM != KM_LANE) {
+                // every lane of the wave active, 16-B aligned and in the same
+                // steady range / keystream shift: the cooperative path
+                const uint32_t al =
+                    (uint32_t)(((uintptr_t)p.in | (uintptr_t)p.out) & 15);
+                coop = wave_uniform(b) && wave_uniform(se) && wave_uniform(p.s) &&
+                       wave_uniform(p.conf ? 1u : 0u) &&
+                       __builtin_amdgcn_ballot_w64(al == 0) == ~0ull;
+            }
+            if (coop) {
+                const uint64_t lq = 16 * (threadIdx.x & 3);
+                const uint64_t pin = (uint64_t)(uintptr_t)p.in;
+                const uint64_t seg0 = (uint64_t)(uintptr_t)p.out & ~63ull;
+                const uint32_t r0 = (uint32_t)(((uintptr_t)p.out >> 4) & 3);
+                CoopPtr cp;
+                cp.in[0] = (const uint8_t *)(uintptr_t)(qbcast64<0>(pin) + lq);
+                cp.in[1] = (const uint8_t *)(uintptr_t)(qbcast64<1>(pin) + lq);
+                cp.in[2] = (const uint8_t *)(uintptr_t)(qbcast64<2>(pin) + lq);
+                cp.in[3] = (const uint8_t *)(uintptr_t)(qbcast64<3>(pin) + lq);
+                cp.seg[0] = (uint8_t *)(uintptr_t)(qbcast64<0>(seg0) + lq);
+                cp.seg[1] = (uint8_t *)(uintptr_t)(qbcast64<1>(seg0) + lq);
+                cp.seg[2] = (uint8_t *)(uintptr_t)(qbcast64<2>(seg0) + lq);
+                cp.seg[3] = (uint8_t *)(uintptr_t)(qbcast64<3>(seg0) + lq);
+                switch (p.s) {
+                case 0:
+                    icm_coop_run<0, NR, TAB4, AUTH, PROTECT>(
+                        b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                    break;
+                case 1:
+                    icm_coop_run<1, NR, TAB4, AUTH, PROTECT>(
+                        b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                    break;
+                case 2:
+                    icm_coop_run<2, NR, TAB4, AUTH, PROTECT>(
+                        b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                    break;
+                default:
+                    icm_coop_run<3, NR, TAB4, AUTH, PROTECT>(
+                        b, se, p, C, rk, T, ks_prev, hst, prev, cp, r0);
+                    break;
+                }
+            } else {
+                switch (p.s) {
+                case 0:
+                    icm_steady_run<0, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                               ks_prev, hst);
+                    break;
+                case 1:
+                    icm_steady_run<1, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                               ks_prev, hst);
+                    break;
+                case 2:
+                    icm_steady_run<2, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                               ks_prev, hst);
+                    break;
+                default:
+                    icm_steady_run<3, NR, TAB4, AUTH, PROTECT>(b, se, p, C, rk, T,
+                                                               ks_prev, hst);
+                    break;
+                }
+            }
+        }
+        for (; b < p.nb; b++)
+            icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst,
+                                               tailq, prev);
+        if (p.L & 15)
+            store_words_partial(p.out + (p.L & ~15u), tailq, (int)(p.L & 15));
+    }
 
     const uint32_t tag_len = key->tag_len;
     const uint32_t mki_size = key->mki_size;
@@ -554,7 +653,10 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
 // 2.24 ms with four tables, MI355X A/B).  Persistent: the grid is sized to
 // the CUs and each workgroup walks the batch, so the tables are loaded once
 // per CU.
-constexpr int ICM_THREADS_UNI = 512;
+#ifndef ICM_THREADS_UNI_N
+#define ICM_THREADS_UNI_N 512
+#endif
+constexpr int ICM_THREADS_UNI = ICM_THREADS_UNI_N;
 constexpr int ICM_THREADS_LANE = 512;
 constexpr uint32_t ICM_SKIP = 0xffffffffu;
 
@@ -573,6 +675,12 @@ void k_icm_hmac(IcmArgs A)
         load_aes_tables<TAB4>(s_tab, s_t0);
     __syncthreads();
     const AesLds T = make_aes_lds(s_tab);
+#ifdef ICM_PRIO
+    // timing experiment: static priority for the second half of the waves
+    // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+    if ((threadIdx.x >> 6) >= (blockDim.x >> 7))
+        __builtin_amdgcn_s_setprio(1);
+#endif
 
     typename std::conditional<KM == KM_LANE, LaneKey<NRK>, UniKey<NRK>>::type rk;
     if (KM == KM_UNI && NR)
