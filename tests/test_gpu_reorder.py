@@ -142,3 +142,28 @@ def test_configs1_receive_1pct_reorder_01pct_dup():
     and 0.1 % duplicates stays on the device, bit-exact against the oracle"""
     _receive("icm128_hmac80", 1 << 20, 0x1234, 1, reorder=0.01, dup=0.001,
              old=0.0, forge=0.0, payloads=(160,))
+
+
+def test_host_buffer_unprotect_batch_on_device_prepass():
+    """srtp_unprotect_batch (per-packet host pointers, the socket receive
+    path of srtp.c:2820-3172 / test/rtp.c:104-149) gathers the batch into the
+    pinned staging arena and runs the device pre-pass: reordered, duplicated
+    and forged packets included, no host-path batch"""
+    _gpu()
+    pol = policy("icm128_hmac80", ssrc=SSRC, seed=5)
+    sent, slen = _sent(pol, 3000, 0xfff0, (0, 20, 160, 1200), 5)
+    arr = _network(3000, random.Random(5), 0.05, 0.01, 0.005, 0.01)
+    pk = []
+    for s, f in arr:
+        b = bytearray(sent[s, :slen[s]].tobytes())
+        if f:
+            b[-1] ^= 0x40
+        pk.append(bytes(b))
+    orc, lib = O.Session([pol]), L.Session([pol])
+    ref = [orc.unprotect(p, len(p)) for p in pk]
+    st, out = lib.unprotect_batch(pk)
+    for i, (rc, o) in enumerate(ref):
+        assert int(st[i]) == rc, (i, int(st[i]), rc)
+        if rc == 0:
+            assert out[i] == o, i
+    assert lib.prepass_stats() == (1, 0), lib.prepass_last_abort()

@@ -1,18 +1,23 @@
 /*
- * e2e_bench.c -- host-memory (PCIe-inclusive) rates of the protect path, for
- * DESIGN.md "End-to-end rate".  The packets start and end in host memory, as
- * they do behind a socket:
+ * e2e_bench.c -- host-memory (PCIe-inclusive) rates of the protect and
+ * unprotect paths, for DESIGN.md "End-to-end rate".  The packets start and
+ * end in host memory, as they do behind a socket:
  *
- *   batch   srtp_protect_batch() over per-packet host pointers (the libsrtp
- *           call shape: the library stages into pinned memory, copies H2D,
- *           runs the host pre-pass and the kernels, copies D2H and out)
+ *   batch   srtp_protect_batch() / srtp_unprotect_batch() over per-packet
+ *           host pointers (the libsrtp call shape: the library gathers into
+ *           pinned memory, copies H2D, runs the device pre-pass and the
+ *           kernels, copies D2H and scatters)
  *   pinned  the application keeps a pinned packet arena: hipMemcpyAsync H2D,
- *           srtp_protect_device() (GPU pre-pass + kernels), hipMemcpyAsync D2H
+ *           srtp_{un}protect_device() (GPU pre-pass + kernels),
+ *           hipMemcpyAsync D2H
  *   pipelined  the same arena in `chunks` pieces over three HIP streams:
- *           H2D(k+1) on a copy stream || protect(k) on the compute stream ||
- *           D2H(k-1) on a second copy stream (PCIe is full duplex)
+ *           H2D(k+1) on a copy stream || {un}protect(k) on the compute
+ *           stream || D2H(k-1) on a second copy stream (PCIe is full duplex)
  *
- *   usage: e2e_bench [packets] [payload] [iters] [chunks]
+ * For unprotect every timed batch is first protected (untimed) by a sender
+ * session on the device and copied to host memory.
+ *
+ *   usage: e2e_bench [packets] [payload] [iters] [chunks] [protect|unprotect]
  *   prints one JSON line.
  */
 #include <hip/hip_runtime_api.h>
@@ -81,13 +86,52 @@ static void fill(uint8_t *pk, size_t slot, size_t n, size_t len, uint32_t seq0)
     (void)len;
 }
 
+/* the sender side of the unprotect runs: n packets from seq0 protected on
+ * the device by `snd` (untimed), then copied to h_dst */
+typedef struct {
+    srtp_t snd;
+    uint8_t *d_arena;
+    uint64_t *d_off;
+    uint32_t *d_len, *d_cap;
+    int32_t *d_st;
+    hipStream_t st;
+} sender_t;
+
+static void produce(sender_t *S, uint8_t *h_dst, size_t n, size_t slot,
+                    size_t len, uint32_t seq0, const uint32_t *h_cap)
+{
+    fill(h_dst, slot, n, len, seq0);
+    CHECK(hipMemcpyAsync(S->d_arena, h_dst, n * slot, hipMemcpyHostToDevice,
+                         S->st));
+    CHECK(hipMemcpyAsync(S->d_cap, h_cap, n * 4, hipMemcpyHostToDevice, S->st));
+    srtp_device_batch_t b;
+    memset(&b, 0, sizeof b);
+    b.n = n;
+    b.in = S->d_arena;
+    b.in_off = S->d_off;
+    b.in_len = S->d_len;
+    b.out = S->d_arena;
+    b.out_off = S->d_off;
+    b.out_len = S->d_cap;
+    b.status = S->d_st;
+    b.stream = S->st;
+    CHECK(srtp_protect_device(S->snd, &b));
+    CHECK(hipMemcpyAsync(h_dst, S->d_arena, n * slot, hipMemcpyDeviceToHost,
+                         S->st));
+    CHECK(hipStreamSynchronize(S->st));
+}
+
 int main(int argc, char **argv)
 {
     size_t n = argc > 1 ? strtoul(argv[1], 0, 0) : (1u << 20);
     size_t payload = argc > 2 ? strtoul(argv[2], 0, 0) : 1400;
     int iters = argc > 3 ? atoi(argv[3]) : 5;
     size_t chunks = argc > 4 ? strtoul(argv[4], 0, 0) : 16;
-    size_t len = 12 + payload, slot = (len + 10 + 15) & ~(size_t)15;
+    const int un = argc > 5 && strcmp(argv[5], "unprotect") == 0;
+    size_t len = 12 + payload, slen = len + 10,
+           slot = (slen + 15) & ~(size_t)15;
+    /* what goes in and what comes out of the measured call */
+    const size_t in_l = un ? slen : len, out_l = un ? len : slen;
     uint8_t key[30];
     for (int i = 0; i < 30; i++)
         key[i] = (uint8_t)splitmix64();
@@ -96,11 +140,12 @@ int main(int argc, char **argv)
     /* ---- pinned arena + device API ----------------------------------- */
     uint8_t *h_arena, *d_arena;
     uint64_t *h_off, *d_off;
-    uint32_t *h_len, *h_cap, *d_len, *d_olen;
+    uint32_t *h_len, *h_cap, *d_len, *d_olen, *h_plen;
     int32_t *d_st;
     CHECK(hipHostMalloc((void **)&h_arena, n * slot, 0));
     CHECK(hipHostMalloc((void **)&h_off, n * 8, 0));
     CHECK(hipHostMalloc((void **)&h_len, n * 4, 0));
+    CHECK(hipHostMalloc((void **)&h_plen, n * 4, 0));
     CHECK(hipHostMalloc((void **)&h_cap, n * 4, 0));
     CHECK(hipMalloc((void **)&d_arena, n * slot));
     CHECK(hipMalloc((void **)&d_off, n * 8));
@@ -113,14 +158,30 @@ int main(int argc, char **argv)
     }
     for (size_t i = 0; i < n; i++) {
         h_off[i] = i * slot;
-        h_len[i] = (uint32_t)len;
+        h_len[i] = (uint32_t)in_l;
+        h_plen[i] = (uint32_t)len;
         h_cap[i] = (uint32_t)slot;
     }
     hipStream_t st;
     CHECK(hipStreamCreate(&st));
     CHECK(hipMemcpy(d_off, h_off, n * 8, hipMemcpyHostToDevice));
     CHECK(hipMemcpy(d_len, h_len, n * 4, hipMemcpyHostToDevice));
+    sender_t S;
+    memset(&S, 0, sizeof S);
+    if (un) {
+        CHECK(hipMalloc((void **)&S.d_arena, n * slot));
+        CHECK(hipMalloc((void **)&S.d_len, n * 4));
+        CHECK(hipMalloc((void **)&S.d_cap, n * 4));
+        CHECK(hipMalloc((void **)&S.d_st, n * 4));
+        CHECK(hipMemcpy(S.d_len, h_plen, n * 4, hipMemcpyHostToDevice));
+        S.d_off = d_off;
+        S.st = st;
+    }
+    srtp_err_status_t (*dev_op)(srtp_t, const srtp_device_batch_t *) =
+        un ? srtp_unprotect_device : srtp_protect_device;
     srtp_t s1 = make_session(key);
+    if (un)
+        S.snd = make_session(key);
     srtp_device_batch_t b;
     memset(&b, 0, sizeof b);
     b.n = n;
@@ -135,13 +196,16 @@ int main(int argc, char **argv)
     uint32_t seq0 = 0x1234;
     double t_pinned = 0;
     for (int it = -1; it < iters; it++) {
-        fill(h_arena, slot, n, len, seq0);
+        if (un)
+            produce(&S, h_arena, n, slot, len, seq0, h_cap);
+        else
+            fill(h_arena, slot, n, len, seq0);
         seq0 += (uint32_t)n;
         double t0 = now();
         CHECK(hipMemcpyAsync(d_arena, h_arena, n * slot, hipMemcpyHostToDevice,
                              st));
         CHECK(hipMemcpyAsync(d_olen, h_cap, n * 4, hipMemcpyHostToDevice, st));
-        CHECK(srtp_protect_device(s1, &b));
+        CHECK(dev_op(s1, &b));
         CHECK(hipMemcpyAsync(h_arena, d_arena, n * slot, hipMemcpyDeviceToHost,
                              st));
         CHECK(hipStreamSynchronize(st));
@@ -151,7 +215,7 @@ int main(int argc, char **argv)
     t_pinned /= iters;
     /* verify lengths came back */
     CHECK(hipMemcpy(h_len, d_olen, n * 4, hipMemcpyDeviceToHost));
-    if (h_len[0] != len + 10) {
+    if (h_len[0] != out_l) {
         fprintf(stderr, "unexpected out_len %u\n", h_len[0]);
         return 1;
     }
@@ -174,11 +238,18 @@ int main(int argc, char **argv)
         CHECK(hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming));
     }
     srtp_t s3 = make_session(key);
+    if (un) {
+        srtp_dealloc(S.snd);
+        S.snd = make_session(key);
+    }
     seq0 = 0x1234;
     double t_pipe = 0;
     size_t pipe_bad = 0;
     for (int it = -1; it < iters; it++) {
-        fill(h_arena, slot, n, len, seq0);
+        if (un)
+            produce(&S, h_arena, n, slot, len, seq0, h_cap);
+        else
+            fill(h_arena, slot, n, len, seq0);
         seq0 += (uint32_t)n;
         double t0 = now();
         for (size_t k = 0; k <= chunks; k++) {
@@ -192,7 +263,7 @@ int main(int argc, char **argv)
             }
             if (k == 0)
                 continue;
-            /* protect chunk k-1 while chunk k is in flight */
+            /* {un}protect chunk k-1 while chunk k is in flight */
             const size_t j = k - 1;
             CHECK(hipStreamWaitEvent(st, ev_in[j], 0));
             srtp_device_batch_t c = b;
@@ -202,7 +273,7 @@ int main(int argc, char **argv)
             c.out_off = d_off + j * cn;
             c.out_len = d_olen + j * cn;
             c.status = d_st + j * cn;
-            CHECK(srtp_protect_device(s3, &c));
+            CHECK(dev_op(s3, &c));
             CHECK(hipEventRecord(ev_done[j], st));
             CHECK(hipStreamWaitEvent(s_d2h, ev_done[j], 0));
             CHECK(hipMemcpyAsync(h_arena + j * cn * slot,
@@ -216,12 +287,16 @@ int main(int argc, char **argv)
     t_pipe /= iters;
     CHECK(hipMemcpy(h_len, d_olen, n * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < n; i++)
-        pipe_bad += h_len[i] != len + 10;
+        pipe_bad += h_len[i] != out_l;
     uint64_t dev_p = 0, host_p = 0;
     srtp_mi355x_prepass_stats(s3, &dev_p, &host_p);
 
     /* ---- libsrtp-shaped batch over host pointers --------------------- */
     srtp_t s2 = make_session(key);
+    if (un) {
+        srtp_dealloc(S.snd);
+        S.snd = make_session(key);
+    }
     uint8_t *pk = (uint8_t *)malloc(n * slot);
     const uint8_t **in = (const uint8_t **)malloc(n * sizeof(void *));
     uint8_t **out = (uint8_t **)malloc(n * sizeof(void *));
@@ -232,27 +307,39 @@ int main(int argc, char **argv)
     for (size_t i = 0; i < n; i++) {
         in[i] = pk + i * slot;
         out[i] = pk + i * slot;
-        il[i] = len;
+        il[i] = in_l;
     }
     seq0 = 0x1234;
     double t_batch = 0;
+    uint64_t dev_h0 = 0, host_h0 = 0, dev_h = 0, host_h = 0;
     for (int it = -1; it < iters; it++) {
-        fill(pk, slot, n, len, seq0);
+        if (un) {
+            produce(&S, h_arena, n, slot, len, seq0, h_cap);
+            memcpy(pk, h_arena, n * slot);
+        } else {
+            fill(pk, slot, n, len, seq0);
+        }
         seq0 += (uint32_t)n;
         for (size_t i = 0; i < n; i++)
             ol[i] = slot;
+        if (it == 0)
+            srtp_mi355x_prepass_stats(s2, &dev_h0, &host_h0);
         double t0 = now();
-        CHECK(srtp_protect_batch(s2, n, in, il, out, ol, NULL, sts));
+        if (un)
+            CHECK(srtp_unprotect_batch(s2, n, in, il, out, ol, sts));
+        else
+            CHECK(srtp_protect_batch(s2, n, in, il, out, ol, NULL, sts));
         if (it >= 0)
             t_batch += now() - t0;
-        if (sts[0] || ol[0] != len + 10) {
+        if (sts[0] || ol[0] != out_l) {
             fprintf(stderr, "batch status %d len %zu\n", sts[0], ol[0]);
             return 1;
         }
     }
     t_batch /= iters;
+    srtp_mi355x_prepass_stats(s2, &dev_h, &host_h);
     double bytes = (double)n * (2.0 * len + 10);
-    printf("{\"packets\": %zu, \"payload\": %zu, \"iters\": %d, "
+    printf("{\"op\": \"%s\", \"packets\": %zu, \"payload\": %zu, \"iters\": %d, "
            "\"pinned_device_api\": {\"pkt_per_s\": %.1f, \"ms\": %.3f, "
            "\"algorithmic_GBps\": %.2f, \"pcie_bytes\": %.0f, "
            "\"device_prepass_batches\": %llu, \"host_prepass_batches\": %llu}, "
@@ -261,15 +348,20 @@ int main(int argc, char **argv)
            "\"device_prepass_batches\": %llu, \"host_prepass_batches\": %llu, "
            "\"bad_lengths\": %zu}, "
            "\"host_batch_api\": {\"pkt_per_s\": %.1f, \"ms\": %.3f, "
-           "\"algorithmic_GBps\": %.2f}}\n",
-           n, payload, iters, n / t_pinned, t_pinned * 1e3,
-           bytes / t_pinned / 1e9, 2.0 * n * slot + 8.0 * n,
+           "\"algorithmic_GBps\": %.2f, \"device_prepass_batches\": %llu, "
+           "\"host_prepass_batches\": %llu}}\n",
+           un ? "unprotect" : "protect", n, payload, iters, n / t_pinned,
+           t_pinned * 1e3, bytes / t_pinned / 1e9, 2.0 * n * slot + 8.0 * n,
            (unsigned long long)dev_b, (unsigned long long)host_b, chunks,
            n / t_pipe, t_pipe * 1e3, n * (double)slot / t_pipe / 1e9,
            (unsigned long long)dev_p, (unsigned long long)host_p, pipe_bad,
-           n / t_batch, t_batch * 1e3, bytes / t_batch / 1e9);
+           n / t_batch, t_batch * 1e3, bytes / t_batch / 1e9,
+           (unsigned long long)(dev_h - dev_h0),
+           (unsigned long long)(host_h - host_h0));
     srtp_dealloc(s1);
     srtp_dealloc(s2);
     srtp_dealloc(s3);
+    if (un)
+        srtp_dealloc(S.snd);
     return pipe_bad ? 1 : 0;
 }
