@@ -188,6 +188,10 @@ typedef struct srtp_gpu_batch {
     const srtp_dev_rec_t *rec;
     const uint32_t *rec_idx;
     const uint32_t *rec_range;
+    /* or NULL: the order-free protect pre-pass classifies inside the AES-ICM
+     * kernel (IcmFused, srtp_gpu_int.h; srtp_prepass.hip pp_protect_fused):
+     * meta is written there, not read */
+    const void *fused;
 } srtp_gpu_batch_t;
 
 int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b);
@@ -269,6 +273,9 @@ typedef struct srtp_gpu_pp_batch {
                                order-free form) */
     int async;              /* protect: return once the pre-pass verdict is
                                published, the crypto kernel still queued */
+    int fused_ok;           /* protect: in place, one AES-ICM kernel variant,
+                               trailers <= 16 bytes: the order-free form may
+                               classify inside the crypto kernel */
 } srtp_gpu_pp_batch_t;
 
 /* pre-pass + crypto for protect.  *fallback != 0: nothing was written (no

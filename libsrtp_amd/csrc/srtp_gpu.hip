@@ -1212,6 +1212,9 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.rec = b->rec;
     A.rec_idx = b->rec_idx;
     A.range = b->rec_range;
+    A.fused = b->fused != nullptr;
+    if (A.fused)
+        A.fz = *(const IcmFused *)b->fused;
     if (A.rec) {
         // key buckets: the wave-aligned groups with a key per wave, then
         // the streams with few packets with a key per lane

@@ -32,6 +32,26 @@ struct srtp_gpu {
     size_t raw_cap;
 };
 
+// The order-free protect pre-pass's classification done by k_icm_hmac
+// itself (srtp_prepass.hip pp_protect_fused): per packet the header parse,
+// stream lookup, checks and index guess of k_pp_classify, the descriptor it
+// then encrypts with, and the per-stream count / highest index; the bytes
+// past the packet that its tag overwrites are saved first (an in-place
+// batch the pre-pass then declines is restored from them).
+struct IcmFused {
+    const uint32_t *in_len, *cap;
+    const srtp_dev_stream_t *st;
+    const uint32_t *hkey, *hval;
+    uint32_t hmask;
+    uint64_t *est;
+    uint32_t *skey, *pstat, *olen;
+    srtp_dev_meta_t *meta;
+    uint32_t *bcount;
+    unsigned long long *new_index;
+    uint32_t *abort;
+    uint32_t (*tsave)[4];   // the trailer bytes [len, len + trailer) (<= 16)
+};
+
 // AES-ICM (+ HMAC-SHA1) kernel arguments
 struct IcmArgs {
     const uint8_t *in;
@@ -49,6 +69,10 @@ struct IcmArgs {
     const srtp_dev_rec_t *rec;
     const uint32_t *rec_idx;
     const uint32_t *range;
+    // order-free protect classified in the kernel (per-lane keys only):
+    // fz valid when fused, meta then written, not read
+    bool fused;
+    IcmFused fz;
 };
 
 // AES-GCM kernel arguments

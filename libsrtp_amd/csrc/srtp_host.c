@@ -191,6 +191,7 @@ typedef struct {
     uint64_t num_left_min;  /* over the keys of eligible streams           */
     uint64_t uses_bound;    /* packets run on the device since the upload  */
     uint32_t uniform, mask;       /* over the protect-eligible streams    */
+    uint32_t max_trailer;         /* ... and their largest trailer        */
     uint32_t rx_uniform, rx_mask; /* over the unprotect-eligible streams  */
     uint64_t fast_batches, host_batches;
     uint64_t sorted_batches; /* fast batches that needed the sorted path  */
@@ -3105,6 +3106,7 @@ static int dev_build(srtp_t ctx)
     dt->num_left_min = UINT64_MAX;
     dt->uniform = dt->rx_uniform = 0xffffffffu;
     dt->mask = dt->rx_mask = 0;
+    dt->max_trailer = 0;
     int first = 1, rx_first = 1;
     uint32_t woff = 0;
     for (uint32_t sid = 0; sid < ns; sid++) {
@@ -3131,6 +3133,10 @@ static int dev_build(srtp_t ctx)
                 dt->uniform = 0xffffffffu;
             first = 0;
             dt->mask |= 1u << k->variant;
+            const uint32_t tr =
+                (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
+            if (tr > dt->max_trailer)
+                dt->max_trailer = tr;
         }
         if (!st->use_mki && st->rdbx.pending_roc == 0 && !xs &&
             st->direction != DIR_SENDER) {
@@ -3275,6 +3281,15 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     pb.uniform_key = dt->uniform;
     pb.mask = dt->mask;
     pb.async = async;
+    /* the order-free form may classify inside the AES-ICM kernel: in place
+     * (the declined case restores the input), per-lane keys, one AES-ICM
+     * kernel variant (variant ids 10..15: family ICM, AES-128/192/256), and
+     * trailers the kernel saves whole */
+    pb.fused_ok = b->in == b->out && b->in_off == b->out_off &&
+                  dt->uniform == 0xffffffffu && dt->mask &&
+                  (dt->mask & (dt->mask - 1)) == 0 &&
+                  (dt->mask & 0xfc00u) == dt->mask && dt->max_trailer <= 16 &&
+                  !async;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))

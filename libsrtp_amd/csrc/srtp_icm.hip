@@ -645,6 +645,148 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
     }
 }
 
+// The order-free protect pre-pass's classification of packet i inside the
+// crypto kernel (IcmFused; srtp_prepass.hip k_pp_classify restated): header
+// parse (the packet's first line, which chunk 0 reads again from cache),
+// stream lookup, the checks of srtp_host.c pre_protect (srtp.c:2515-2600),
+// the index guessed from the stream's stored index (rdbx.c:112-145), the
+// descriptor, and the stream's packet count and highest index -- a wave's
+// lanes of one stream merged by ballots before their atomics.  In-place
+// packets save the bytes their tag will overwrite.
+constexpr uint32_t FZ_NOCHAIN = 0xffffffffu;
+constexpr uint32_t FZ_AB_UNKNOWN = 1, FZ_AB_INELIGIBLE = 2, FZ_AB_ORDER = 8;
+
+DEV void fz_agg(const IcmFused &F, uint32_t key, uint64_t e)
+{
+    bool done = key == FZ_NOCHAIN;
+    for (int it = 0; it < 4; it++) {
+        const uint64_t am = __builtin_amdgcn_ballot_w64(!done);
+        if (!am)
+            return;
+        const uint32_t lead = (uint32_t)__builtin_amdgcn_readlane(
+            (int)key, (int)__builtin_ctzll(am));
+        const bool mine = !done && key == lead;
+        const uint64_t mm = __builtin_amdgcn_ballot_w64(mine);
+        if (__popcll(mm) == 1)
+            break;   // the wave's packets are spread over many streams
+        uint64_t v = mine ? e : 0;
+        for (int m = 1; m < 64; m <<= 1) {
+            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+            const uint64_t o = ((uint64_t)hi << 32) | lo;
+            v = o > v ? o : v;
+        }
+        if (mine && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(mm)) {
+            atomicAdd(&F.bcount[lead], (uint32_t)__popcll(mm));
+            atomicMax(&F.new_index[lead], (unsigned long long)v);
+        }
+        done = done || mine;
+    }
+    if (!done) {
+        atomicAdd(&F.bcount[key], 1u);
+        atomicMax(&F.new_index[key], (unsigned long long)e);
+    }
+}
+
+DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i)
+{
+    const IcmFused &F = A.fz;
+    const uint64_t off = A.in_off[i];
+    const uint32_t len = F.in_len[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
+    uint32_t code = 0, key = FZ_NOCHAIN, ab = 0;
+    uint64_t e = 0;
+    srtp_dev_meta_t m;
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;   // no crypto
+    if (h.enc_start >> 24) {
+        code = h.enc_start >> 24;   // header does not parse: no stream touched
+    } else {
+        const uint32_t sid = srtp_map_lookup(F.hkey, F.hval, F.hmask, h.ssrc);
+        if (sid == FZ_NOCHAIN) {
+            ab |= FZ_AB_UNKNOWN;    // template clone: host
+        } else {
+            const srtp_dev_stream_t S = F.st[sid];
+            if (!(S.flags & SRTP_DS_ELIGIBLE) || (S.dir & SRTP_DIR_RX))
+                ab |= FZ_AB_INELIGIBLE;
+            if (F.cap[i] < len + S.trailer) {
+                code = 28;           // srtp_err_status_buffer_small
+                atomicAdd(&F.bcount[sid], 1u);
+            } else if (h.enc_start > len) {
+                code = 21;           // srtp_err_status_parse_err
+                atomicAdd(&F.bcount[sid], 1u);
+            } else {
+                key = sid;
+                // aes_icm.c:317-322: at most 0xffff keystream blocks
+                if ((S.flags & SRTP_DS_ICM_CONF) &&
+                    (len - h.enc_start + 15) / 16 > 0xffffu)
+                    code = 8;        // srtp_err_status_cipher_fail
+                uint64_t idx = S.index, g;
+                const uint32_t seq = h.seq_len & 0xffffu;
+                // srtp_prepass.hip guess_index
+                int64_t delta;
+                if (idx > 32768) {
+                    const uint32_t lroc = (uint32_t)(idx >> 16);
+                    const uint32_t lseq = (uint32_t)(idx & 0xffffu);
+                    uint32_t roc = lroc;
+                    delta = (int64_t)seq - (int64_t)lseq;
+                    if (lseq < 32768) {
+                        if ((int)seq - (int)lseq > 32768) {
+                            roc = lroc - 1;
+                            delta -= 65536;
+                        }
+                    } else if ((int)lseq - 32768 > (int)seq) {
+                        roc = lroc + 1;
+                        delta += 65536;
+                    }
+                    g = ((uint64_t)roc << 16) | seq;
+                } else {
+                    g = seq;
+                    delta = (int64_t)seq - (int64_t)idx;
+                }
+                e = g;
+                if (delta < 1)
+                    ab |= FZ_AB_ORDER;   // the sorted path decides
+                F.est[i] = e;
+                if (code == 0) {
+                    m.key = S.key;
+                    m.roc = (uint32_t)(e >> 16);
+                    m.info = h.enc_start | (S.variant << 24);
+                    m.len = len;
+                    F.olen[i] = len + S.trailer;
+                    // the bytes the tag overwrites (in place), for the undo
+                    const uint8_t *t = A.out + A.out_off[i] + len;
+                    const uint32_t tn = S.trailer < 16 ? S.trailer : 16;
+                    uint32_t w[4] = { 0, 0, 0, 0 };
+                    const bool al = ((uintptr_t)t & 3) == 0;
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; j++) {
+                        if (4 * j + 4 <= tn && al) {
+                            w[j] = *(const uint32_t *)(t + 4 * j);
+                            continue;
+                        }
+                        for (uint32_t b = 4 * j; b < tn && b < 4 * j + 4; b++)
+                            w[j] |= (uint32_t)t[b] << (8 * (b & 3));
+                    }
+                    F.tsave[i][0] = w[0];
+                    F.tsave[i][1] = w[1];
+                    F.tsave[i][2] = w[2];
+                    F.tsave[i][3] = w[3];
+                }
+            }
+        }
+    }
+    F.pstat[i] = code;
+    F.skey[i] = key;
+    F.meta[i] = m;
+    if (ab)
+        atomicOr(F.abort, ab);
+    fz_agg(F, key, e);
+    return m;
+}
+
 // All four T-tables (128 KiB of LDS, one 512-lane workgroup per CU).  The
 // AES schedule sits in SGPRs (KM_UNI / KM_WAVE) or VGPRs (KM_LANE).  With
 // per-lane keys the kernel needs 230-256 VGPRs, so two waves per SIMD is
@@ -660,7 +802,7 @@ constexpr int ICM_THREADS_UNI = ICM_THREADS_UNI_N;
 constexpr int ICM_THREADS_LANE = 512;
 constexpr uint32_t ICM_SKIP = 0xffffffffu;
 
-template <int NR, bool AUTH, bool PROTECT, int KM>
+template <int NR, bool AUTH, bool PROTECT, int KM, bool FUSED = false>
 __global__ __launch_bounds__(KM == KM_LANE ? ICM_THREADS_LANE : ICM_THREADS_UNI)
 void k_icm_hmac(IcmArgs A)
 {
@@ -693,9 +835,16 @@ void k_icm_hmac(IcmArgs A)
         // packet order
         const uint32_t stride = gridDim.x * blockDim.x;
         const uint32_t first = blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + lpos;
-        for (uint32_t i = first; i < A.n; i += stride)
-            icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                A, A.meta[i], A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+        for (uint32_t i = first; i < A.n; i += stride) {
+            if constexpr (FUSED) {
+                const srtp_dev_meta_t m = fz_classify(A, i);
+                icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
+                    A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+            } else {
+                icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
+                    A, A.meta[i], A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+            }
+        }
         return;
     }
     // key buckets: records [range[0], range[1])
@@ -747,6 +896,13 @@ static void icm_go(const IcmArgs &A, int ncu, hipStream_t st)
     const size_t cap = (size_t)ncu;
     if (wgs > cap)
         wgs = cap;
+    if constexpr (KM == KM_LANE && PR && NR > 0) {
+        if (A.fused) {
+            hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM, true>),
+                               dim3((unsigned)wgs), dim3((unsigned)T), 0, st, A);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM>), dim3((unsigned)wgs),
                        dim3((unsigned)T), 0, st, A);
 }

@@ -45,6 +45,7 @@
 #include <string.h>
 
 #include "srtp_dev.h"
+#include "srtp_gpu_int.h"
 #include "srtp_rtp_hdr.h"
 #include "srtp_scan.h"
 
@@ -115,6 +116,9 @@ struct PpState {
     unsigned long long *pu_first = nullptr;
     uint64_t pu_first_cap = 0;
     uint32_t pu_gen = 0;
+    // order-free protect classified in the crypto kernel: the trailer bytes
+    // each in-place packet's tag overwrites (16 per packet)
+    uint32_t (*tsave)[4] = nullptr;
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -640,6 +644,23 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
     const uint32_t off = st[s].win_off, words = st[s].win_bits >> 5;
     for (uint32_t w = 0; w < words; w++)
         win[off + w] = wnew[off + w];
+}
+
+// An in-place batch classified inside the crypto kernel that the pre-pass
+// then declined: the bytes past every encrypted packet that its tag
+// overwrote come back (its payload is restored by k_undo)
+__global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
+                                  const uint32_t *in_len, const uint32_t *olen,
+                                  const srtp_dev_meta_t *meta,
+                                  const uint32_t (*tsave)[4], uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || SRTP_META_STATUS(meta[i].info))
+        return;
+    const uint32_t len = in_len[i], tn = olen[i] - len;
+    uint8_t *t = arena + off[i] + len;
+    for (uint32_t b = 0; b < tn && b < 16; b++)
+        t[b] = (uint8_t)(tsave[i][b >> 2] >> (8 * (b & 3)));
 }
 
 // ---------------------------------------------------------------------------
@@ -2136,6 +2157,9 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipMalloc((void **)&P->meta, c * sizeof(srtp_dev_meta_t)));
     PPCHK(hipMalloc((void **)&P->auth, c));
     PPCHK(hipMalloc((void **)&P->top, c * 8));
+    if (P->tsave)
+        PPCHK(hipFree(P->tsave));
+    PPCHK(hipMalloc((void **)&P->tsave, c * 16));
     // buckets: region A <= 2 x its packets (>= BK_MIN per stream, padded
     // to 64), region B <= its packets
     PPCHK(hipMalloc((void **)&P->rec, 2 * c * sizeof(srtp_dev_rec_t)));
@@ -2176,7 +2200,7 @@ void srtp_gpu_pp_free(void *p)
                      P->hist, P->auth, P->top, P->abort, P->bk_off, P->bk_cur,
                      P->rec, P->rec_idx, P->bk_range, P->ch_tile,
                      P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
-                     P->pu_first };
+                     P->pu_first, P->tsave };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2372,6 +2396,17 @@ static hipError_t stream_order(PpState *P, uint32_t ns, uint32_t N,
 }
 
 // SRTP_PP_FUSED=0: one-stream batches through the multi-launch chain form
+// SRTP_PP_FUSED_OF=0: the order-free protect form classifies in its own
+// kernel (k_pp_classify) again
+static bool fused_of_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("SRTP_PP_FUSED_OF");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 static bool fused_on()
 {
     static const bool on = [] {
@@ -2494,6 +2529,86 @@ static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     return 0;
 }
 
+// The order-free form with its classification inside the crypto kernel
+// (IcmFused, srtp_icm.hip fz_classify): no separate header pass -- every
+// packet's first line is read once, by the kernel that encrypts it.  The
+// conditions of the order-free form (k_pp_usetbits) are checked after the
+// crypto; a batch outside them (or with an unknown / ineligible stream) is
+// restored -- k_undo re-applies the keystream, k_pp_tail_restore writes back
+// the bytes the tags overwrote -- and, for AB_ORDER, *sorted set: the caller
+// runs the sorted chain form, else the host decides (*fallback).  Only in
+// place, one AES-ICM kernel variant, trailers <= 16 bytes (fused_ok).
+static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
+                            hipStream_t stream, int *fallback, bool *sorted)
+{
+    const uint32_t N = (uint32_t)b->n, ns = P->ns;
+    const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
+    *sorted = false;
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    hipLaunchKernelGGL(k_pp_reset, dim3(ns / 256 + 1), blk, 0, stream,
+                       P->abort, P->bcount, (unsigned long long *)P->new_index,
+                       nullptr, nullptr, ns);
+    IcmFused F;
+    F.in_len = b->in_len;
+    F.cap = b->out_len;
+    F.st = P->st;
+    F.hkey = P->hkey;
+    F.hval = P->hval;
+    F.hmask = P->hcap - 1;
+    F.est = P->est;
+    F.skey = P->skey;
+    F.pstat = P->pstat;
+    F.olen = P->skey2;
+    F.meta = P->meta;
+    F.bcount = P->bcount;
+    F.new_index = (unsigned long long *)P->new_index;
+    F.abort = P->abort;
+    F.tsave = P->tsave;
+    srtp_gpu_batch_t cb = {};
+    cb.n = b->n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;
+    cb.auth_ok = nullptr;
+    cb.uniform_key = 0xffffffffu;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = nullptr;   // the kernel itself classifies: it always runs
+    cb.fused = &F;
+    if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "fused crypto"))
+        return -1;
+    hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
+                       P->new_index, P->win, P->wnew);
+    hipLaunchKernelGGL(k_pp_usetbits, gp, blk, 0, stream, P->skey, P->est,
+                       P->st, ns, N, P->new_index, P->wnew, P->abort);
+    hipLaunchKernelGGL(k_pp_commit_of, gp, blk, 0, stream, P->pstat, P->skey2,
+                       N, P->abort, b->status, b->out_len);
+    hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
+                       P->new_index, P->bcount, P->wnew, P->win, P->abort,
+                       P->h_abort_dev);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "fused commit"))
+        return -1;
+    PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    const uint32_t ab = *(volatile uint32_t *)P->h_abort;
+    *fallback = (int)ab;
+    if (!ab)
+        return 0;
+    // declined: the input comes back exactly
+    if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
+        return -1;
+    hipLaunchKernelGGL(k_pp_tail_restore, gp, blk, 0, stream, b->out,
+                       b->out_off, b->in_len, P->skey2, P->meta, P->tsave, N);
+    PPCHK(hipGetLastError());
+    PPCHK(hipStreamSynchronize(stream));
+    *sorted = ab == AB_ORDER;
+    return 0;
+}
+
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback)
 {
@@ -2522,6 +2637,15 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return e && *e == '1';
     }();
     bool unordered = ns > 1 && !force_sorted;
+    if (unordered && b->fused_ok && fused_of_on() &&
+        !(b->uniform_key == 0xffffffffu && buckets_on())) {
+        bool sorted = false;
+        if (pp_protect_fused(g, P, b, stream, fallback, &sorted))
+            return -1;
+        if (!sorted)
+            return 0;
+        unordered = false;   // restored, nothing committed: the chain form
+    }
     for (;;) {
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
     hipLaunchKernelGGL(k_pp_reset, dim3(ns / 256 + 1), blk, 0, stream, P->abort, P->bcount,

@@ -57,6 +57,28 @@ __device__ __forceinline__ srtp_dev_hdr_t srtp_parse_rtp(const uint8_t *p,
     return h;
 }
 
+// SSRC -> device stream id through the device copy of the host's
+// open-addressing map (srtp_host.c map_hash / map_get: first inserted wins,
+// as srtp_stream_list_get, srtp.c:5292-5305); ~0 when absent
+__device__ __forceinline__ uint32_t srtp_map_lookup(const uint32_t *hkey,
+                                                    const uint32_t *hval,
+                                                    uint32_t hmask,
+                                                    uint32_t ssrc)
+{
+    uint32_t h = ssrc * 0x9e3779b1u;
+    h ^= h >> 15;
+    uint32_t p = h & hmask;
+    for (uint32_t probe = 0; probe <= hmask; probe++) {
+        const uint32_t v = hval[p];
+        if (v == 0xffffffffu)
+            return 0xffffffffu;
+        if (hkey[p] == ssrc)
+            return v;
+        p = (p + 1) & hmask;
+    }
+    return 0xffffffffu;
+}
+
 // CSRC count, X bit and extension profile of a header srtp_parse_rtp
 // accepted: [15:0] profile, [19:16] CC, bit 20 X
 __device__ __forceinline__ uint32_t srtp_rtp_xinfo(const uint8_t *p,

@@ -424,3 +424,81 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
     assert snd.prepass_sorted_batches() == 0
     snd.L.srtp_mi355x_set_key_buckets(0)
+
+
+# --------------------------------------------------------------------------
+# the order-free form classified inside the AES-ICM kernel (in place, one
+# ICM variant, per-lane keys: srtp_prepass.hip pp_protect_fused): a batch it
+# declines must come back untouched before the sorted / host path runs
+
+def _device_protect_raw(sess, pkts, caps, fill=0xa5):
+    """in place; the capacity region past each packet pre-filled with
+    `fill`; returns (status, arena bytes, offsets, out lengths)"""
+    import torch
+    offs, pos = [], 0
+    for p, c in zip(pkts, caps):
+        offs.append(pos)
+        pos += (max(len(p), c) + 15) & ~15
+    buf = bytearray([fill]) * (pos + 16)
+    for o, p in zip(offs, pkts):
+        buf[o:o + len(p)] = p
+    orig = bytes(buf)
+    arena = torch.frombuffer(buf, dtype=torch.uint8).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor([len(p) for p in pkts], dtype=torch.int32).cuda()
+    cap = torch.tensor(caps, dtype=torch.int32).cuda()
+    st = torch.full((len(pkts),), -1, dtype=torch.int32).cuda()
+    assert sess.protect_device(arena, off, ln, arena, off, cap, st) == 0
+    return st.cpu().tolist(), arena.cpu().numpy().tobytes(), orig, offs, \
+        cap.cpu().tolist()
+
+
+@pytest.mark.parametrize("case", ["duplicate", "unknown_ssrc", "long_chain"])
+def test_fused_order_free_declined_batch_is_restored(case):
+    """duplicate -> host path, unknown SSRC -> host path, a stream with more
+    packets than its window -> the sorted chain form: statuses and bytes
+    equal to the oracle's, and every rejected packet's bytes up to its
+    capacity (its trailer space included) exactly as they were"""
+    _gpu()
+    rng = random.Random(600 + len(case))
+    ssrcs, lib, orc = _stream_set(40)
+    seq0 = {s: 0xfff0 - 3 * k for k, s in enumerate(ssrcs)}
+    pk = _interleaved(rng, ssrcs, seq0, 150 if case == "long_chain" else 20)
+    if case == "duplicate":
+        pk.insert(300, pk[17])
+    elif case == "unknown_ssrc":
+        pk.insert(100, rtp_packet(rng, 0x0bad0bad, 5, 40))
+    caps = [len(p) + 16 for p in pk]
+    st, got, orig, offs, olen = _device_protect_raw(lib, pk, caps)
+    for i, p in enumerate(pk):
+        rc, ref = orc.protect(p, caps[i])
+        assert st[i] == rc, (i, st[i], rc)
+        o = offs[i]
+        if rc == 0:
+            assert got[o:o + olen[i]] == ref, i
+        else:
+            assert got[o:o + caps[i]] == orig[o:o + caps[i]], i
+    if case == "long_chain":
+        assert lib.prepass_stats() == (1, 0)
+        assert lib.prepass_sorted_batches() == 1
+    else:
+        assert lib.prepass_stats() == (0, 1)
+
+
+def test_fused_order_free_trailer_space_untouched_on_success():
+    """accepted packets: bytes past packet + tag up to the capacity are not
+    written (the saved-trailer logic reads exactly the tag's bytes)"""
+    _gpu()
+    rng = random.Random(611)
+    ssrcs, lib, orc = _stream_set(64)
+    seq0 = {s: 7 for s in ssrcs}
+    pk = _interleaved(rng, ssrcs, seq0, 8)
+    caps = [len(p) + 10 + rng.randrange(0, 40) for p in pk]
+    st, got, orig, offs, olen = _device_protect_raw(lib, pk, caps)
+    assert lib.prepass_stats() == (1, 0)
+    for i, p in enumerate(pk):
+        rc, ref = orc.protect(p, caps[i])
+        assert st[i] == rc == 0
+        o = offs[i]
+        assert got[o:o + olen[i]] == ref
+        assert got[o + olen[i]:o + caps[i]] == orig[o + olen[i]:o + caps[i]]

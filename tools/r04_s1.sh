@@ -16,3 +16,7 @@ cat gpurun_out/s1_g711_variants.log
 timeout -k 10 200 python3 bench.py --op unprotect --steps 20 --warmup 3 --no-cpu-baseline \
     --traffic off > gpurun_out/s1_bench_unprotect.json 2> gpurun_out/s1_bench_unprotect.err || exit 1
 tail -c 700 gpurun_out/s1_bench_unprotect.json
+for op in protect unprotect; do
+  timeout -k 10 300 ./tools/e2e_bench $((1<<20)) 1400 5 16 $op > gpurun_out/s1_e2e_$op.json 2> gpurun_out/s1_e2e_$op.err || exit 1
+  cat gpurun_out/s1_e2e_$op.json
+done
