@@ -45,8 +45,8 @@ struct IcmPkt {
     uint32_t cb[4];    // counter block, block counter (bytes 14..15) zero
 };
 
-// One 64-byte chunk b of a packet in its general form, given its four
-// input quads v (zero past the data): header words that are not encrypted,
+// The arithmetic of one 64-byte chunk b (icm_chunk below), given its four
+// input quads v (zero past the data), for icm_chunk_coop64: header words that are not encrypted,
 // the ROC / terminator / length words of the SHA-1 message tail (sha1.c
 // srtp_sha1_final); the output quads go to oq.  The keystream blocks that
 // any payload byte uses come from the counter cache inside the first epoch
@@ -129,9 +129,15 @@ DEV void icm_chunk_core(uint32_t b, const IcmPkt &p, const CtrCache &C,
     }
 }
 
-// chunk b, one lane per packet: 16-byte loads and stores of the lane's own
-// packet.  The partial last quad is kept in tailq and stored once after the
-// chunk loop (a byte-wise store here, unrolled per quad, costs ~65 VGPRs).
+// One 64-byte chunk b of a packet in its general form, one lane per packet
+// (the coop64 path below shares icm_chunk_core's arithmetic; this copy keeps
+// the uniform-key kernels' register allocation: 2 % faster on configs[1]): header words that
+// are not encrypted, quads past the end of the data, the partial last quad
+// (kept in tailq, stored once after the chunk loop: a byte-wise store here,
+// unrolled per quad, costs ~65 VGPRs), and the ROC / terminator / length
+// words of the SHA-1 message tail (sha1.c srtp_sha1_final).  The keystream
+// blocks that any payload byte uses come from the counter cache inside the
+// first epoch (blocks 0..255), from full AES past it.
 template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
 DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
                    const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
@@ -147,19 +153,83 @@ DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
         if (q0 + t < p.nq)
             v[t] = *(const u32x4 *)(ip + 16 * t);
     }
-    icm_chunk_core<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, v,
-                                            oq);
+    uint32_t ks[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t jj = q0 + t - p.qoff;
+        ks[t][0] = p.cb[0];
+        ks[t][1] = p.cb[1];
+        ks[t][2] = p.cb[2];
+        ks[t][3] = p.cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+    }
+    if constexpr (NR > 0) {
+        if (p.conf) {
+#pragma unroll
+            for (int g = 0; g < 4; g += ICM_NB) {
+                const int jf = (int)(q0 + g) - (int)p.qoff;
+                if (jf + ICM_NB - 1 < 0 || 16 * jf >= (int)p.P)
+                    continue;
+                auto &kg = *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]);
+                if (jf >= 0 && jf + ICM_NB - 1 < 256) {
+                    uint32_t jb[ICM_NB];
+#pragma unroll
+                    for (int j = 0; j < ICM_NB; j++)
+                        jb[j] = (uint32_t)(jf + j) << 8;
+                    aes_ctr<ICM_NB, NR, TAB4>(kg, jb, C, rk, T);
+                } else {
+                    aes_blocks<ICM_NB, NR, TAB4>(kg, rk, T);
+                }
+            }
+        }
+    }
+    if (NR == 0 || !p.conf) {
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+    }
+    uint32_t wv[16];
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const uint32_t q = q0 + t;
+        uint32_t kk[4];
+        ks_shift(ks_prev, ks[t], p.s, kk);
+        if (b < p.bclean) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (4 * q + u < p.hw)
+                    kk[u] = 0;   // header words are never encrypted
+        }
+        uint32_t o[4] = { v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
+                          v[t].w ^ kk[3] };
+        oq[t] = u32x4{ o[0], o[1], o[2], o[3] };
         if (16 * q + 16 <= p.L) {
-            *(u32x4 *)(op + 16 * t) = oq[t];
+            *(u32x4 *)(op + 16 * t) = u32x4{ o[0], o[1], o[2], o[3] };
         } else if (16 * q < p.L) {
             // the one partial quad: stored after the loop
 #pragma unroll
             for (int u = 0; u < 4; u++)
-                tailq[u] = oq[t][u];
+                tailq[u] = o[u];
         }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
+            ks_prev[u] = ks[t][u];
+        }
+    }
+    if (AUTH) {
+        if (64 * b + 64 > p.L) {
+            // message tail: ROC, the 0x80 terminator, zero padding and
+            // the bit length (sha1.c srtp_sha1_final)
+#pragma unroll
+            for (int g = 0; g < 16; g++)
+                wv[g] = tail_word(wv[g], (int)p.L - (int)(64 * b + 4 * g),
+                                  p.roc);
+            if (b == p.nb - 1) {
+                wv[14] = 0;
+                wv[15] = (64 + p.L + 4) * 8;
+            }
+        }
+        sha1_compress(hst, wv);
     }
 }
 
@@ -656,46 +726,50 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
 constexpr uint32_t FZ_NOCHAIN = 0xffffffffu;
 constexpr uint32_t FZ_AB_UNKNOWN = 1, FZ_AB_INELIGIBLE = 2, FZ_AB_ORDER = 8;
 
-DEV void fz_agg(const IcmFused &F, uint32_t key, uint64_t e)
+// What a lane keeps between its packets: the last stream it looked up
+// (a lane's packets of a batch are often one stream's: the persistent grid's
+// stride is a multiple of the stream count in round-robin batches), and the
+// running packet count / highest index of its current stream, flushed with
+// one atomic pair when the stream changes and at the end.  The per-packet
+// atomics stalled the crypto behind them (an atomic stays in vmcnt for
+// ~3000 cycles under load, MI355X_MICROARCH.md).
+struct FzLane {
+    uint32_t ssrc, sid;            // cached lookup (sid ~0: none)
+    uint32_t key, variant, flags, trailer, dir;
+    uint64_t index;
+    uint32_t run_sid, run_cnt;     // current run (run_sid ~0: none)
+    uint64_t run_max;
+};
+
+DEV void fz_flush(const IcmFused &F, FzLane &z)
 {
-    bool done = key == FZ_NOCHAIN;
-    for (int it = 0; it < 4; it++) {
-        const uint64_t am = __builtin_amdgcn_ballot_w64(!done);
-        if (!am)
-            return;
-        const uint32_t lead = (uint32_t)__builtin_amdgcn_readlane(
-            (int)key, (int)__builtin_ctzll(am));
-        const bool mine = !done && key == lead;
-        const uint64_t mm = __builtin_amdgcn_ballot_w64(mine);
-        if (__popcll(mm) == 1)
-            break;   // the wave's packets are spread over many streams
-        uint64_t v = mine ? e : 0;
-        for (int m = 1; m < 64; m <<= 1) {
-            const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
-            const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
-            const uint64_t o = ((uint64_t)hi << 32) | lo;
-            v = o > v ? o : v;
-        }
-        if (mine && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(mm)) {
-            atomicAdd(&F.bcount[lead], (uint32_t)__popcll(mm));
-            atomicMax(&F.new_index[lead], (unsigned long long)v);
-        }
-        done = done || mine;
+    if (z.run_sid != FZ_NOCHAIN) {
+        atomicAdd(&F.bcount[z.run_sid], z.run_cnt);
+        if (z.run_max)
+            atomicMax(&F.new_index[z.run_sid], (unsigned long long)z.run_max);
     }
-    if (!done) {
-        atomicAdd(&F.bcount[key], 1u);
-        atomicMax(&F.new_index[key], (unsigned long long)e);
-    }
+    z.run_sid = FZ_NOCHAIN;
+    z.run_cnt = 0;
+    z.run_max = 0;
 }
 
-DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i)
+DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, uint64_t e)
+{
+    if (sid != z.run_sid) {
+        fz_flush(F, z);
+        z.run_sid = sid;
+    }
+    z.run_cnt++;
+    z.run_max = e > z.run_max ? e : z.run_max;
+}
+
+DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
 {
     const IcmFused &F = A.fz;
     const uint64_t off = A.in_off[i];
     const uint32_t len = F.in_len[i];
     const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
     uint32_t code = 0, key = FZ_NOCHAIN, ab = 0;
-    uint64_t e = 0;
     srtp_dev_meta_t m;
     m.key = 0;
     m.roc = 0;
@@ -704,28 +778,41 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i)
     if (h.enc_start >> 24) {
         code = h.enc_start >> 24;   // header does not parse: no stream touched
     } else {
-        const uint32_t sid = srtp_map_lookup(F.hkey, F.hval, F.hmask, h.ssrc);
+        if (h.ssrc != z.ssrc || z.sid == FZ_NOCHAIN) {
+            z.ssrc = h.ssrc;
+            z.sid = srtp_map_lookup(F.hkey, F.hval, F.hmask, h.ssrc);
+            if (z.sid != FZ_NOCHAIN) {
+                const srtp_dev_stream_t S = F.st[z.sid];
+                z.key = S.key;
+                z.variant = S.variant;
+                z.flags = S.flags;
+                z.trailer = S.trailer;
+                z.dir = S.dir;
+                z.index = S.index;
+            }
+        }
+        const uint32_t sid = z.sid;
         if (sid == FZ_NOCHAIN) {
             ab |= FZ_AB_UNKNOWN;    // template clone: host
         } else {
-            const srtp_dev_stream_t S = F.st[sid];
-            if (!(S.flags & SRTP_DS_ELIGIBLE) || (S.dir & SRTP_DIR_RX))
+            if (!(z.flags & SRTP_DS_ELIGIBLE) || (z.dir & SRTP_DIR_RX))
                 ab |= FZ_AB_INELIGIBLE;
-            if (F.cap[i] < len + S.trailer) {
+            if (F.cap[i] < len + z.trailer) {
                 code = 28;           // srtp_err_status_buffer_small
-                atomicAdd(&F.bcount[sid], 1u);
+                fz_count(F, z, sid, 0);
             } else if (h.enc_start > len) {
                 code = 21;           // srtp_err_status_parse_err
-                atomicAdd(&F.bcount[sid], 1u);
+                fz_count(F, z, sid, 0);
             } else {
                 key = sid;
                 // aes_icm.c:317-322: at most 0xffff keystream blocks
-                if ((S.flags & SRTP_DS_ICM_CONF) &&
+                if ((z.flags & SRTP_DS_ICM_CONF) &&
                     (len - h.enc_start + 15) / 16 > 0xffffu)
                     code = 8;        // srtp_err_status_cipher_fail
-                uint64_t idx = S.index, g;
+                const uint64_t idx = z.index;
                 const uint32_t seq = h.seq_len & 0xffffu;
-                // srtp_prepass.hip guess_index
+                uint64_t e;
+                // srtp_prepass.hip guess_index (rdbx.c:112-145)
                 int64_t delta;
                 if (idx > 32768) {
                     const uint32_t lroc = (uint32_t)(idx >> 16);
@@ -741,24 +828,24 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i)
                         roc = lroc + 1;
                         delta += 65536;
                     }
-                    g = ((uint64_t)roc << 16) | seq;
+                    e = ((uint64_t)roc << 16) | seq;
                 } else {
-                    g = seq;
+                    e = seq;
                     delta = (int64_t)seq - (int64_t)idx;
                 }
-                e = g;
                 if (delta < 1)
                     ab |= FZ_AB_ORDER;   // the sorted path decides
                 F.est[i] = e;
+                fz_count(F, z, sid, e);
                 if (code == 0) {
-                    m.key = S.key;
+                    m.key = z.key;
                     m.roc = (uint32_t)(e >> 16);
-                    m.info = h.enc_start | (S.variant << 24);
+                    m.info = h.enc_start | (z.variant << 24);
                     m.len = len;
-                    F.olen[i] = len + S.trailer;
+                    F.olen[i] = len + z.trailer;
                     // the bytes the tag overwrites (in place), for the undo
                     const uint8_t *t = A.out + A.out_off[i] + len;
-                    const uint32_t tn = S.trailer < 16 ? S.trailer : 16;
+                    const uint32_t tn = z.trailer < 16 ? z.trailer : 16;
                     uint32_t w[4] = { 0, 0, 0, 0 };
                     const bool al = ((uintptr_t)t & 3) == 0;
 #pragma unroll
@@ -783,7 +870,6 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i)
     F.meta[i] = m;
     if (ab)
         atomicOr(F.abort, ab);
-    fz_agg(F, key, e);
     return m;
 }
 
@@ -835,16 +921,24 @@ void k_icm_hmac(IcmArgs A)
         // packet order
         const uint32_t stride = gridDim.x * blockDim.x;
         const uint32_t first = blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + lpos;
-        for (uint32_t i = first; i < A.n; i += stride) {
-            if constexpr (FUSED) {
-                const srtp_dev_meta_t m = fz_classify(A, i);
+        if constexpr (FUSED) {
+            FzLane z;
+            z.ssrc = 0;
+            z.sid = FZ_NOCHAIN;
+            z.run_sid = FZ_NOCHAIN;
+            z.run_cnt = 0;
+            z.run_max = 0;
+            for (uint32_t i = first; i < A.n; i += stride) {
+                const srtp_dev_meta_t m = fz_classify(A, i, z);
                 icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
                     A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
-            } else {
-                icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                    A, A.meta[i], A.in_off[i], A.out_off[i], i, A.uni, T, rk);
             }
+            fz_flush(A.fz, z);
+            return;
         }
+        for (uint32_t i = first; i < A.n; i += stride)
+            icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
+                A, A.meta[i], A.in_off[i], A.out_off[i], i, A.uni, T, rk);
         return;
     }
     // key buckets: records [range[0], range[1])

@@ -44,7 +44,8 @@ def _sent(pol, n, seq0, payloads, seed):
 def _network(n, rng, reorder, dup, old, forge):
     """arrival order as (sent index, forged) pairs: local displacements of up
     to 32 places, duplicates of recent packets, old copies 200..400 behind
-    (past a 128-bit window), forgeries (a copy with a flipped tag bit)"""
+    (past a 128-bit window), forgeries (a copy with a flipped tag bit that
+    arrives just before the genuine packet)"""
     order = list(range(n))
     for i in range(n - 1):
         if rng.random() < reorder:
@@ -52,14 +53,14 @@ def _network(n, rng, reorder, dup, old, forge):
             order[i], order[j] = order[j], order[i]
     out = []
     for i, s in enumerate(order):
-        out.append((s, False))
         r = rng.random()
+        if dup + old <= r < dup + old + forge:
+            out.append((s, True))   # arrives first: auth_fail, not a replay
+        out.append((s, False))
         if r < dup:
             out.append((order[max(0, i - rng.randrange(0, 64))], False))
         elif r < dup + old and i > 400:
             out.append((order[i - rng.randrange(200, 400)], False))
-        elif r < dup + old + forge:
-            out.append((s, True))
     return out
 
 

@@ -13,6 +13,8 @@ cat gpurun_out/s1_icm_variants.log
 VARIANTS="r3g711" timeout -k 10 600 bash tools/step_variants.sh g711 2 \
     > gpurun_out/s1_g711_variants.log 2>&1 || exit 1
 cat gpurun_out/s1_g711_variants.log
+SRTP_PP_FUSED_OF=0 timeout -k 10 200 python3 bench.py --config g711 --steps 20 --warmup 3 \
+    --no-cpu-baseline --traffic off 2>/dev/null | python3 -c "import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); print('tree_nofused', round(d['ms_per_step'],4), round(d['roofline']['kernel_ms'],4))" || exit 1
 timeout -k 10 200 python3 bench.py --op unprotect --steps 20 --warmup 3 --no-cpu-baseline \
     --traffic off > gpurun_out/s1_bench_unprotect.json 2> gpurun_out/s1_bench_unprotect.err || exit 1
 tail -c 700 gpurun_out/s1_bench_unprotect.json
