@@ -34,18 +34,18 @@ struct srtp_gpu {
 
 // The order-free protect pre-pass's classification done by k_icm_hmac
 // itself (srtp_prepass.hip pp_protect_fused): per packet the header parse,
-// stream lookup, checks and index guess of k_pp_classify, the descriptor it
-// then encrypts with, and the per-stream count / highest index; the bytes
-// past the packet that its tag overwrites are saved first (an in-place
-// batch the pre-pass then declines is restored from them).
+// stream lookup, checks and index guess of k_pp_classify (status, stream id,
+// index out; the descriptor it encrypts with stays in registers), and the
+// per-stream count / highest index; the bytes past the packet that its tag
+// overwrites are saved first (an in-place batch the pre-pass then declines
+// is restored from them).
 struct IcmFused {
     const uint32_t *in_len, *cap;
     const srtp_dev_stream_t *st;
     const uint32_t *hkey, *hval;
     uint32_t hmask;
     uint64_t *est;
-    uint32_t *skey, *pstat, *olen;
-    srtp_dev_meta_t *meta;
+    uint32_t *skey, *pstat;
     uint32_t *bcount;
     unsigned long long *new_index;
     uint32_t *abort;

@@ -580,8 +580,11 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
     // of the wave 64-byte aligned with as many chunks: the whole packet in
     // lane quads (icm_chunk_coop64).  Not in the uniform-key kernels: the
     // extra path costs them 13 spilled VGPRs.
+#ifndef ICM_COOP64
+#define ICM_COOP64 1
+#endif
     bool all64 = false;
-    if constexpr (KM == KM_LANE) {
+    if constexpr (KM == KM_LANE && ICM_COOP64) {
         const uint32_t al64 =
             (uint32_t)(((uintptr_t)p.in | (uintptr_t)p.out) & 63);
         all64 = __builtin_amdgcn_ballot_w64(al64 == 0) == ~0ull &&
@@ -842,7 +845,6 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
                     m.roc = (uint32_t)(e >> 16);
                     m.info = h.enc_start | (z.variant << 24);
                     m.len = len;
-                    F.olen[i] = len + z.trailer;
                     // the bytes the tag overwrites (in place), for the undo
                     const uint8_t *t = A.out + A.out_off[i] + len;
                     const uint32_t tn = z.trailer < 16 ? z.trailer : 16;
@@ -865,9 +867,10 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
             }
         }
     }
+    // the descriptor is not stored: a declined batch rebuilds it for the
+    // undo (srtp_prepass.hip k_fz_meta), commit derives the lengths
     F.pstat[i] = code;
     F.skey[i] = key;
-    F.meta[i] = m;
     if (ab)
         atomicOr(F.abort, ab);
     return m;

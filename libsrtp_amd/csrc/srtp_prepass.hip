@@ -650,17 +650,63 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
 // then declined: the bytes past every encrypted packet that its tag
 // overwrote come back (its payload is restored by k_undo)
 __global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
-                                  const uint32_t *in_len, const uint32_t *olen,
+                                  const uint32_t *in_len, const uint32_t *skey,
+                                  const srtp_dev_stream_t *st,
                                   const srtp_dev_meta_t *meta,
                                   const uint32_t (*tsave)[4], uint32_t n)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || SRTP_META_STATUS(meta[i].info))
         return;
-    const uint32_t len = in_len[i], tn = olen[i] - len;
+    const uint32_t len = in_len[i], tn = st[skey[i]].trailer;
     uint8_t *t = arena + off[i] + len;
     for (uint32_t b = 0; b < tn && b < 16; b++)
         t[b] = (uint8_t)(tsave[i][b >> 2] >> (8 * (b & 3)));
+}
+
+// Fused order-free form: the per-packet commit (status, protected length
+// from the stream's trailer) unless the batch was declined
+__global__ void k_fz_commit(const uint32_t *pstat, const uint32_t *skey,
+                            const uint32_t *in_len,
+                            const srtp_dev_stream_t *st, uint32_t n,
+                            const uint32_t *abort, int32_t *status,
+                            uint32_t *out_len)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || *abort)
+        return;
+    const uint32_t code = pstat[i];
+    status[i] = (int32_t)code;
+    if (code == 0)
+        out_len[i] = in_len[i] + st[skey[i]].trailer;
+}
+
+// ... and a declined batch's descriptors, as k_icm_hmac had them, for the
+// undo (k_undo re-applies the keystream)
+__global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
+                          const uint32_t *in_len, const uint32_t *pstat,
+                          const uint32_t *skey, const uint64_t *est,
+                          const srtp_dev_stream_t *st, uint32_t n,
+                          srtp_dev_meta_t *meta)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    srtp_dev_meta_t m;
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;
+    const uint32_t s = skey[i];
+    if (s != NOCHAIN && pstat[i] == 0) {
+        const uint64_t off = in_off[i];
+        const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
+        m.key = st[s].key;
+        m.roc = (uint32_t)(est[i] >> 16);
+        m.info = h.enc_start | (st[s].variant << 24);
+        m.len = in_len[i];
+    }
+    meta[i] = m;
 }
 
 // ---------------------------------------------------------------------------
@@ -2558,8 +2604,6 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     F.est = P->est;
     F.skey = P->skey;
     F.pstat = P->pstat;
-    F.olen = P->skey2;
-    F.meta = P->meta;
     F.bcount = P->bcount;
     F.new_index = (unsigned long long *)P->new_index;
     F.abort = P->abort;
@@ -2583,8 +2627,8 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
                        P->new_index, P->win, P->wnew);
     hipLaunchKernelGGL(k_pp_usetbits, gp, blk, 0, stream, P->skey, P->est,
                        P->st, ns, N, P->new_index, P->wnew, P->abort);
-    hipLaunchKernelGGL(k_pp_commit_of, gp, blk, 0, stream, P->pstat, P->skey2,
-                       N, P->abort, b->status, b->out_len);
+    hipLaunchKernelGGL(k_fz_commit, gp, blk, 0, stream, P->pstat, P->skey,
+                       b->in_len, P->st, N, P->abort, b->status, b->out_len);
     hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
                        P->new_index, P->bcount, P->wnew, P->win, P->abort,
                        P->h_abort_dev);
@@ -2599,10 +2643,14 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     if (!ab)
         return 0;
     // declined: the input comes back exactly
+    hipLaunchKernelGGL(k_fz_meta, gp, blk, 0, stream, b->in, b->in_off,
+                       b->in_len, P->pstat, P->skey, P->est, P->st, N, P->meta);
+    PPCHK(hipGetLastError());
     if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
         return -1;
     hipLaunchKernelGGL(k_pp_tail_restore, gp, blk, 0, stream, b->out,
-                       b->out_off, b->in_len, P->skey2, P->meta, P->tsave, N);
+                       b->out_off, b->in_len, P->skey, P->st, P->meta,
+                       P->tsave, N);
     PPCHK(hipGetLastError());
     PPCHK(hipStreamSynchronize(stream));
     *sorted = ab == AB_ORDER;
