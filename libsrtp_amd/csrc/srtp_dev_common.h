@@ -186,11 +186,24 @@ DEV uint32_t rot2(uint32_t x) { return TAB4 ? x : rotl(x, 16); }
 template <int NR>
 struct LaneKey {
     uint32_t rk[4 * (NR + 1)];
+    uint32_t slot = 0xffffffffu;   // the slot rk holds (reload(): ~0 none)
     DEV void load(const srtp_dev_key_t *k)
     {
 #pragma unroll
         for (int i = 0; i < 4 * (NR + 1); i++)
             rk[i] = k->rk[i];
+    }
+    // the schedule of slot s, fetched only when the lane's previous packet
+    // used another key: a lane's packets often share a stream (a stream's
+    // packets in one batch, or configs[3]'s round-robin layout under the
+    // persistent grid's stride), and the 176-704-byte gather per packet is
+    // then a latency the lane need not pay again
+    DEV void reload(const srtp_dev_key_t *keys, uint32_t s)
+    {
+        if (s == slot)
+            return;
+        load(keys + s);
+        slot = s;
     }
     DEV uint32_t operator()(int i) const { return rk[i]; }
 };

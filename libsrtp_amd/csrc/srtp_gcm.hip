@@ -45,7 +45,7 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
     const uint32_t slot = UNIFORM ? A.uni : m.key;
     const srtp_dev_key_t *key = A.keys + slot;
     if constexpr (!UNIFORM) {
-        rk.load(key);
+        rk.reload(A.keys, slot);
         G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
     }
 

@@ -45,93 +45,7 @@ struct IcmPkt {
     uint32_t cb[4];    // counter block, block counter (bytes 14..15) zero
 };
 
-// The arithmetic of one 64-byte chunk b (icm_chunk below), given its four
-// input quads v (zero past the data), for icm_chunk_coop64: header words that are not encrypted,
-// the ROC / terminator / length words of the SHA-1 message tail (sha1.c
-// srtp_sha1_final); the output quads go to oq.  The keystream blocks that
-// any payload byte uses come from the counter cache inside the first epoch
-// (blocks 0..255), from full AES past it.
-template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
-DEV void icm_chunk_core(uint32_t b, const IcmPkt &p, const CtrCache &C,
-                        const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
-                        uint32_t hst[5], const u32x4 (&v)[4],
-                        u32x4 (&oq)[4])
-{
-    const uint32_t q0 = 4 * b;
-    uint32_t ks[4][4];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const uint32_t jj = q0 + t - p.qoff;
-        ks[t][0] = p.cb[0];
-        ks[t][1] = p.cb[1];
-        ks[t][2] = p.cb[2];
-        ks[t][3] = p.cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
-    }
-    if constexpr (NR > 0) {
-        if (p.conf) {
-#pragma unroll
-            for (int g = 0; g < 4; g += ICM_NB) {
-                const int jf = (int)(q0 + g) - (int)p.qoff;
-                if (jf + ICM_NB - 1 < 0 || 16 * jf >= (int)p.P)
-                    continue;
-                auto &kg = *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]);
-                if (jf >= 0 && jf + ICM_NB - 1 < 256) {
-                    uint32_t jb[ICM_NB];
-#pragma unroll
-                    for (int j = 0; j < ICM_NB; j++)
-                        jb[j] = (uint32_t)(jf + j) << 8;
-                    aes_ctr<ICM_NB, NR, TAB4>(kg, jb, C, rk, T);
-                } else {
-                    aes_blocks<ICM_NB, NR, TAB4>(kg, rk, T);
-                }
-            }
-        }
-    }
-    if (NR == 0 || !p.conf) {
-#pragma unroll
-        for (int t = 0; t < 4; t++)
-            ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
-    }
-    uint32_t wv[16];
-#pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const uint32_t q = q0 + t;
-        uint32_t kk[4];
-        ks_shift(ks_prev, ks[t], p.s, kk);
-        if (b < p.bclean) {
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                if (4 * q + u < p.hw)
-                    kk[u] = 0;   // header words are never encrypted
-        }
-        oq[t] = u32x4{ v[t].x ^ kk[0], v[t].y ^ kk[1], v[t].z ^ kk[2],
-                       v[t].w ^ kk[3] };
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            wv[4 * t + u] = bswap(PROTECT ? oq[t][u] : v[t][u]);
-            ks_prev[u] = ks[t][u];
-        }
-    }
-    if (AUTH) {
-        if (64 * b + 64 > p.L) {
-            // message tail: ROC, the 0x80 terminator, zero padding and
-            // the bit length (sha1.c srtp_sha1_final)
-#pragma unroll
-            for (int g = 0; g < 16; g++)
-                wv[g] = tail_word(wv[g], (int)p.L - (int)(64 * b + 4 * g),
-                                  p.roc);
-            if (b == p.nb - 1) {
-                wv[14] = 0;
-                wv[15] = (64 + p.L + 4) * 8;
-            }
-        }
-        sha1_compress(hst, wv);
-    }
-}
-
-// One 64-byte chunk b of a packet in its general form, one lane per packet
-// (the coop64 path below shares icm_chunk_core's arithmetic; this copy keeps
-// the uniform-key kernels' register allocation: 2 % faster on configs[1]): header words that
+// One 64-byte chunk b of a packet in its general form: header words that
 // are not encrypted, quads past the end of the data, the partial last quad
 // (kept in tailq, stored once after the chunk loop: a byte-wise store here,
 // unrolled per quad, costs ~65 VGPRs), and the ROC / terminator / length
@@ -230,69 +144,6 @@ DEV void icm_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
             }
         }
         sha1_compress(hst, wv);
-    }
-}
-
-template <int J>
-DEV uint32_t qbcast32(uint32_t v)   // value of lane (L & ~3) + J
-{
-    return qperm<J | (J << 2) | (J << 4) | (J << 6)>(v);
-}
-
-// chunk b of a wave whose 64 packets all start 64-byte aligned (in and out)
-// and have the same number of chunks -- BASELINE configs[3]'s 172-byte
-// packets in 192-byte slots: every chunk of every packet moves in lane
-// quads.  Load instruction j: lanes 4m..4m+3 read chunk b of packet 16j+m
-// (64 contiguous bytes; quads past a packet's readable end, roundup16(len),
-// are not read); the 4x4 transpose hands each lane its own chunk; after the
-// crypto the output is transposed back and instruction j stores chunk b of
-// packet 16j+m: whole aligned 64-byte segments up to the packet's last full
-// quad, the partial quad as one dwordx1..3 store plus its odd bytes.
-template <int NR, bool TAB4, bool AUTH, bool PROTECT, class KEY>
-DEV void icm_chunk_coop64(uint32_t b, const IcmPkt &p, const CtrCache &C,
-                          const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
-                          uint32_t hst[5])
-{
-    const uint32_t lq = threadIdx.x & 3, q = 4 * b + lq;
-    const uint64_t pin = (uint64_t)(uintptr_t)p.in;
-    const uint64_t pout = (uint64_t)(uintptr_t)p.out;
-    uint32_t Lj[4];
-    Lj[0] = qbcast32<0>(p.L);
-    Lj[1] = qbcast32<1>(p.L);
-    Lj[2] = qbcast32<2>(p.L);
-    Lj[3] = qbcast32<3>(p.L);
-    uint64_t ij[4];
-    ij[0] = qbcast64<0>(pin);
-    ij[1] = qbcast64<1>(pin);
-    ij[2] = qbcast64<2>(pin);
-    ij[3] = qbcast64<3>(pin);
-    u32x4 v[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        v[j] = u32x4{ 0, 0, 0, 0 };
-        if (16 * q < Lj[j])
-            v[j] = *(gcptr)(uintptr_t)(ij[j] + 16 * q);
-    }
-    quad_transpose(v);
-    u32x4 o[4];
-    icm_chunk_core<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, v,
-                                            o);
-    quad_transpose(o);
-    uint64_t oj[4];
-    oj[0] = qbcast64<0>(pout);
-    oj[1] = qbcast64<1>(pout);
-    oj[2] = qbcast64<2>(pout);
-    oj[3] = qbcast64<3>(pout);
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int rem = (int)Lj[j] - (int)(16 * q);
-        uint8_t *dst = (uint8_t *)(uintptr_t)(oj[j] + 16 * q);
-        if (rem >= 16) {
-            *(gptr)dst = o[j];
-        } else if (rem > 0) {
-            const uint32_t w[4] = { o[j].x, o[j].y, o[j].z, o[j].w };
-            store_words_partial(dst, w, rem);
-        }
     }
 }
 
@@ -557,7 +408,7 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
         slot = m.key;
     const srtp_dev_key_t *key = A.keys + slot;
     if constexpr (KM == KM_LANE && NR > 0)
-        rk.load(key);
+        rk.reload(A.keys, slot);
 
     IcmPkt p = make_pkt<NR, AUTH>(A.in + in_off, A.out + out_off, m, key);
 
@@ -576,25 +427,7 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
             C = ctr_cache<NR, TAB4>(p.cb, rk, T);
     }
     uint32_t b = 0;
-    // per-lane keys (many short packets: BASELINE configs[3]), every packet
-    // of the wave 64-byte aligned with as many chunks: the whole packet in
-    // lane quads (icm_chunk_coop64).  Not in the uniform-key kernels: the
-    // extra path costs them 13 spilled VGPRs.
-#ifndef ICM_COOP64
-#define ICM_COOP64 1
-#endif
-    bool all64 = false;
-    if constexpr (KM == KM_LANE && ICM_COOP64) {
-        const uint32_t al64 =
-            (uint32_t)(((uintptr_t)p.in | (uintptr_t)p.out) & 63);
-        all64 = __builtin_amdgcn_ballot_w64(al64 == 0) == ~0ull &&
-                wave_uniform(p.nb);
-    }
-    if (all64) {
-        for (; b < p.nb; b++)
-            icm_chunk_coop64<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev,
-                                                      hst);
-    } else {
+    {
         for (; b < p.bclean && b < p.nb; b++)
             icm_chunk<NR, TAB4, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst,
                                                tailq, prev);
