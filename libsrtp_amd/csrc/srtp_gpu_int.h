@@ -39,17 +39,24 @@ struct srtp_gpu {
 // per-stream count / highest index; the bytes past the packet that its tag
 // overwrites are saved first (an in-place batch the pre-pass then declines
 // is restored from them).
+// one packet's classification, one 16-byte store (dense: a wave writes
+// whole cache lines)
+struct alignas(16) FzRec {
+    uint64_t est;          // the index guessed from the stored one
+    uint32_t skey;         // stream id, ~0 when the packet is not a chain one
+    uint32_t pstat;        // status code
+};
+
 struct IcmFused {
     const uint32_t *in_len, *cap;
     const srtp_dev_stream_t *st;
     const uint32_t *hkey, *hval;
     uint32_t hmask;
-    uint64_t *est;
-    uint32_t *skey, *pstat;
+    FzRec *rec;
+    uint32_t (*tsave)[4];  // the trailer bytes [len, len + trailer) (<= 16)
     uint32_t *bcount;
     unsigned long long *new_index;
     uint32_t *abort;
-    uint32_t (*tsave)[4];   // the trailer bytes [len, len + trailer) (<= 16)
 };
 
 // AES-ICM (+ HMAC-SHA1) kernel arguments

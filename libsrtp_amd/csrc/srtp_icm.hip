@@ -599,6 +599,38 @@ DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, uint64_t e)
     z.run_max = e > z.run_max ? e : z.run_max;
 }
 
+// w = the tn (<= 16) bytes at t, little-endian words; bytes past tn are
+// whatever memory holds
+DEV void fz_tail_save(const uint8_t *t, uint32_t tn, u32x4 &w)
+{
+    const uintptr_t a8 = (uintptr_t)t & ~(uintptr_t)7;
+    const uint32_t o = (uint32_t)((uintptr_t)t & 7), end = o + tn;
+    uint32_t W[6] = { 0, 0, 0, 0, 0, 0 };
+    if (tn == 0) {
+        w = u32x4{ 0, 0, 0, 0 };
+        return;
+    }
+    if (end > 8) {
+        const u32x4 v = *(const u32x4a4 *)a8;
+        W[0] = v[0]; W[1] = v[1]; W[2] = v[2]; W[3] = v[3];
+    } else {
+        const uint2 v = *(const uint2 *)a8;
+        W[0] = v.x; W[1] = v.y;
+    }
+    if (end > 16) {
+        const uint2 v = *(const uint2 *)(a8 + 16);
+        W[4] = v.x; W[5] = v.y;
+    }
+    const bool q = o >= 4;
+    const uint32_t r = o & 3;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t lo = q ? W[k + 1] : W[k];
+        const uint32_t hi = q ? W[k + 2] : W[k + 1];
+        w[k] = __builtin_amdgcn_alignbyte(hi, lo, r);
+    }
+}
+
 DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
 {
     const IcmFused &F = A.fz;
@@ -606,6 +638,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
     const uint32_t len = F.in_len[i];
     const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
     uint32_t code = 0, key = FZ_NOCHAIN, ab = 0;
+    uint64_t e = 0;
     srtp_dev_meta_t m;
     m.key = 0;
     m.roc = 0;
@@ -647,7 +680,6 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
                     code = 8;        // srtp_err_status_cipher_fail
                 const uint64_t idx = z.index;
                 const uint32_t seq = h.seq_len & 0xffffu;
-                uint64_t e;
                 // srtp_prepass.hip guess_index (rdbx.c:112-145)
                 int64_t delta;
                 if (idx > 32768) {
@@ -671,39 +703,30 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
                 }
                 if (delta < 1)
                     ab |= FZ_AB_ORDER;   // the sorted path decides
-                F.est[i] = e;
                 fz_count(F, z, sid, e);
                 if (code == 0) {
                     m.key = z.key;
                     m.roc = (uint32_t)(e >> 16);
                     m.info = h.enc_start | (z.variant << 24);
                     m.len = len;
-                    // the bytes the tag overwrites (in place), for the undo
-                    const uint8_t *t = A.out + A.out_off[i] + len;
-                    const uint32_t tn = z.trailer < 16 ? z.trailer : 16;
-                    uint32_t w[4] = { 0, 0, 0, 0 };
-                    const bool al = ((uintptr_t)t & 3) == 0;
-#pragma unroll
-                    for (uint32_t j = 0; j < 4; j++) {
-                        if (4 * j + 4 <= tn && al) {
-                            w[j] = *(const uint32_t *)(t + 4 * j);
-                            continue;
-                        }
-                        for (uint32_t b = 4 * j; b < tn && b < 4 * j + 4; b++)
-                            w[j] |= (uint32_t)t[b] << (8 * (b & 3));
-                    }
-                    F.tsave[i][0] = w[0];
-                    F.tsave[i][1] = w[1];
-                    F.tsave[i][2] = w[2];
-                    F.tsave[i][3] = w[3];
+#ifndef FZ_EXP_NO_TSAVE
+                    // the bytes the tag overwrites (in place), for the undo:
+                    // at most two loads of the 8-byte-aligned span around
+                    // them (each 8-byte half read holds a byte of
+                    // [len, len + trailer), so no read leaves the pages the
+                    // packet's buffer is in), then a byte-aligned extract
+                    u32x4 w;
+                    fz_tail_save(A.out + A.out_off[i] + len,
+                                 z.trailer < 16 ? z.trailer : 16, w);
+                    *(u32x4 *)F.tsave[i] = w;
+#endif
                 }
             }
         }
     }
     // the descriptor is not stored: a declined batch rebuilds it for the
     // undo (srtp_prepass.hip k_fz_meta), commit derives the lengths
-    F.pstat[i] = code;
-    F.skey[i] = key;
+    *(u32x4 *)&F.rec[i] = u32x4{ (uint32_t)e, (uint32_t)(e >> 32), key, code };
     if (ab)
         atomicOr(F.abort, ab);
     return m;
@@ -768,6 +791,7 @@ void k_icm_hmac(IcmArgs A)
                 const srtp_dev_meta_t m = fz_classify(A, i, z);
                 icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
                     A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+
             }
             fz_flush(A.fz, z);
             return;

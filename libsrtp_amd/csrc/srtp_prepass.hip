@@ -118,6 +118,7 @@ struct PpState {
     uint32_t pu_gen = 0;
     // order-free protect classified in the crypto kernel: the trailer bytes
     // each in-place packet's tag overwrites (16 per packet)
+    FzRec *fzrec = nullptr;   // fused classification records
     uint32_t (*tsave)[4] = nullptr;
 };
 
@@ -650,24 +651,50 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
 // then declined: the bytes past every encrypted packet that its tag
 // overwrote come back (its payload is restored by k_undo)
 __global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
-                                  const uint32_t *in_len, const uint32_t *skey,
+                                  const uint32_t *in_len,
                                   const srtp_dev_stream_t *st,
                                   const srtp_dev_meta_t *meta,
+                                  const FzRec *rec,
                                   const uint32_t (*tsave)[4], uint32_t n)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || SRTP_META_STATUS(meta[i].info))
         return;
-    const uint32_t len = in_len[i], tn = st[skey[i]].trailer;
+    const uint32_t len = in_len[i], tn = st[rec[i].skey].trailer;
     uint8_t *t = arena + off[i] + len;
     for (uint32_t b = 0; b < tn && b < 16; b++)
         t[b] = (uint8_t)(tsave[i][b >> 2] >> (8 * (b & 3)));
 }
 
-// Fused order-free form: the per-packet commit (status, protected length
-// from the stream's trailer) unless the batch was declined
-__global__ void k_fz_commit(const uint32_t *pstat, const uint32_t *skey,
-                            const uint32_t *in_len,
+// Fused order-free form: k_pp_usetbits over the kernel's packet records
+__global__ void k_fz_setbits(const FzRec *rec, const srtp_dev_stream_t *st,
+                             uint32_t ns, uint32_t n,
+                             const uint64_t *new_index, uint32_t *wnew,
+                             uint32_t *abort)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint4 r4 = *(const uint4 *)&rec[i];
+    const uint32_t r[4] = { r4.x, r4.y, r4.z, r4.w };
+    const uint32_t s = r[2];
+    if (s >= ns)
+        return;
+    const uint64_t hi = new_index[s], e = r[0] | ((uint64_t)r[1] << 32);
+    const uint32_t bits = st[s].win_bits;
+    if (hi - e >= bits) {
+        atomicOr(abort, AB_ORDER);
+        return;
+    }
+    const uint32_t bit = bits - 1 - (uint32_t)(hi - e);
+    const uint32_t m = 1u << (bit & 31);
+    if (atomicOr(&wnew[st[s].win_off + (bit >> 5)], m) & m)
+        atomicOr(abort, AB_SEQUENCE);
+}
+
+// ... the per-packet commit (status, protected length from the stream's
+// trailer) unless the batch was declined
+__global__ void k_fz_commit(const FzRec *rec, const uint32_t *in_len,
                             const srtp_dev_stream_t *st, uint32_t n,
                             const uint32_t *abort, int32_t *status,
                             uint32_t *out_len)
@@ -675,17 +702,18 @@ __global__ void k_fz_commit(const uint32_t *pstat, const uint32_t *skey,
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n || *abort)
         return;
-    const uint32_t code = pstat[i];
+    const uint4 r4 = *(const uint4 *)&rec[i];
+    const uint32_t r[4] = { r4.x, r4.y, r4.z, r4.w };
+    const uint32_t code = r[3];
     status[i] = (int32_t)code;
     if (code == 0)
-        out_len[i] = in_len[i] + st[skey[i]].trailer;
+        out_len[i] = in_len[i] + st[r[2]].trailer;
 }
 
 // ... and a declined batch's descriptors, as k_icm_hmac had them, for the
 // undo (k_undo re-applies the keystream)
 __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
-                          const uint32_t *in_len, const uint32_t *pstat,
-                          const uint32_t *skey, const uint64_t *est,
+                          const uint32_t *in_len, const FzRec *rec,
                           const srtp_dev_stream_t *st, uint32_t n,
                           srtp_dev_meta_t *meta)
 {
@@ -697,12 +725,12 @@ __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
     m.roc = 0;
     m.len = 0;
     m.info = 0xff0000u;
-    const uint32_t s = skey[i];
-    if (s != NOCHAIN && pstat[i] == 0) {
+    const uint32_t s = rec[i].skey;
+    if (s != NOCHAIN && rec[i].pstat == 0) {
         const uint64_t off = in_off[i];
         const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
         m.key = st[s].key;
-        m.roc = (uint32_t)(est[i] >> 16);
+        m.roc = (uint32_t)(rec[i].est >> 16);
         m.info = h.enc_start | (st[s].variant << 24);
         m.len = in_len[i];
     }
@@ -2203,6 +2231,9 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipMalloc((void **)&P->meta, c * sizeof(srtp_dev_meta_t)));
     PPCHK(hipMalloc((void **)&P->auth, c));
     PPCHK(hipMalloc((void **)&P->top, c * 8));
+    if (P->fzrec)
+        PPCHK(hipFree(P->fzrec));
+    PPCHK(hipMalloc((void **)&P->fzrec, c * sizeof(FzRec)));
     if (P->tsave)
         PPCHK(hipFree(P->tsave));
     PPCHK(hipMalloc((void **)&P->tsave, c * 16));
@@ -2246,7 +2277,7 @@ void srtp_gpu_pp_free(void *p)
                      P->hist, P->auth, P->top, P->abort, P->bk_off, P->bk_cur,
                      P->rec, P->rec_idx, P->bk_range, P->ch_tile,
                      P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
-                     P->pu_first, P->tsave };
+                     P->pu_first, P->fzrec, P->tsave };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2601,13 +2632,11 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     F.hkey = P->hkey;
     F.hval = P->hval;
     F.hmask = P->hcap - 1;
-    F.est = P->est;
-    F.skey = P->skey;
-    F.pstat = P->pstat;
+    F.rec = P->fzrec;
+    F.tsave = P->tsave;
     F.bcount = P->bcount;
     F.new_index = (unsigned long long *)P->new_index;
     F.abort = P->abort;
-    F.tsave = P->tsave;
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
     cb.in = b->in;
@@ -2625,10 +2654,10 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
         return -1;
     hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
                        P->new_index, P->win, P->wnew);
-    hipLaunchKernelGGL(k_pp_usetbits, gp, blk, 0, stream, P->skey, P->est,
-                       P->st, ns, N, P->new_index, P->wnew, P->abort);
-    hipLaunchKernelGGL(k_fz_commit, gp, blk, 0, stream, P->pstat, P->skey,
-                       b->in_len, P->st, N, P->abort, b->status, b->out_len);
+    hipLaunchKernelGGL(k_fz_setbits, gp, blk, 0, stream, P->fzrec, P->st, ns,
+                       N, P->new_index, P->wnew, P->abort);
+    hipLaunchKernelGGL(k_fz_commit, gp, blk, 0, stream, P->fzrec, b->in_len,
+                       P->st, N, P->abort, b->status, b->out_len);
     hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
                        P->new_index, P->bcount, P->wnew, P->win, P->abort,
                        P->h_abort_dev);
@@ -2644,12 +2673,12 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
         return 0;
     // declined: the input comes back exactly
     hipLaunchKernelGGL(k_fz_meta, gp, blk, 0, stream, b->in, b->in_off,
-                       b->in_len, P->pstat, P->skey, P->est, P->st, N, P->meta);
+                       b->in_len, P->fzrec, P->st, N, P->meta);
     PPCHK(hipGetLastError());
     if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
         return -1;
     hipLaunchKernelGGL(k_pp_tail_restore, gp, blk, 0, stream, b->out,
-                       b->out_off, b->in_len, P->skey, P->st, P->meta,
+                       b->out_off, b->in_len, P->st, P->meta, P->fzrec,
                        P->tsave, N);
     PPCHK(hipGetLastError());
     PPCHK(hipStreamSynchronize(stream));

@@ -247,7 +247,8 @@ def test_device_api_orders_after_torch_default_stream():
 # the order-free form of the many-stream pre-pass (no sort): packets of a
 # stream may arrive in any order inside one replay window
 
-def _interleaved(rng, ssrcs, seq0, per, shuffle_within=0, steps=(1, 1, 1, 2)):
+def _interleaved(rng, ssrcs, seq0, per, shuffle_within=0, steps=(1, 1, 1, 2),
+                 payloads=(0, 33, 160)):
     """per packets per stream, streams interleaved at random; each stream's
     sequence numbers advance by `steps`; with shuffle_within > 0 neighbouring
     packets of one stream may be swapped (reordering inside the window)"""
@@ -268,7 +269,7 @@ def _interleaved(rng, ssrcs, seq0, per, shuffle_within=0, steps=(1, 1, 1, 2)):
     pos = {s: 0 for s in ssrcs}
     pk = []
     for s in order:
-        pk.append(rtp_packet(rng, s, chains[s][pos[s]], rng.choice([0, 33, 160])))
+        pk.append(rtp_packet(rng, s, chains[s][pos[s]], rng.choice(payloads)))
         pos[s] += 1
     return pk
 
@@ -453,22 +454,33 @@ def _device_protect_raw(sess, pkts, caps, fill=0xa5):
         cap.cpu().tolist()
 
 
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm128_nullauth",
+                                  "icm256_hmac32"])
+@pytest.mark.parametrize("caps_mode", ["roomy", "tight"])
 @pytest.mark.parametrize("case", ["duplicate", "unknown_ssrc", "long_chain"])
-def test_fused_order_free_declined_batch_is_restored(case):
+def test_fused_order_free_declined_batch_is_restored(case, caps_mode, name):
     """duplicate -> host path, unknown SSRC -> host path, a stream with more
     packets than its window -> the sorted chain form: statuses and bytes
     equal to the oracle's, and every rejected packet's bytes up to its
-    capacity (its trailer space included) exactly as they were"""
+    capacity (its trailer space included) exactly as they were; "tight":
+    capacities of the tag's length (+0..2), the trailer save reading around
+    the tag space at every byte alignment; tags of 10, 0 and 4 bytes"""
     _gpu()
     rng = random.Random(600 + len(case))
-    ssrcs, lib, orc = _stream_set(40)
+    ssrcs, lib, orc = _stream_set(40, name)
     seq0 = {s: 0xfff0 - 3 * k for k, s in enumerate(ssrcs)}
-    pk = _interleaved(rng, ssrcs, seq0, 150 if case == "long_chain" else 20)
+    pk = _interleaved(rng, ssrcs, seq0, 150 if case == "long_chain" else 20,
+                      payloads=(0, 1, 2, 3, 4, 5, 6, 7, 33, 160))
     if case == "duplicate":
         pk.insert(300, pk[17])
     elif case == "unknown_ssrc":
         pk.insert(100, rtp_packet(rng, 0x0bad0bad, 5, 40))
-    caps = [len(p) + 16 for p in pk]
+    if caps_mode == "roomy":
+        caps = [len(p) + 16 for p in pk]
+    else:
+        tag = {"icm128_hmac80": 10, "icm128_nullauth": 0,
+               "icm256_hmac32": 4}[name]
+        caps = [len(p) + tag + rng.randrange(0, 3) for p in pk]
     st, got, orig, offs, olen = _device_protect_raw(lib, pk, caps)
     for i, p in enumerate(pk):
         rc, ref = orc.protect(p, caps[i])
@@ -492,7 +504,7 @@ def test_fused_order_free_trailer_space_untouched_on_success():
     rng = random.Random(611)
     ssrcs, lib, orc = _stream_set(64)
     seq0 = {s: 7 for s in ssrcs}
-    pk = _interleaved(rng, ssrcs, seq0, 8)
+    pk = _interleaved(rng, ssrcs, seq0, 8, payloads=(0, 1, 2, 3, 4, 5, 6, 7, 160))
     caps = [len(p) + 10 + rng.randrange(0, 40) for p in pk]
     st, got, orig, offs, olen = _device_protect_raw(lib, pk, caps)
     assert lib.prepass_stats() == (1, 0)
