@@ -113,6 +113,13 @@ def parse():
                     "launches, which run synchronously with timing on)")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target wall time of the CPU-baseline sample")
+    ap.add_argument("--reorder", type=float, default=0.0,
+                    help="--op unprotect: fraction of arrivals swapped with "
+                    "one up to 32 places later (network reordering)")
+    ap.add_argument("--dup", type=float, default=0.0,
+                    help="--op unprotect: fraction of arrivals that are a "
+                    "copy of a packet up to 64 places earlier (duplicates; "
+                    "the packet they displace is lost): replay_fail")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
                     help="auto: measure roofline.traffic and roofline.issue "
                          "with rocprofv3 PMC passes (child processes, N=1 "
@@ -555,6 +562,28 @@ def dry_run(a, world, rank, json_out):
         dist.destroy_process_group()
 
 
+def arrival_rows(n, reorder, dup, seed):
+    """arrival order of a receive batch (the rows of the sent batch): local
+    swaps of up to 32 places, then duplicates -- a copy of a packet that
+    arrived up to 64 places earlier, in place of a packet that is lost"""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    rows = np.arange(n, dtype=np.int64)
+    for i in np.nonzero(rng.random(n) < reorder)[0]:
+        j = min(n - 1, int(i) + int(rng.integers(1, 33)))
+        rows[i], rows[j] = rows[j], rows[i]
+    pos = np.nonzero(rng.random(n) < dup)[0]
+    pos = pos[pos >= 64]
+    isdup = np.zeros(n, dtype=bool)
+    isdup[pos] = True
+    for i in pos:
+        src = int(i) - int(rng.integers(1, 65))
+        while isdup[src]:
+            src -= 1
+        rows[i] = rows[src]
+    return rows, len(pos)
+
+
 def result_line(a, world, n, payload, tag, dt, roofline, cpu, prepass):
     rtp_len = 12 + payload
     value = n * a.steps * world / dt
@@ -582,7 +611,9 @@ def result_line(a, world, n, payload, tag, dt, roofline, cpu, prepass):
                        (a.config, world > 1), None),
                    "submission": "pipelined (srtp_protect_device_async)"
                    if a.pipelined and a.op == "protect"
-                   else "synchronous (srtp_%s_device)" % a.op},
+                   else "synchronous (srtp_%s_device)" % a.op,
+                   **({"arrival": {"reorder": a.reorder, "dup": a.dup}}
+                      if a.reorder or a.dup else {})},
         "payload_GBps": value * payload / 1e9,
         "roofline": roofline,
         "cpu_baseline": cpu,
@@ -716,6 +747,9 @@ def run_gpu(a, world, rank, local, json_out):
     statuses = [torch.full((n,), -1, dtype=torch.int32, device=dev)
                 for _ in range(nb)]
     stream = torch.cuda.current_stream().cuda_stream
+    expect_dups = []
+    if (a.reorder or a.dup) and a.op != "unprotect":
+        raise SystemExit("--reorder / --dup apply to --op unprotect")
     if a.op == "unprotect":
         # the sender's side, untimed: protect every batch in place; the
         # receiver (`sess`) then unprotects them in order
@@ -729,6 +763,14 @@ def run_gpu(a, world, rank, local, json_out):
                 raise RuntimeError("bench: protecting the receive batches")
         snd.close()
         in_len = srtp_len
+        if a.reorder or a.dup:
+            # network arrival order, built untimed: each receive batch's
+            # packets permuted (and duplicated) in HBM
+            for k in range(nb):
+                rows, ndup = arrival_rows(n, a.reorder, a.dup, 1000 + k)
+                arenas[k] = arenas[k].view(n, slot)[
+                    torch.from_numpy(rows).to(dev)].reshape(-1)
+                expect_dups.append(ndup)
     sess.set_timing(True)
     # out_len: capacities in, lengths out.  Filled once: a step leaves the
     # lengths it produced (<= slot), which are exactly the capacities the
@@ -772,7 +814,13 @@ def run_gpu(a, world, rank, local, json_out):
         if not warm_ms:
             raise SystemExit("--pipelined needs --warmup >= 1 (kernel timing)")
         kms = warm_ms[1:] or warm_ms
-    bad = sum(int((st != 0).sum()) for st in statuses)
+    if expect_dups:
+        # every displaced copy is replay_fail (status 9), all else accepted
+        bad = sum(int(((st != 0) & (st != 9)).sum()) +
+                  abs(int((st == 9).sum()) - d)
+                  for st, d in zip(statuses, expect_dups))
+    else:
+        bad = sum(int((st != 0).sum()) for st in statuses)
     dev_b, host_b = sess.prepass_stats()
     if bad or host_b != host_b0:
         raise SystemExit("bench: %d packets with a nonzero status, %d batches "

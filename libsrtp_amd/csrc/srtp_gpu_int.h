@@ -54,8 +54,13 @@ struct IcmFused {
     uint32_t hmask;
     FzRec *rec;
     uint32_t (*tsave)[4];  // the trailer bytes [len, len + trailer) (<= 16)
-    uint32_t *bcount;
-    unsigned long long *new_index;
+    // per stream: packets touched (low 32 bits) and chain packets (high),
+    // highest and lowest chain index, and a bitmap of the chain indices mod
+    // M = the window size rounded up to a power of two (M / 32 words at
+    // word 2 * win_off; zero between batches)
+    unsigned long long *cnt;
+    unsigned long long *new_index, *emin;
+    uint32_t *bmap;
     uint32_t *abort;
 };
 

@@ -565,38 +565,52 @@ constexpr uint32_t FZ_AB_UNKNOWN = 1, FZ_AB_INELIGIBLE = 2, FZ_AB_ORDER = 8;
 // What a lane keeps between its packets: the last stream it looked up
 // (a lane's packets of a batch are often one stream's: the persistent grid's
 // stride is a multiple of the stream count in round-robin batches), and the
-// running packet count / highest index of its current stream, flushed with
-// one atomic pair when the stream changes and at the end.  The per-packet
-// atomics stalled the crypto behind them (an atomic stays in vmcnt for
-// ~3000 cycles under load, MI355X_MICROARCH.md).
+// running counts / highest / lowest index of its current stream, flushed
+// with one atomic triple when the stream changes and at the end.  The
+// per-packet atomics stalled the crypto behind them (an atomic stays in
+// vmcnt for ~3000 cycles under load, MI355X_MICROARCH.md); the one
+// per-packet atomic left, the bitmap bit, returns nothing and is not waited
+// on.
 struct FzLane {
     uint32_t ssrc, sid;            // cached lookup (sid ~0: none)
     uint32_t key, variant, flags, trailer, dir;
+    uint32_t boff, bmask;          // bitmap word offset, M - 1
     uint64_t index;
-    uint32_t run_sid, run_cnt;     // current run (run_sid ~0: none)
-    uint64_t run_max;
+    uint32_t run_sid;              // current run (run_sid ~0: none)
+    uint64_t run_cnt;              // packets | chain packets << 32
+    uint64_t run_max, run_min;
 };
 
 DEV void fz_flush(const IcmFused &F, FzLane &z)
 {
     if (z.run_sid != FZ_NOCHAIN) {
-        atomicAdd(&F.bcount[z.run_sid], z.run_cnt);
-        if (z.run_max)
+        atomicAdd(&F.cnt[z.run_sid], (unsigned long long)z.run_cnt);
+        if (z.run_cnt >> 32) {
             atomicMax(&F.new_index[z.run_sid], (unsigned long long)z.run_max);
+            atomicMin(&F.emin[z.run_sid], (unsigned long long)z.run_min);
+        }
     }
     z.run_sid = FZ_NOCHAIN;
     z.run_cnt = 0;
     z.run_max = 0;
+    z.run_min = ~0ull;
 }
 
-DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, uint64_t e)
+// a packet of stream sid; chain packets (index e) also set their bitmap bit
+DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, bool chain,
+                  uint64_t e)
 {
     if (sid != z.run_sid) {
         fz_flush(F, z);
         z.run_sid = sid;
     }
-    z.run_cnt++;
-    z.run_max = e > z.run_max ? e : z.run_max;
+    z.run_cnt += chain ? 1ull | (1ull << 32) : 1ull;
+    if (chain) {
+        z.run_max = e > z.run_max ? e : z.run_max;
+        z.run_min = e < z.run_min ? e : z.run_min;
+        const uint32_t r = (uint32_t)e & z.bmask;
+        atomicOr(&F.bmap[z.boff + (r >> 5)], 1u << (r & 31));
+    }
 }
 
 // w = the tn (<= 16) bytes at t, little-endian words; bytes past tn are
@@ -658,6 +672,9 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
                 z.trailer = S.trailer;
                 z.dir = S.dir;
                 z.index = S.index;
+                z.boff = 2 * S.win_off;
+                z.bmask = (S.win_bits > 32 ? 2u << (31 - __clz(S.win_bits - 1))
+                                           : 32u) - 1;
             }
         }
         const uint32_t sid = z.sid;
@@ -668,10 +685,10 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
                 ab |= FZ_AB_INELIGIBLE;
             if (F.cap[i] < len + z.trailer) {
                 code = 28;           // srtp_err_status_buffer_small
-                fz_count(F, z, sid, 0);
+                fz_count(F, z, sid, false, 0);
             } else if (h.enc_start > len) {
                 code = 21;           // srtp_err_status_parse_err
-                fz_count(F, z, sid, 0);
+                fz_count(F, z, sid, false, 0);
             } else {
                 key = sid;
                 // aes_icm.c:317-322: at most 0xffff keystream blocks
@@ -703,7 +720,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
                 }
                 if (delta < 1)
                     ab |= FZ_AB_ORDER;   // the sorted path decides
-                fz_count(F, z, sid, e);
+                fz_count(F, z, sid, true, e);
                 if (code == 0) {
                     m.key = z.key;
                     m.roc = (uint32_t)(e >> 16);
@@ -787,6 +804,7 @@ void k_icm_hmac(IcmArgs A)
             z.run_sid = FZ_NOCHAIN;
             z.run_cnt = 0;
             z.run_max = 0;
+            z.run_min = ~0ull;
             for (uint32_t i = first; i < A.n; i += stride) {
                 const srtp_dev_meta_t m = fz_classify(A, i, z);
                 icm_packet<NR, TAB4, AUTH, PROTECT, KM>(

@@ -120,6 +120,10 @@ struct PpState {
     // each in-place packet's tag overwrites (16 per packet)
     FzRec *fzrec = nullptr;   // fused classification records
     uint32_t (*tsave)[4] = nullptr;
+    // per stream: counts, lowest chain index; index bitmaps (2 x nwords)
+    unsigned long long *fz_cnt = nullptr, *fz_emin = nullptr;
+    uint32_t *fz_bmap = nullptr;
+    uint32_t bmap_cap = 0;
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -666,48 +670,110 @@ __global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
         t[b] = (uint8_t)(tsave[i][b >> 2] >> (8 * (b & 3)));
 }
 
-// Fused order-free form: k_pp_usetbits over the kernel's packet records
-__global__ void k_fz_setbits(const FzRec *rec, const srtp_dev_stream_t *st,
-                             uint32_t ns, uint32_t n,
-                             const uint64_t *new_index, uint32_t *wnew,
-                             uint32_t *abort)
+// Fused order-free form (IcmFused): the per-stream aggregates start at
+// zero / empty (the bitmaps are zero between batches)
+__global__ void k_fz_reset(uint32_t *abort, unsigned long long *cnt,
+                           unsigned long long *new_index,
+                           unsigned long long *emin, uint32_t ns)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
-        return;
-    const uint4 r4 = *(const uint4 *)&rec[i];
-    const uint32_t r[4] = { r4.x, r4.y, r4.z, r4.w };
-    const uint32_t s = r[2];
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s == 0)
+        *abort = 0;
     if (s >= ns)
         return;
-    const uint64_t hi = new_index[s], e = r[0] | ((uint64_t)r[1] << 32);
-    const uint32_t bits = st[s].win_bits;
-    if (hi - e >= bits) {
-        atomicOr(abort, AB_ORDER);
-        return;
-    }
-    const uint32_t bit = bits - 1 - (uint32_t)(hi - e);
-    const uint32_t m = 1u << (bit & 31);
-    if (atomicOr(&wnew[st[s].win_off + (bit >> 5)], m) & m)
-        atomicOr(abort, AB_SEQUENCE);
+    cnt[s] = 0;
+    new_index[s] = 0;
+    emin[s] = ~0ull;
 }
 
-// ... the per-packet commit (status, protected length from the stream's
-// trailer) unless the batch was declined
-__global__ void k_fz_commit(const FzRec *rec, const uint32_t *in_len,
-                            const srtp_dev_stream_t *st, uint32_t n,
-                            const uint32_t *abort, int32_t *status,
-                            uint32_t *out_len)
+// ... per stream, after the crypto: the conditions of the order-free form
+// (k_pp_usetbits restated over the aggregates: every chain index within one
+// window of the highest -- else AB_ORDER, the sorted path decides -- and as
+// many distinct indices as chain packets -- else AB_SEQUENCE, two packets
+// share an index: host), the window shifted by the advance with the batch's
+// bits (rdbx_add, rdbx.c:253-270), and the bitmap cleared for the next batch
+__global__ void k_fz_stream(const srtp_dev_stream_t *st, uint32_t ns,
+                            const unsigned long long *cnt,
+                            const unsigned long long *new_index,
+                            const unsigned long long *emin, uint32_t *bmap,
+                            const uint32_t *win, uint32_t *wnew,
+                            uint32_t *abort)
 {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || *abort)
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns)
         return;
-    const uint4 r4 = *(const uint4 *)&rec[i];
-    const uint32_t r[4] = { r4.x, r4.y, r4.z, r4.w };
-    const uint32_t code = r[3];
-    status[i] = (int32_t)code;
-    if (code == 0)
-        out_len[i] = in_len[i] + st[r[2]].trailer;
+    const uint32_t chain = (uint32_t)(cnt[s] >> 32);
+    if (!chain)
+        return;
+    const srtp_dev_stream_t S = st[s];
+    const uint64_t hi = new_index[s], lo = emin[s];
+    const uint32_t bits = S.win_bits, words = bits >> 5;
+    const uint32_t M = bits > 32 ? 2u << (31 - __clz(bits - 1)) : 32u;
+    const uint32_t mw = M >> 5;
+    uint32_t *bm = bmap + 2 * S.win_off;
+    const uint32_t *w = win + S.win_off;
+    uint32_t *o = wnew + S.win_off;
+    const uint64_t adv = hi - S.index;
+    // window bit p <-> index hi - bits + 1 + p <-> bitmap residue of it
+    const uint32_t base = (uint32_t)(hi - bits + 1);
+    uint32_t seen = 0;
+    for (uint32_t j = 0; j < words; j++) {
+        uint32_t v = 0;
+        if (adv < bits) {
+            const uint32_t q = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+            const uint32_t a = j + q < words ? w[j + q] : 0u;
+            const uint32_t b = j + q + 1 < words ? w[j + q + 1] : 0u;
+            v = bi ? (a >> bi) | (b << (32 - bi)) : a;
+        }
+        const uint32_t r0 = (base + 32 * j) & (M - 1), sh = r0 & 31;
+        const uint32_t b0 = bm[r0 >> 5], b1 = bm[((r0 >> 5) + 1) & (mw - 1)];
+        const uint32_t x = sh ? (b0 >> sh) | (b1 << (32 - sh)) : b0;
+        seen += __popc(x);
+        o[j] = v | x;
+    }
+    for (uint32_t j = 0; j < mw; j++)
+        bm[j] = 0;
+    if (hi - lo >= bits)
+        atomicOr(abort, AB_ORDER);
+    else if (seen != chain)
+        atomicOr(abort, AB_SEQUENCE);   // two packets with one index: host
+}
+
+// ... then, unless the batch was declined, every packet's status and
+// protected length (from the stream's trailer) and every touched stream's
+// state, in one launch over max(n, ns) threads
+__global__ void k_fz_commit(const FzRec *rec, const uint32_t *in_len,
+                            srtp_dev_stream_t *st, uint32_t n, uint32_t ns,
+                            const unsigned long long *cnt,
+                            const unsigned long long *new_index,
+                            const uint32_t *wnew, uint32_t *win,
+                            const uint32_t *abort, int32_t *status,
+                            uint32_t *out_len, uint32_t *pub)
+{
+    publish_abort(pub, abort);
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (*abort)
+        return;
+    if (i < n) {
+        const uint4 r = *(const uint4 *)&rec[i];
+        status[i] = (int32_t)r.w;
+        if (r.w == 0)
+            out_len[i] = in_len[i] + st[r.z].trailer;
+    }
+    if (i < ns) {
+        const uint32_t c = (uint32_t)cnt[i];
+        if (!c)
+            return;
+        st[i].uses += c;
+        st[i].dir |= SRTP_DIR_TX;
+        const uint64_t ni = new_index[i];
+        if (ni == 0)
+            return;
+        st[i].index = ni;
+        const uint32_t off = st[i].win_off, words = st[i].win_bits >> 5;
+        for (uint32_t w = 0; w < words; w++)
+            win[off + w] = wnew[off + w];
+    }
 }
 
 // ... and a declined batch's descriptors, as k_icm_hmac had them, for the
@@ -2277,7 +2343,8 @@ void srtp_gpu_pp_free(void *p)
                      P->hist, P->auth, P->top, P->abort, P->bk_off, P->bk_cur,
                      P->rec, P->rec_idx, P->bk_range, P->ch_tile,
                      P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
-                     P->pu_first, P->fzrec, P->tsave };
+                     P->pu_first, P->fzrec, P->tsave, P->fz_cnt,
+                     P->fz_emin, P->fz_bmap };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2295,15 +2362,17 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
     uint32_t c1 = P->ns_cap, c2 = P->ns_cap, c5 = P->ns_cap,
              c6 = P->ns_cap, c7 = P->ns_cap, c8 = P->ns_cap, c9 = P->ns_cap,
-             c3 = P->nwords_cap;
+             c10 = P->ns_cap, c11 = P->ns_cap, c3 = P->nwords_cap;
     if (regrow(&P->st, &P->ns_cap, ns + 1) ||
         regrow(&P->bcount, &c1, ns + 1) || regrow(&P->new_index, &c2, ns + 1) ||
         regrow(&P->seg_first, &c5, ns + 1) ||
         regrow(&P->bcount2, &c6, ns + 1) ||
         regrow(&P->new_index2, &c7, ns + 1) ||
         regrow(&P->bk_off, &c8, ns + 1) || regrow(&P->bk_cur, &c9, ns + 1) ||
+        regrow(&P->fz_cnt, &c10, ns + 1) || regrow(&P->fz_emin, &c11, ns + 1) ||
         regrow(&P->win, &P->nwords_cap, nwords + 1) ||
-        regrow(&P->wnew, &c3, nwords + 1))
+        regrow(&P->wnew, &c3, nwords + 1) ||
+        regrow(&P->fz_bmap, &P->bmap_cap, 2 * nwords + 2))
         return -1;
     if (hcap > P->hcap_cap || !P->hkey) {
         uint32_t c4 = P->hcap_cap;
@@ -2330,6 +2399,7 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     P->ns = ns;
     P->nwords = nwords;
     P->hcap = hcap;
+    PPCHK(hipMemsetAsync(P->fz_bmap, 0, (2ull * nwords + 2) * 4, stream));
     PPCHK(hipMemcpyAsync(P->st, streams, ns * sizeof *streams,
                          hipMemcpyHostToDevice, stream));
     if (nwords) {
@@ -2622,9 +2692,9 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
     *sorted = false;
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
-    hipLaunchKernelGGL(k_pp_reset, dim3(ns / 256 + 1), blk, 0, stream,
-                       P->abort, P->bcount, (unsigned long long *)P->new_index,
-                       nullptr, nullptr, ns);
+    unsigned long long *hi = (unsigned long long *)P->new_index;
+    hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
+                       P->abort, P->fz_cnt, hi, P->fz_emin, ns);
     IcmFused F;
     F.in_len = b->in_len;
     F.cap = b->out_len;
@@ -2634,8 +2704,10 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     F.hmask = P->hcap - 1;
     F.rec = P->fzrec;
     F.tsave = P->tsave;
-    F.bcount = P->bcount;
-    F.new_index = (unsigned long long *)P->new_index;
+    F.cnt = P->fz_cnt;
+    F.new_index = hi;
+    F.emin = P->fz_emin;
+    F.bmap = P->fz_bmap;
     F.abort = P->abort;
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
@@ -2650,20 +2722,22 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     cb.stream = stream;
     cb.abort = nullptr;   // the kernel itself classifies: it always runs
     cb.fused = &F;
+    // a failed step may leave bitmap bits behind: clear them all
+    auto fail = [&]() {
+        (void)hipMemsetAsync(P->fz_bmap, 0, (2ull * P->nwords + 2) * 4, stream);
+        return -1;
+    };
     if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "fused crypto"))
-        return -1;
-    hipLaunchKernelGGL(k_pp_window, gs, blk, 0, stream, P->st, ns,
-                       P->new_index, P->win, P->wnew);
-    hipLaunchKernelGGL(k_fz_setbits, gp, blk, 0, stream, P->fzrec, P->st, ns,
-                       N, P->new_index, P->wnew, P->abort);
-    hipLaunchKernelGGL(k_fz_commit, gp, blk, 0, stream, P->fzrec, b->in_len,
-                       P->st, N, P->abort, b->status, b->out_len);
-    hipLaunchKernelGGL(k_pp_commit_stream, gs, blk, 0, stream, P->st, ns,
-                       P->new_index, P->bcount, P->wnew, P->win, P->abort,
+        return fail();
+    hipLaunchKernelGGL(k_fz_stream, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
+                       hi, P->fz_emin, P->fz_bmap, P->win, P->wnew, P->abort);
+    const uint32_t nc = N > ns ? N : ns;
+    hipLaunchKernelGGL(k_fz_commit, dim3((nc + 255) / 256), blk, 0, stream,
+                       P->fzrec, b->in_len, P->st, N, ns, P->fz_cnt, hi,
+                       P->wnew, P->win, P->abort, b->status, b->out_len,
                        P->h_abort_dev);
-    PPCHK(hipGetLastError());
-    if (pp_step(stream, "fused commit"))
-        return -1;
+    if (hipGetLastError() != hipSuccess || pp_step(stream, "fused commit"))
+        return fail();
     PPCHK(hipStreamSynchronize(stream));
     if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
         PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));

@@ -514,3 +514,49 @@ def test_fused_order_free_trailer_space_untouched_on_success():
         o = offs[i]
         assert got[o:o + olen[i]] == ref
         assert got[o + olen[i]:o + caps[i]] == orig[o + olen[i]:o + caps[i]]
+
+
+def test_fused_window_sizes_jumps_and_state():
+    """the fused order-free form's replay windows (srtp_prepass.hip
+    k_fz_stream: a bitmap of the batch's indices mod the window size rounded
+    up to a power of two, merged into the shifted stored window) at window
+    sizes 64, 96, 160 and 1024, with streams that jump past their whole
+    window inside the batch; the windows left behind are probed packet by
+    packet through the host path (skipped indices accepted, sent ones
+    replay_fail, ones past the window replay_old) against the oracle"""
+    _gpu()
+    rng = random.Random(612)
+    wins = [64, 96, 160, 1024]
+    ssrcs = [0x21000000 + 5 * k for k in range(48)]
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k, window=wins[k % 4])
+            for k, s in enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(100, 0xf000) for s in ssrcs}
+    sent = {s: [] for s in ssrcs}
+    for b in range(3):
+        if b == 1:   # every third stream jumps ahead by 70 .. 3000
+            for s in ssrcs[::3]:
+                seq0[s] += rng.randrange(70, 3000)
+        pk = _interleaved(rng, ssrcs, seq0, 24, shuffle_within=0.3,
+                          payloads=(0, 5, 160))
+        for p in pk:
+            sent[int.from_bytes(p[8:12], "big")].append(
+                int.from_bytes(p[2:4], "big"))
+        _check(lib, orc, pk, [len(p) + 16 for p in pk])
+        assert lib.prepass_last_abort() == 0, (b, lib.prepass_last_abort())
+    assert lib.prepass_stats() == (3, 0)
+    assert lib.prepass_sorted_batches() == 0
+    for k, s in enumerate(ssrcs):
+        assert lib.get_roc(s)[1] == orc.get_roc(s)[1]
+        top = (seq0[s] - 1) & 0xffff
+        probes = {top - d for d in (1, 2, 3, 7, 40, 63, 64, 65, 95, 96, 97,
+                                    159, 160, 161, 700, 1023, 1024, 1100)}
+        probes |= set(rng.sample(sent[s], 3))
+        for q in sorted(probes):
+            if not 0 < q < 0x10000:
+                continue
+            p = rtp_packet(rng, s, q & 0xffff, 20)
+            st, out = lib.protect(p, len(p) + 16)
+            rc, ref = orc.protect(p, len(p) + 16)
+            assert st == rc, (k, wins[k % 4], top - q, st, rc)
+            assert rc or out == ref
