@@ -224,11 +224,12 @@ int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
  * the GPU advances it, and the host pulls it back before any host-side use
  * of stream state. */
 enum {
-    SRTP_DS_ELIGIBLE = 1,    /* protect: sender/unknown direction, no MKI,
-                                no pending ROC */
+    SRTP_DS_ELIGIBLE = 1,    /* protect: sender/unknown direction, no
+                                pending ROC (MKI: the devtab's key index) */
     SRTP_DS_ICM_CONF = 2,    /* AES-ICM encrypting: 2^16 keystream blocks */
     SRTP_DS_RX_ELIGIBLE = 4, /* unprotect: receiver/unknown direction, no
-                                MKI, no pending ROC */
+                                pending ROC (MKI: packets carrying another
+                                key's MKI abort to the host) */
     SRTP_DS_AEAD = 8         /* AES-GCM: key usage counted before the tag
                                 check (srtp.c:2390-2406) */
 };
@@ -244,6 +245,12 @@ typedef struct srtp_dev_stream {
     uint32_t win_bits;  /* replay window bits (multiple of 32)               */
     uint32_t win_off;   /* word offset of the window in the window arena     */
     uint32_t dir;       /* SRTP_DIR_* bits set by device batches             */
+    uint32_t mki;       /* MKI streams: MKI bytes | their distance from the
+                           packet end << 16 (tag + MKI; AES-GCM: MKI only,
+                           srtp.c:1961-2016); 0 without MKI.  `key` is the
+                           slot of the key device batches use (the host's
+                           devtab mki_j-th master key)                     */
+    uint32_t rsv;
     uint64_t index;     /* rdbx index (ROC << 16 | SEQ)                      */
     uint64_t uses;      /* packets charged to the key since the upload       */
 } srtp_dev_stream_t;

@@ -201,6 +201,12 @@ typedef struct {
     void *async_stream;     /* ... on this stream                          */
     int async_err;          /* a queued batch failed on the GPU: sticky,
                                every later packet call returns _fail      */
+    /* MKI streams (srtp.c:1961-2036): device batches use master key mki_j
+     * of each; protect batches select it by a uniform mki_index, receive
+     * batches follow the key the host path last matched (rx_hint) */
+    int has_mki;
+    uint32_t mki_j;
+    uint32_t rx_hint;
 } devtab_t;
 
 struct srtp_ctx_t_ {
@@ -2021,6 +2027,8 @@ static int pre_unprotect(srtp_t ctx, provset_t *ps, const pkt_sum_t *s,
     u->sverdict = un_static(kst, s, cap, mki_bytes, &k, meta);
     if (u->sverdict)
         return 0;
+    if (kst->use_mki)   /* the key the next device batch takes to be in use */
+        ctx->dt.rx_hint = (uint32_t)(k - kst->keys->k);
     meta->roc = (uint32_t)(est >> 16);
     const int known = u->gpu && u->est == est;
     int accept, run = 0;
@@ -2484,14 +2492,6 @@ static int run_gpu(srtp_t ctx, int op, size_t n, const uint8_t *in,
 
 static size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
-/* 1 if any mki_index[i] is non-zero (the device pre-pass has no MKI) */
-static int memchr_nonzero(const size_t *v, size_t n)
-{
-    for (size_t i = 0; i < n; i++)
-        if (v[i])
-            return 1;
-    return 0;
-}
 
 /* k_xrtp verdicts of a protect batch: a header-extension parse error
  * (srtp_process_header_encryption / srtp_cryptex_protect, srtp.c:2745-2762)
@@ -2517,7 +2517,7 @@ static int xrtp_protect_results(srtp_t ctx, size_t n, srtp_err_status_t *status,
  * batch API over host buffers
  * ---------------------------------------------------------------------- */
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
-                               int async);
+                               int async, const size_t *mki_wide);
 static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b);
 
 /* a parallel for over [0, n) on up to 8 host threads: the gather into and
@@ -2598,6 +2598,7 @@ static void scatter_part(void *p, size_t lo, size_t hi)
 static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
                              const uint8_t *const *in, const size_t *in_len,
                              uint8_t *const *out, size_t *out_len,
+                             const size_t *mki_index,
                              srtp_err_status_t *status)
 {
     if (n < 64 || n > 0x7fffffffu)
@@ -2641,7 +2642,7 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
     if (async_drain(ctx))   /* staged on the library's own stream */
         return -1;
     int fast = unprotect ? unprotect_device_fast(ctx, &b)
-                         : protect_device_fast(ctx, &b, 0);
+                         : protect_device_fast(ctx, &b, 0, mki_index);
     if (fast <= 0)
         return fast;
     ctx->dt.fast_batches++;
@@ -2668,9 +2669,11 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
     ASYNC_DRAIN_CHECK(ctx);
     if (!n)
         return srtp_err_status_ok;
-    if (!mki_index || !memchr_nonzero(mki_index, n)) {
+    {
+        /* MKI: one mki_index for the whole batch runs on the device
+         * (protect_device_fast, dev_mki_select) */
         int fast = batch_device_fast(ctx, 0, n, rtp, rtp_len, srtp, srtp_len,
-                                     status);
+                                     mki_index, status);
         if (fast < 0) {
             log_msg(srtp_log_level_error, srtp_gpu_last_error());
             return srtp_err_status_fail;
@@ -2930,7 +2933,7 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
     ASYNC_DRAIN_CHECK(ctx);
     if (!n)
         return srtp_err_status_ok;
-    int fast = batch_device_fast(ctx, 1, n, srtp, srtp_len, rtp, rtp_len,
+    int fast = batch_device_fast(ctx, 1, n, srtp, srtp_len, rtp, rtp_len, NULL,
                                  status);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
@@ -3109,9 +3112,12 @@ static int dev_build(srtp_t ctx)
     dt->max_trailer = 0;
     int first = 1, rx_first = 1;
     uint32_t woff = 0;
+    dt->has_mki = 0;
     for (uint32_t sid = 0; sid < ns; sid++) {
         srtp_stream_ctx_t *st = ctx->list[sid];
-        const hkey_t *k = &st->keys->k[0];
+        /* MKI streams: master key mki_j, ineligible if they have fewer */
+        const int mki_ok = !st->use_mki || dt->mki_j < st->keys->n;
+        const hkey_t *k = &st->keys->k[st->use_mki && mki_ok ? dt->mki_j : 0];
         srtp_dev_stream_t *d = &dt->hs[sid];
         dt->sv[sid] = st;
         st->dev_sid = sid;
@@ -3119,10 +3125,18 @@ static int dev_build(srtp_t ctx)
         d->key = k->slot;
         d->variant = k->variant;
         d->flags = 0;
+        d->mki = 0;
+        d->rsv = 0;
+        if (st->use_mki) {
+            dt->has_mki = 1;
+            const uint32_t back = (uint32_t)st->mki_size +
+                (k->family == SRTP_DEV_GCM ? 0u : (uint32_t)k->tag_len);
+            d->mki = (uint32_t)st->mki_size | (back << 16);
+        }
         /* header-extension encryption / cryptex streams and routed keys:
          * host pre-pass */
         const int xs = k->variant >= SRTP_VARIANT_X;
-        if (!st->use_mki && st->rdbx.pending_roc == 0 && !xs &&
+        if (mki_ok && st->rdbx.pending_roc == 0 && !xs &&
             st->direction != DIR_RECEIVER) {
             d->flags |= SRTP_DS_ELIGIBLE;
             if (k->num_left < dt->num_left_min)
@@ -3138,7 +3152,7 @@ static int dev_build(srtp_t ctx)
             if (tr > dt->max_trailer)
                 dt->max_trailer = tr;
         }
-        if (!st->use_mki && st->rdbx.pending_roc == 0 && !xs &&
+        if (mki_ok && st->rdbx.pending_roc == 0 && !xs &&
             st->direction != DIR_SENDER) {
             d->flags |= SRTP_DS_RX_ELIGIBLE;
             if (k->num_left < dt->num_left_min)
@@ -3215,6 +3229,51 @@ static int async_drain(srtp_t ctx)
     return 0;
 }
 
+static void dev_pull(srtp_t ctx);
+
+/* MKI sessions: the master key a protect batch selects (mki_index, one per
+ * packet, srtp.c:2536-2545) must be one for the whole batch to run on the
+ * device; a change of key rebuilds the device table (the device-advanced
+ * state comes back first, its key uses charged to the previous key).
+ * Returns 1 when the batch must take the host path. */
+static int dev_mki_select(srtp_t ctx, const uint8_t *m8, const size_t *m64,
+                          size_t n)
+{
+    devtab_t *dt = &ctx->dt;
+    const size_t j = m64 ? m64[0] : m8 ? m8[0] : 0;
+    for (size_t i = 1; (m8 || m64) && i < n; i++)
+        if ((m64 ? m64[i] : m8[i]) != j) {
+            dt->last_abort = 256;
+            return 1;
+        }
+    if (j > 0xffffffffu) {
+        dt->last_abort = 256;
+        return 1;
+    }
+    if ((uint32_t)j != dt->mki_j) {
+        dev_pull(ctx);
+        dt->mki_j = (uint32_t)j;
+        if (dev_build(ctx))
+            return 1;
+    }
+    return 0;
+}
+
+/* ... and the key a receive batch's MKI streams are taken to use: the one
+ * the host path matched last (a packet carrying another key's MKI sends the
+ * batch back to the host, srtp_prepass.hip AB_MKI) */
+static int dev_mki_rx(srtp_t ctx)
+{
+    devtab_t *dt = &ctx->dt;
+    if (dt->rx_hint != dt->mki_j) {
+        dev_pull(ctx);
+        dt->mki_j = dt->rx_hint;
+        if (dev_build(ctx))
+            return 1;
+    }
+    return 0;
+}
+
 static void dev_pull(srtp_t ctx)
 {
     devtab_t *dt = &ctx->dt;
@@ -3239,7 +3298,7 @@ static void dev_pull(srtp_t ctx)
         const srtp_dev_stream_t *d = &dt->hs[sid];
         st->rdbx.index = d->index;
         memcpy(st->rdbx.w, dt->hwin + d->win_off, st->rdbx.bits / 8);
-        st->keys->k[0].num_left -= d->uses;
+        st->keys->k[st->use_mki ? dt->mki_j : 0].num_left -= d->uses;
         /* a device batch never used a stream against its direction (the
          * eligibility flags), so no ssrc_collision event is due here */
         if (st->direction == DIR_UNKNOWN && (d->dir & SRTP_DIR_TX))
@@ -3252,7 +3311,7 @@ static void dev_pull(srtp_t ctx)
 /* the device pre-pass; returns 1 when the batch was completed on the GPU,
  * 0 when the host path must run it, -1 on a device error */
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
-                               int async)
+                               int async, const size_t *mki_wide)
 {
     devtab_t *dt = &ctx->dt;
     if (!ctx->n || b->n > 0x7fffffffu) {
@@ -3261,6 +3320,8 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     }
     if (!dt->valid && dev_build(ctx))
         return -1;
+    if (dt->has_mki && dev_mki_select(ctx, b->mki_index, mki_wide, b->n))
+        return 0;
     /* no key can reach its soft limit inside this batch (key.c:74-90) */
     if (dt->num_left_min == UINT64_MAX ||
         dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT) {
@@ -3334,7 +3395,7 @@ static srtp_err_status_t protect_device(srtp_t ctx,
     if (ctx->dt.async_pending && ctx->dt.async_stream != b->stream &&
         async_drain(ctx))
         return srtp_err_status_fail;
-    int fast = protect_device_fast(ctx, b, async);
+    int fast = protect_device_fast(ctx, b, async, NULL);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         return srtp_err_status_fail;
@@ -3393,6 +3454,8 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
         return 0;
     }
     if (!dt->valid && dev_build(ctx))
+        return -1;
+    if (dt->has_mki && dev_mki_rx(ctx))
         return -1;
     if (dt->num_left_min == UINT64_MAX ||
         dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT) {

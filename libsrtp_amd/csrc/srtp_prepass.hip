@@ -61,7 +61,8 @@ constexpr uint32_t NOCHAIN = 0xffffffffu;
 // abort reasons (bits of the abort word; any bit -> host path)
 enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4,
        AB_ORDER = 8, /* order-free form does not apply: sorted path */
-       AB_STATIC = 16 /* unprotect: a packet with a length/capacity error */ };
+       AB_STATIC = 16, /* unprotect: a packet with a length/capacity error */
+       AB_MKI = 32 /* unprotect: a packet whose MKI is not the device key's */ };
 
 struct PpState {
     // stream table
@@ -184,7 +185,27 @@ struct ClassifyArgs {
     unsigned long long *new_index;
     srtp_dev_meta_t *meta;
     uint32_t *olen;
+    // unprotect: the key records (MKI streams compare the packet's MKI with
+    // their device key's)
+    const srtp_dev_key_t *keys;
 };
+
+// an MKI stream's packet (length checks passed) carries its device key's
+// MKI (srtp.c:1961-2016 srtp_get_session_keys_for_packet; any other MKI,
+// including an unknown one, is the host path's: bad_mki or another key)
+__device__ __forceinline__ bool mki_is_device_key(const srtp_dev_key_t *keys,
+                                                  const srtp_dev_stream_t &S,
+                                                  const uint8_t *pkt,
+                                                  uint32_t len)
+{
+    const uint32_t sz = S.mki & 0xffffu, back = S.mki >> 16;
+    const uint8_t *p = pkt + len - back;
+    const uint8_t *m = keys[S.key].mki;
+    uint32_t d = 0;
+    for (uint32_t b = 0; b < sz; b++)
+        d |= p[b] ^ m[b];
+    return d == 0;
+}
 
 // index_guess against a stream's stored index (srtp_host.c estimate /
 // index_guess = rdbx.c:112-145, 280-299); returns delta
@@ -850,7 +871,7 @@ __global__ void k_pu_classify(ClassifyArgs A)
                 atomicOr(A.abort, AB_UNKNOWN_SSRC);   // template clone: host
             } else {
                 const srtp_dev_stream_t &S = A.st[sid];
-                const uint32_t tag = S.trailer;       // no MKI on this path
+                const uint32_t tag = S.trailer;       // tag + MKI
                 if (!(S.flags & SRTP_DS_RX_ELIGIBLE) || (S.dir & SRTP_DIR_TX))
                     atomicOr(A.abort, AB_INELIGIBLE);
                 // srtp_host.c un_static (srtp.c:2905-2990, 2298-2352)
@@ -860,6 +881,9 @@ __global__ void k_pu_classify(ClassifyArgs A)
                     ((S.flags & SRTP_DS_ICM_CONF) &&
                      (len - tag - h.enc_start + 15) / 16 > 0xffffu)) {
                     atomicOr(A.abort, AB_STATIC);
+                } else if (S.mki &&
+                           !mki_is_device_key(A.keys, S, A.in + off, len)) {
+                    atomicOr(A.abort, AB_MKI);
                 } else {
                     key = sid;
                     if (A.est) {   // order-free form
@@ -1641,7 +1665,7 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
     const uint32_t tile = s_tile;
     const srtp_dev_stream_t S = C.st[0];
     const uint64_t stored = S.index;
-    const uint32_t tag = S.trailer;   // no MKI on this path
+    const uint32_t tag = S.trailer;   // tag + MKI
     const uint32_t base = tile * CH_TILE + t * CH_ITEMS;
     uint32_t bad = 0, nm = 0, abort = 0, chain = 0, cand = 0;
     uint64_t off[CH_ITEMS];
@@ -1680,6 +1704,9 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
                 ((S.flags & SRTP_DS_ICM_CONF) &&
                  (L - tag - h.enc_start + 15) / 16 > 0xffffu)) {
                 abort |= AB_STATIC;
+            } else if (S.mki &&
+                       !mki_is_device_key(C.keys, S, C.in + off[k], L)) {
+                abort |= AB_MKI;
             } else {
                 chain |= 1u << k;
                 cand++;
@@ -3003,6 +3030,7 @@ static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
     A.C.new_index = nullptr;
     A.C.meta = P->meta;
     A.C.olen = nullptr;
+    A.C.keys = g->d_keys;
     A.auth = P->auth;
     A.tile = tile;
     A.ctl = ctl;
@@ -3130,6 +3158,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     C.abort = P->abort;
     C.est = unordered ? P->est : nullptr;
     C.new_index = unordered ? (unsigned long long *)P->new_index : nullptr;
+    C.keys = g->d_keys;
     hipLaunchKernelGGL(k_pu_classify, gp, blk, 0, stream, C);
     PPCHK(hipGetLastError());
     const uint32_t *ks, *kp;   // the order the kernels below walk

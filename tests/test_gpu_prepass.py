@@ -560,3 +560,78 @@ def test_fused_window_sizes_jumps_and_state():
             rc, ref = orc.protect(p, len(p) + 16)
             assert st == rc, (k, wins[k % 4], top - q, st, rc)
             assert rc or out == ref
+
+
+def _device_run(sess, pkts, caps, op, mki=None):
+    """one srtp_{un}protect_device call in place -> (status, outputs)"""
+    import torch
+    offs, pos = [], 0
+    for p, c in zip(pkts, caps):
+        offs.append(pos)
+        pos += (max(len(p), c) + 15) & ~15
+    buf = bytearray(pos + 16)
+    for o, p in zip(offs, pkts):
+        buf[o:o + len(p)] = p
+    arena = torch.frombuffer(buf, dtype=torch.uint8).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor([len(p) for p in pkts], dtype=torch.int32).cuda()
+    cap = torch.tensor(caps, dtype=torch.int32).cuda()
+    st = torch.full((len(pkts),), -1, dtype=torch.int32).cuda()
+    fn = sess.protect_device if op == "protect" else sess.unprotect_device
+    kw = {"mki": mki} if mki is not None else {}
+    assert fn(arena, off, ln, arena, off, cap, st, **kw) == 0
+    st, cap = st.cpu().tolist(), cap.cpu().tolist()
+    host = arena.cpu().numpy().tobytes()
+    return st, [host[o:o + c] if s == 0 else None
+                for o, c, s in zip(offs, cap, st)]
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_mki_streams_on_device_prepass(name):
+    """MKI streams (srtp.c:1961-2036) on the device pre-pass: protect
+    batches with one mki_index for the batch run on the device with that
+    master key (a change of key rebuilds the device table); a batch mixing
+    keys takes the host path.  Receive batches run on the device with the
+    key the host path matched last; a batch carrying another key's MKI
+    goes back to the host (AB_MKI), the next one is on the device again.
+    Every status and byte against the oracle, one packet at a time."""
+    _gpu()
+    rng = random.Random(613)
+    ssrcs = [0x22000000 + 3 * k for k in range(24)]
+    pols = [policy(name, ssrc=s, seed=k, mki=4, nkeys=3)
+            for k, s in enumerate(ssrcs)]
+    snd, orc = L.Session(pols), O.Session(pols)
+    rcv, orc_r = L.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
+    plan = [("uniform", 0, 1), ("uniform", 2, 1), ("uniform", 2, 1),
+            ("mixed", None, 0), ("uniform", 1, 1)]
+    d0, h0 = 0, 0
+    for kind, j, dev in plan:
+        pk = _interleaved(rng, ssrcs, seq0, 12, payloads=(0, 7, 160))
+        mki = [j] * len(pk) if kind == "uniform" else \
+            [rng.randrange(3) for _ in pk]
+        caps = [len(p) + 32 for p in pk]
+        st, out = _device_run(snd, pk, caps, "protect", mki)
+        sent = []
+        for i, p in enumerate(pk):
+            rc, ref = orc.protect(p, caps[i], mki[i])
+            assert st[i] == rc, (kind, i, st[i], rc)
+            assert rc or out[i] == ref, (kind, i)
+            sent.append(ref)
+        d, h = snd.prepass_stats()
+        assert (d - d0, h - h0) == ((1, 0) if dev else (0, 1)), (kind, j)
+        d0, h0 = d, h
+        # the receiver: first batch of a new key on the host, then device
+        rd0, rh0 = rcv.prepass_stats()
+        st, out = _device_run(rcv, sent, [len(p) for p in sent], "unprotect")
+        for i, p in enumerate(sent):
+            rc, ref = orc_r.unprotect(p, len(p))
+            assert st[i] == rc, ("rx", kind, i, st[i], rc)
+            assert rc or out[i] == ref, ("rx", kind, i)
+    rd, rh = rcv.prepass_stats()
+    # keys 0, 2, 2, mixed, 1: the batches after a key change and the mixed
+    # one are host batches, the rest device
+    assert rd >= 2 and rh >= 2, (rd, rh)
+    for s in ssrcs[::5]:
+        assert snd.get_roc(s)[1] == orc.get_roc(s)[1]
+        assert rcv.get_roc(s)[1] == orc_r.get_roc(s)[1]

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 timeout -k 10 500 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread \
-    tests/test_gpu_prepass.py > gpurun_out/s7_tests.log 2>&1 || { tail -30 gpurun_out/s7_tests.log; exit 1; }
+    tests/test_gpu_prepass.py tests/test_gpu_parity.py tests/test_gpu_replica.py tests/test_gpu_kdf.py > gpurun_out/s7_tests.log 2>&1 || { tail -30 gpurun_out/s7_tests.log; exit 1; }
 tail -2 gpurun_out/s7_tests.log
 tools/step_variants.sh g711 2 || exit 1
 tools/ktrace.sh g711_s7 --config g711 --steps 10 --warmup 2
@@ -20,6 +20,6 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d gpurun_out/fcal_$c -o p \
       -- tools/fetch_cal > gpurun_out/fcal_$c.log 2>&1 || { tail -5 gpurun_out/fcal_$c.log; exit 1; }
   python3 tools/pmc_reduce.py gpurun_out/fcal_$c
-  cat gpurun_out/fcal_$c/*/pmc_summary.csv gpurun_out/fcal_$c/pmc_summary.csv 2>/dev/null | grep -v "^Kernel_Name" || true
+  grep -rh "k_" gpurun_out/fcal_$c --include=pmc_summary.csv || true
 done
 tail -1 gpurun_out/fcal_FETCH_SIZE.log
