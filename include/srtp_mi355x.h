@@ -413,9 +413,10 @@ srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
 void srtp_mi355x_set_timing(srtp_t ctx, int on);
 double srtp_mi355x_last_kernel_ms(srtp_t ctx);
 /* device-API batches completed by the GPU pre-pass / by the host pre-pass
- * (the latter: streams needing a template clone, MKI, a pending ROC, a
- * receiver-direction stream, non-advancing sequence numbers, or keys near
- * their usage limit -- DESIGN.md "Device pre-pass") */
+ * (the latter: streams needing a template clone, a pending ROC, a stream
+ * used in the other direction, duplicate indices on protect, a protect
+ * batch mixing MKI keys or a receive batch carrying another key's MKI, or
+ * keys near their usage limit -- DESIGN.md "Device pre-passes") */
 void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
                                uint64_t *host_batches);
 /* device pre-pass batches of more than one stream that could not use the

@@ -32,9 +32,15 @@
 // than its window, or an index at or below the stored one) is re-run
 // through the sorted chain path.  Anything
 // outside the condition (unknown SSRC needing a template clone, a stream
-// with MKI / pending ROC / receiver direction, a non-advancing sequence)
-// raises the abort word: nothing is committed, the crypto kernels exit,
-// and the host runs its exact path on the untouched state.  Key-limit
+// with a pending ROC / receiver direction, a protect batch's duplicate
+// index, an MKI other than the device key's on receive) raises the abort
+// word: nothing is committed, the crypto kernels exit, and the host runs
+// its exact path on the untouched state.  MKI streams run with the one
+// master key the host's device table selected (srtp_host.c
+// dev_mki_select).  One-stream receive batches in any arrival order:
+// pp_unprotect_chain1 below.  The order-free protect form of in-place
+// AES-ICM batches classifies inside the crypto kernel (pp_protect_fused,
+// srtp_icm.hip fz_classify).  Key-limit
 // events cannot occur on this path: the host only takes it while every key
 // has more than SOFT_LIMIT uses left after the batch.
 
