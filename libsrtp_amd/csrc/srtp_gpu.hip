@@ -14,11 +14,14 @@ namespace {
 // ---------------------------------------------------------------------------
 // Restore kernel for speculative unprotect: XORs the keystream the
 // speculative pass used back over [enc_start, len) so the ciphertext of a
-// packet that must be re-run is intact again (CTR decryption is an XOR).
-// Rare path: byte-granular, runtime round count.
+// packet that must be re-run (or is rejected) is intact again (CTR
+// decryption is an XOR).  One packet by a whole wave: lane l takes CTR
+// blocks l, l + 64, ...
+// (a 1400-byte packet is 88 blocks: two AES steps per lane instead of 88
+// dependent ones on one lane)
 template <int NR>
-DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
-                  uint8_t *p, const AesLds &T)
+DEV void undo_wave(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
+                   uint8_t *p, const AesLds &T, uint32_t lane)
 {
     GlobalKey rk{ key };
     const uint32_t enc_start = SRTP_META_ENC_START(m.info);
@@ -39,14 +42,14 @@ DEV void undo_one(const srtp_dev_key_t *key, const srtp_dev_meta_t &m,
         c2 = key->salt[2] ^ bswap(m.roc);
         c3base = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
     }
-    for (uint32_t j = 0; 16 * j < P; j++) {
+    for (uint32_t j = lane; 16 * j < P; j += 64) {
         uint32_t x0 = c0, x1 = c1, x2 = c2, x3;
         if (gcm)
             x3 = bswap(j + 2);
         else
             x3 = c3base ^ ((j >> 8) << 16) ^ ((j & 0xffu) << 24);
         aes_block<NR, false>(x0, x1, x2, x3, rk, T);
-        uint32_t ks[4] = { x0, x1, x2, x3 };
+        const uint32_t ks[4] = { x0, x1, x2, x3 };
         for (uint32_t b = 0; b < 16 && 16 * j + b < P; b++)
             p[enc_start + 16 * j + b] ^= (uint8_t)(ks[b >> 2] >> (8 * (b & 3)));
     }
@@ -57,41 +60,64 @@ DEV uint8_t xrtp_unprotect(const srtp_dev_key_t *keys, const srtp_dev_meta_t &m,
                            const uint8_t *src, uint8_t *p, bool undo,
                            const AesLds &T);
 
-__global__ __launch_bounds__(256) void k_undo(uint8_t *arena,
-                                              const uint64_t *off,
-                                              const srtp_dev_meta_t *meta,
-                                              const srtp_dev_key_t *keys,
-                                              uint32_t n)
+// The packets to undo, compacted (wave-aggregated atomic): most batches
+// have few or none
+__global__ __launch_bounds__(256) void k_undo_list(const srtp_dev_meta_t *meta,
+                                                   uint32_t n, uint32_t *list,
+                                                   uint32_t *count)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool todo = i < n && !SRTP_META_STATUS(meta[i].info);
+    const uint64_t bal = __ballot(todo);
+    if (!bal)
+        return;
+    const uint32_t lane = threadIdx.x & 63, lead = __ffsll((long long)bal) - 1;
+    uint32_t base = 0;
+    if (lane == lead)
+        base = atomicAdd(count, (uint32_t)__popcll(bal));
+    base = __shfl(base, lead);
+    if (todo)
+        list[base + __popcll(bal & ((1ull << lane) - 1))] = i;
+}
+
+// ... then one wave per listed packet; the
+// blocks past the list leave before building the tables
+__global__ __launch_bounds__(256) void k_undo_wave(uint8_t *arena,
+                                                   const uint64_t *off,
+                                                   const srtp_dev_meta_t *meta,
+                                                   const srtp_dev_key_t *keys,
+                                                   const uint32_t *list,
+                                                   const uint32_t *count)
 {
     __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    srtp_dev_meta_t m = {};
-    if (i < n)
-        m = meta[i];
-    const bool todo = i < n && !SRTP_META_STATUS(m.info);
-    // most blocks have nothing to undo (every packet authenticated): they
-    // leave before building the tables
-    if (!__syncthreads_or(todo))
+    const uint32_t cnt = *count;
+    const uint32_t wpb = blockDim.x >> 6;
+    if (blockIdx.x * wpb >= cnt)
         return;
     load_aes_tables<false>(s_tab);
     __syncthreads();
-    if (!todo)
-        return;
-    const srtp_dev_key_t *key = keys + m.key;
     const AesLds T = make_aes_lds(s_tab);
-    uint8_t *p = arena + off[i];
-    if (SRTP_META_VARIANT(m.info) == SRTP_VARIANT_X) {
-        xrtp_unprotect(keys, m, p, p, true, T);
-        return;
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t w = blockIdx.x * wpb + (threadIdx.x >> 6); w < cnt;
+         w += gridDim.x * wpb) {
+        const uint32_t i = list[w];
+        const srtp_dev_meta_t m = meta[i];
+        const srtp_dev_key_t *key = keys + m.key;
+        uint8_t *p = arena + off[i];
+        if (SRTP_META_VARIANT(m.info) == SRTP_VARIANT_X) {
+            if (lane == 0)
+                xrtp_unprotect(keys, m, p, p, true, T);
+            continue;
+        }
+        if (!key->conf || key->family == SRTP_DEV_NULL)
+            continue;
+        if (key->rounds == 10)
+            undo_wave<10>(key, m, p, T, lane);
+        else if (key->rounds == 12)
+            undo_wave<12>(key, m, p, T, lane);
+        else
+            undo_wave<14>(key, m, p, T, lane);
     }
-    if (!key->conf || key->family == SRTP_DEV_NULL)
-        return;
-    if (key->rounds == 10)
-        undo_one<10>(key, m, p, T);
-    else if (key->rounds == 12)
-        undo_one<12>(key, m, p, T);
-    else
-        undo_one<14>(key, m, p, T);
 }
 
 // ---------------------------------------------------------------------------
@@ -852,7 +878,7 @@ DEV uint8_t xrtp_protect(const srtp_dev_key_t *keys, const srtp_dev_meta_t &m,
 // unprotect: verify on the input, then write the output.  `undo` re-applies
 // a run's transform to its output (XOR is its own inverse; the profile goes
 // back to the cryptex one) so a speculative run at a wrong index can be
-// taken back (k_undo).
+// taken back (k_undo_wave).
 DEV uint8_t xrtp_unprotect(const srtp_dev_key_t *keys, const srtp_dev_meta_t &m,
                            const uint8_t *src, uint8_t *p, bool undo,
                            const AesLds &T)
@@ -1325,6 +1351,7 @@ void srtp_gpu_close(srtp_gpu_t *g)
     (void)hipFree(g->d_keys);
     (void)hipFree(g->d_ghash);
     (void)hipFree(g->d_raw);
+    (void)hipFree(g->d_undo);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);
     (void)hipStreamDestroy(g->stream);
@@ -1482,8 +1509,22 @@ int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,
     if (!n)
         return 0;
     hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
-    hipLaunchKernelGGL(k_undo, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       st, arena, off, meta, g->d_keys, (uint32_t)n);
+    if (n > g->undo_cap) {
+        // in-flight work may still read the old list: hipFree waits for it
+        (void)hipFree(g->d_undo);
+        g->d_undo = nullptr;
+        g->undo_cap = 0;
+        HIPCHK(hipMalloc((void **)&g->d_undo, (n + 1) * 4));
+        g->undo_cap = n;
+    }
+    uint32_t *count = g->d_undo + n;
+    HIPCHK(hipMemsetAsync(count, 0, 4, st));
+    hipLaunchKernelGGL(k_undo_list, dim3((unsigned)((n + 255) / 256)),
+                       dim3(256), 0, st, meta, (uint32_t)n, g->d_undo, count);
+    size_t blocks = 2 * (size_t)g->ncu, need = (n + 3) / 4;
+    blocks = blocks < need ? blocks : need;
+    hipLaunchKernelGGL(k_undo_wave, dim3((unsigned)blocks), dim3(256), 0, st,
+                       arena, off, meta, g->d_keys, g->d_undo, count);
     HIPCHK(hipGetLastError());
     return 0;
 }

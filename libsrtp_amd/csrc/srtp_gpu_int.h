@@ -30,6 +30,9 @@ struct srtp_gpu {
     // (srtp_plugin.c -> srtp_gpu_raw): scratch grown on demand
     uint8_t *d_raw;
     size_t raw_cap;
+    // srtp_gpu_undo: the compacted list of packets to undo (+ its count)
+    uint32_t *d_undo;
+    size_t undo_cap;
 };
 
 // The order-free protect pre-pass's classification done by k_icm_hmac
@@ -42,13 +45,17 @@ struct srtp_gpu {
 // one packet's classification, one 16-byte store (dense: a wave writes
 // whole cache lines)
 struct alignas(16) FzRec {
-    uint64_t est;          // the index guessed from the stored one
+    uint64_t est;          // the index guessed from the stored one (48 bits)
+                           // | status code << 48
     uint32_t skey;         // stream id, ~0 when the packet is not a chain one
-    uint32_t pstat;        // status code
+    uint32_t cap;          // the caller's capacity (out_len before the kernel
+                           // wrote the protected length), for a decline
 };
 
 struct IcmFused {
-    const uint32_t *in_len, *cap;
+    const uint32_t *in_len;
+    uint32_t *cap;         // capacities in, protected lengths out
+    int32_t *status;
     const srtp_dev_stream_t *st;
     const uint32_t *hkey, *hval;
     uint32_t hmask;

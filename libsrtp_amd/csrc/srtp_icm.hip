@@ -742,8 +742,16 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
         }
     }
     // the descriptor is not stored: a declined batch rebuilds it for the
-    // undo (srtp_prepass.hip k_fz_meta), commit derives the lengths
-    *(u32x4 *)&F.rec[i] = u32x4{ (uint32_t)e, (uint32_t)(e >> 32), key, code };
+    // undo (srtp_prepass.hip k_fz_meta).  Status and protected length are
+    // written now (the commit of an accepted batch); a declined batch gets
+    // its capacities back from the record and its statuses from the path
+    // that then runs it
+    const uint32_t cap = F.cap[i];
+    *(u32x4 *)&F.rec[i] =
+        u32x4{ (uint32_t)e, (uint32_t)(e >> 32) | (code << 16), key, cap };
+    F.status[i] = (int32_t)code;
+    if (code == 0 && key != FZ_NOCHAIN)
+        F.cap[i] = len + z.trailer;
     if (ab)
         atomicOr(F.abort, ab);
     return m;

@@ -680,7 +680,7 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
 
 // An in-place batch classified inside the crypto kernel that the pre-pass
 // then declined: the bytes past every encrypted packet that its tag
-// overwrote come back (its payload is restored by k_undo)
+// overwrote come back (its payload is restored by k_undo_wave)
 __global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
                                   const uint32_t *in_len,
                                   const srtp_dev_stream_t *st,
@@ -766,49 +766,38 @@ __global__ void k_fz_stream(const srtp_dev_stream_t *st, uint32_t ns,
         atomicOr(abort, AB_SEQUENCE);   // two packets with one index: host
 }
 
-// ... then, unless the batch was declined, every packet's status and
-// protected length (from the stream's trailer) and every touched stream's
-// state, in one launch over max(n, ns) threads
-__global__ void k_fz_commit(const FzRec *rec, const uint32_t *in_len,
-                            srtp_dev_stream_t *st, uint32_t n, uint32_t ns,
+// ... then, unless the batch was declined, every touched stream's state
+// (the packets' statuses and lengths came from the crypto kernel)
+__global__ void k_fz_commit(srtp_dev_stream_t *st, uint32_t ns,
                             const unsigned long long *cnt,
                             const unsigned long long *new_index,
                             const uint32_t *wnew, uint32_t *win,
-                            const uint32_t *abort, int32_t *status,
-                            uint32_t *out_len, uint32_t *pub)
+                            const uint32_t *abort, uint32_t *pub)
 {
     publish_abort(pub, abort);
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (*abort)
+    if (*abort || i >= ns)
         return;
-    if (i < n) {
-        const uint4 r = *(const uint4 *)&rec[i];
-        status[i] = (int32_t)r.w;
-        if (r.w == 0)
-            out_len[i] = in_len[i] + st[r.z].trailer;
-    }
-    if (i < ns) {
-        const uint32_t c = (uint32_t)cnt[i];
-        if (!c)
-            return;
-        st[i].uses += c;
-        st[i].dir |= SRTP_DIR_TX;
-        const uint64_t ni = new_index[i];
-        if (ni == 0)
-            return;
-        st[i].index = ni;
-        const uint32_t off = st[i].win_off, words = st[i].win_bits >> 5;
-        for (uint32_t w = 0; w < words; w++)
-            win[off + w] = wnew[off + w];
-    }
+    const uint32_t c = (uint32_t)cnt[i];
+    if (!c)
+        return;
+    st[i].uses += c;
+    st[i].dir |= SRTP_DIR_TX;
+    const uint64_t ni = new_index[i];
+    if (ni == 0)
+        return;
+    st[i].index = ni;
+    const uint32_t off = st[i].win_off, words = st[i].win_bits >> 5;
+    for (uint32_t w = 0; w < words; w++)
+        win[off + w] = wnew[off + w];
 }
 
 // ... and a declined batch's descriptors, as k_icm_hmac had them, for the
-// undo (k_undo re-applies the keystream)
+// undo (k_undo_wave re-applies the keystream); the capacities come back
 __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
                           const uint32_t *in_len, const FzRec *rec,
                           const srtp_dev_stream_t *st, uint32_t n,
-                          srtp_dev_meta_t *meta)
+                          srtp_dev_meta_t *meta, uint32_t *cap)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
@@ -818,14 +807,16 @@ __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
     m.roc = 0;
     m.len = 0;
     m.info = 0xff0000u;
-    const uint32_t s = rec[i].skey;
-    if (s != NOCHAIN && rec[i].pstat == 0) {
+    const uint4 r = *(const uint4 *)&rec[i];
+    const uint32_t s = r.z, code = r.y >> 16;
+    if (s != NOCHAIN && code == 0) {
         const uint64_t off = in_off[i];
         const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
         m.key = st[s].key;
-        m.roc = (uint32_t)(rec[i].est >> 16);
+        m.roc = (r.x >> 16) | ((r.y & 0xffffu) << 16);
         m.info = h.enc_start | (st[s].variant << 24);
         m.len = in_len[i];
+        cap[i] = r.w;
     }
     meta[i] = m;
 }
@@ -2714,7 +2705,7 @@ static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
 // packet's first line is read once, by the kernel that encrypts it.  The
 // conditions of the order-free form (k_pp_usetbits) are checked after the
 // crypto; a batch outside them (or with an unknown / ineligible stream) is
-// restored -- k_undo re-applies the keystream, k_pp_tail_restore writes back
+// restored -- k_undo_wave re-applies the keystream, k_pp_tail_restore writes back
 // the bytes the tags overwrote -- and, for AB_ORDER, *sorted set: the caller
 // runs the sorted chain form, else the host decides (*fallback).  Only in
 // place, one AES-ICM kernel variant, trailers <= 16 bytes (fused_ok).
@@ -2731,6 +2722,7 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     IcmFused F;
     F.in_len = b->in_len;
     F.cap = b->out_len;
+    F.status = b->status;
     F.st = P->st;
     F.hkey = P->hkey;
     F.hval = P->hval;
@@ -2764,11 +2756,8 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
         return fail();
     hipLaunchKernelGGL(k_fz_stream, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
                        hi, P->fz_emin, P->fz_bmap, P->win, P->wnew, P->abort);
-    const uint32_t nc = N > ns ? N : ns;
-    hipLaunchKernelGGL(k_fz_commit, dim3((nc + 255) / 256), blk, 0, stream,
-                       P->fzrec, b->in_len, P->st, N, ns, P->fz_cnt, hi,
-                       P->wnew, P->win, P->abort, b->status, b->out_len,
-                       P->h_abort_dev);
+    hipLaunchKernelGGL(k_fz_commit, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
+                       hi, P->wnew, P->win, P->abort, P->h_abort_dev);
     if (hipGetLastError() != hipSuccess || pp_step(stream, "fused commit"))
         return fail();
     PPCHK(hipStreamSynchronize(stream));
@@ -2780,7 +2769,7 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
         return 0;
     // declined: the input comes back exactly
     hipLaunchKernelGGL(k_fz_meta, gp, blk, 0, stream, b->in, b->in_off,
-                       b->in_len, P->fzrec, P->st, N, P->meta);
+                       b->in_len, P->fzrec, P->st, N, P->meta, b->out_len);
     PPCHK(hipGetLastError());
     if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
         return -1;

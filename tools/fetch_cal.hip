@@ -8,6 +8,8 @@
 //   k_rd_linear the wave sweeps its packets' span, 1 KiB per instruction
 //   k_cp_quad   quad loads + 64-B-aligned quad stores (the headline
 //               kernel's steady state) into a second arena
+//   k_cp_quad_ip the same in place, k_cp_lane_ip per-lane 16-B pieces in
+//               place (the per-lane-key kernel's shape)
 // Each kernel runs once after one untimed warmup launch of all; the known
 // bytes per launch are printed.  Run the counters in separate passes:
 //   rocprofv3 --pmc FETCH_SIZE -- tools/fetch_cal
@@ -54,7 +56,8 @@ __global__ __launch_bounds__(512) void k_rd_lane(const uint8_t *in, uint8_t *out
 __global__ __launch_bounds__(512) void k_rd_quad(const uint8_t *in, uint8_t *out, uint32_t n) { rd<1>(in, out, n); }
 __global__ __launch_bounds__(512) void k_rd_linear(const uint8_t *in, uint8_t *out, uint32_t n) { rd<3>(in, out, n); }
 
-__global__ __launch_bounds__(512) void k_cp_quad(const uint8_t *in, uint8_t *out, uint32_t n)
+template <int MODE>
+__device__ void cp(const uint8_t *in, uint8_t *out, uint32_t n)
 {
     const uint32_t l = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * (blockDim.x / 64);
@@ -63,10 +66,16 @@ __global__ __launch_bounds__(512) void k_cp_quad(const uint8_t *in, uint8_t *out
         for (uint32_t s = 0; s + 1 < NCH; s++)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
-                const uint64_t o = piece<2>(64 * w, l, s, k);
+                const uint64_t o = piece<MODE>(64 * w, l, s, k);
                 *(u32x4 *)(out + o) = *(const u32x4 *)(in + o) ^ 0x5a5a5a5au;
             }
 }
+
+// copies of 21 chunks per packet: aligned quads out of place and in place
+// (the SRTP kernels protect in place), per-lane 16-B pieces in place
+__global__ __launch_bounds__(512) void k_cp_quad(const uint8_t *in, uint8_t *out, uint32_t n) { cp<2>(in, out, n); }
+__global__ __launch_bounds__(512) void k_cp_quad_ip(const uint8_t *in, uint8_t *out, uint32_t n) { cp<2>(in, out, n); }
+__global__ __launch_bounds__(512) void k_cp_lane_ip(const uint8_t *in, uint8_t *out, uint32_t n) { cp<0>(in, out, n); }
 
 int main()
 {
@@ -83,10 +92,12 @@ int main()
         hipLaunchKernelGGL(k_rd_quad, g, b, 0, 0, in, out, n);
         hipLaunchKernelGGL(k_rd_linear, g, b, 0, 0, in, out, n);
         hipLaunchKernelGGL(k_cp_quad, g, b, 0, 0, in, out, n);
+        hipLaunchKernelGGL(k_cp_quad_ip, g, b, 0, 0, in, in, n);
+        hipLaunchKernelGGL(k_cp_lane_ip, g, b, 0, 0, in, in, n);
         if (hipDeviceSynchronize() != hipSuccess)
             return 2;
     }
-    printf("{\"read_bytes_per_launch\": %llu, \"cp_quad_bytes_each_way\": %llu}\n",
+    printf("{\"read_bytes_per_launch\": %llu, \"cp_bytes_each_way\": %llu}\n",
            (unsigned long long)n * NCH * 64,
            (unsigned long long)n * (NCH - 1) * 64);
     return 0;
