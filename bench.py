@@ -160,15 +160,47 @@ DIST_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
              "SRTP_FORCE_DIST")
 
 
+# FETCH_SIZE / WRITE_SIZE of a byte-exact copy in the kernel's own access
+# shape, per byte moved (tools/fetch_cal.hip on MI355X, profiles/r04/fcal,
+# profiles/r04_fetch_calibration.md): read-only streams count 0.50-0.70 of
+# their bytes (the guide's 1/2 for 128-B requests), copies 0.83-1.95 of the
+# reads and 1.03-2.82 of the writes depending on the shape.
+SHAPE_CAL = {
+    # in-place lane quads, 64-B-aligned stores (k_icm_hmac, uniform key)
+    "lane_quad_inplace": (0.833, 1.134),
+    # in-place, every lane its own packet, 16-B pieces (k_gcm; k_icm_hmac
+    # with per-lane keys)
+    "lane_inplace": (1.954, 2.822),
+}
+KERNEL_SHAPE = {"icm128": "lane_quad_inplace", "gcm256": "lane_inplace",
+                "g711": "lane_inplace"}
+
+
+def traffic_shape(a, n, rtp_len, tag, pmc):
+    """the counters against what a byte-exact copy of the same shape and
+    size shows: `ratio` near 1 means the kernel moves no more than its
+    access shape forces; raw FETCH_SIZE is not corrected by one global
+    factor because the calibration shows none fits every shape"""
+    if "FETCH_SIZE" not in pmc or "WRITE_SIZE" not in pmc:
+        return None
+    shape = KERNEL_SHAPE[a.config]
+    fr, fw = SHAPE_CAL[shape]
+    rd = n * (rtp_len + (tag if a.op == "unprotect" else 0))
+    wr = n * (rtp_len + (0 if a.op == "unprotect" else tag))
+    base = fr * rd + fw * wr
+    f, w = pmc["FETCH_SIZE"] * 1024.0, pmc["WRITE_SIZE"] * 1024.0
+    return {"shape": shape, "fetch": f, "write": w,
+            "fetch_over_shape": f / (fr * rd), "write_over_shape": w / (fw * wr),
+            "shape_baseline": base, "ratio": (f + w) / base}
+
+
 def measure_pmc(a, kname, device=0):
     """per-launch PMC counters of the dominant kernel over a short run of
     this same workload, one rocprofv3 --pmc pass per entry of PMC_PASSES,
     each a child process started before this process touches the GPU.
-    FETCH_SIZE is TCC_EA0_RDREQ x 64 B; the kernel's reads are 64-B pieces
-    (lane quads) and 16-B lane reads, and the measured value equals the
-    algorithmic read bytes within 3 %, so it is taken as is (the x2
-    correction of the guide is for 128-B requests of fully coalesced 1 KiB
-    wave reads)."""
+    FETCH_SIZE is TCC_EA0_RDREQ x 64 B.  `traffic` is FETCH_SIZE +
+    WRITE_SIZE as counted; traffic_shape() sets it against the calibrated
+    counts of a byte-exact copy in the kernel's access shape (SHAPE_CAL)."""
     import glob
     import shutil
     import subprocess
@@ -840,6 +872,7 @@ def run_gpu(a, world, rank, local, json_out):
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
+                "traffic_shape": traffic_shape(a, n, rtp_len, tag, pmc),
                 "kernel": kname, "kernel_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "issue": issue_roofline(pmc, kernel_ms)}

@@ -1839,6 +1839,7 @@ struct PuVerdictArgs {
     uint32_t *pstat;      // out: the verdict code of every candidate
     uint64_t *top;        // out: T_k inclusive (highest authenticated)
     uint32_t gen;         // k_pu_first's generation of this batch
+    uint64_t first_cap;   // entries of `first` (k_pu_first's span check)
 };
 
 __global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
@@ -1856,8 +1857,12 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
     const srtp_dev_stream_t S = A.st[0];
     const uint64_t stored = S.index;
     const uint32_t bits = S.win_bits;
-    const bool nonmono = A.ctl->nonmono != 0;
+    // the first-authenticated array exists only when k_pu_first ran: some
+    // advance <= 0 and the candidates' index span fits it (else k_pu_first
+    // raised AB_ORDER and nothing is read from it here)
     const uint64_t lo = A.ctl->umin;
+    const bool nonmono = A.ctl->nonmono != 0 &&
+                         A.ctl->umax - lo + 1 <= A.first_cap;
     const uint32_t gen = A.gen;
     const uint32_t base = tile * CH_TILE + t * CH_ITEMS;
     uint64_t u[CH_ITEMS];
@@ -3064,6 +3069,7 @@ static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
     V.pstat = P->pstat;
     V.top = P->top;
     V.gen = P->pu_gen;
+    V.first_cap = P->pu_first_cap;
     hipLaunchKernelGGL(k_pu_verdict1, dim3(nt), dim3(CH_THREADS), 0, stream, V);
     PU1CHK(hipGetLastError(), "k_pu_verdict1");
     if (pp_step(stream, "pu_verdict1"))
