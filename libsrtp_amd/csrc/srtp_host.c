@@ -4400,6 +4400,24 @@ static int rep_kref_cmp(const void *a, const void *b)
     return x < y ? -1 : x > y;
 }
 
+/* by key set, then by the first stream using it */
+static int rep_kref_cmp2(const void *a, const void *b)
+{
+    const int c = rep_kref_cmp(a, b);
+    if (c)
+        return c;
+    const uint32_t x = ((const rep_kref_t *)a)->idx,
+                   y = ((const rep_kref_t *)b)->idx;
+    return x < y ? -1 : x > y;
+}
+
+static int rep_kref_cmp_idx(const void *a, const void *b)
+{
+    const uint32_t x = ((const rep_kref_t *)a)->idx,
+                   y = ((const rep_kref_t *)b)->idx;
+    return x < y ? -1 : x > y;
+}
+
 /* the streams in blob order: the list (insertion order), then the template */
 static srtp_stream_ctx_t *rep_stream_at(srtp_t ctx, size_t i)
 {
@@ -4416,22 +4434,36 @@ srtp_err_status_t srtp_mi355x_session_export(srtp_t ctx, void *buf, size_t cap,
     if (kq_flush(ctx))
         return srtp_err_status_fail;
     const size_t ns = ctx->n + (ctx->templ ? 1 : 0);
-    /* key sets, each once (template clones share theirs) */
+    /* key sets, each once (template clones share theirs), in the order of
+     * the first stream that uses each: the blob does not depend on where
+     * the heap put them, so a replica exports the same bytes */
     rep_kref_t *ref = (rep_kref_t *)malloc((ns + 1) * sizeof *ref);
-    if (!ref)
+    rep_kref_t *ord = (rep_kref_t *)malloc((ns + 1) * sizeof *ord);
+    if (!ref || !ord) {
+        free(ref);
+        free(ord);
         return srtp_err_status_alloc_fail;
-    for (size_t i = 0; i < ns; i++)
+    }
+    for (size_t i = 0; i < ns; i++) {
         ref[i].ks = rep_stream_at(ctx, i)->keys;
-    qsort(ref, ns, sizeof *ref, rep_kref_cmp);
+        ref[i].idx = (uint32_t)i;
+    }
+    qsort(ref, ns, sizeof *ref, rep_kref_cmp2);
     size_t nk = 0;
     for (size_t i = 0; i < ns; i++)
         if (!nk || ref[nk - 1].ks != ref[i].ks)
-            ref[nk++].ks = ref[i].ks;
+            ref[nk++] = ref[i];
+    memcpy(ord, ref, nk * sizeof *ord);
+    qsort(ord, nk, sizeof *ord, rep_kref_cmp_idx);
+    for (size_t k = 0; k < nk; k++) {
+        rep_kref_t *e = (rep_kref_t *)bsearch(&ord[k], ref, nk, sizeof *ref,
+                                              rep_kref_cmp);
+        e->idx = (uint32_t)k;
+    }
     size_t total = sizeof(rep_hdr_t), nkeys = 0;
     srtp_err_status_t rc = srtp_err_status_ok;
     for (size_t k = 0; k < nk; k++) {
-        ref[k].idx = (uint32_t)k;
-        const keyset_t *ks = ref[k].ks;
+        const keyset_t *ks = ord[k].ks;
         for (size_t j = 0; j < ks->n; j++)
             if (ks->k[j].variant == SRTP_VARIANT_V)
                 rc = srtp_err_status_bad_param; /* keys in host vtables */
@@ -4445,6 +4477,7 @@ srtp_err_status_t srtp_mi355x_session_export(srtp_t ctx, void *buf, size_t cap,
     *len = total;
     if (rc || !buf || cap < total) {
         free(ref);
+        free(ord);
         return rc ? rc : (buf ? srtp_err_status_bad_param : srtp_err_status_ok);
     }
     uint8_t *p = (uint8_t *)buf;
@@ -4459,7 +4492,7 @@ srtp_err_status_t srtp_mi355x_session_export(srtp_t ctx, void *buf, size_t cap,
     memcpy(p, &h, sizeof h);
     p += sizeof h;
     for (size_t k = 0; k < nk; k++) {
-        const keyset_t *ks = ref[k].ks;
+        const keyset_t *ks = ord[k].ks;
         uint32_t w[2] = { (uint32_t)ks->n, (uint32_t)ks->cryptex };
         memcpy(p, w, sizeof w);
         p += sizeof w;
@@ -4511,6 +4544,7 @@ srtp_err_status_t srtp_mi355x_session_export(srtp_t ctx, void *buf, size_t cap,
         p += s->rdbx.bits / 8;
     }
     free(ref);
+    free(ord);
     if (srtp_gpu_get_keys(ctx->gpu, nslots, (srtp_dev_key_t *)p)) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         return srtp_err_status_fail;
