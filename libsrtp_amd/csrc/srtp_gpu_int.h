@@ -69,6 +69,12 @@ struct IcmFused {
     unsigned long long *new_index, *emin;
     uint32_t *bmap;
     uint32_t *abort;
+    // unprotect (pp_unprotect_fused): highest candidate index per stream,
+    // the authenticated indices' bitmaps (same layout as bmap), the count of
+    // candidates that failed their tag check
+    unsigned long long *hicand;
+    uint32_t *bmap2;
+    uint32_t *nfail;
 };
 
 // AES-ICM (+ HMAC-SHA1) kernel arguments

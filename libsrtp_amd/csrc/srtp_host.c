@@ -3475,6 +3475,13 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     pb.stream = b->stream;
     pb.uniform_key = dt->rx_uniform;
     pb.mask = dt->rx_mask;
+    /* the order-free receive form may classify inside the AES-ICM kernel:
+     * in place (a declined batch is restored), per-lane keys, one AES-ICM
+     * kernel variant */
+    pb.fused_ok = b->in == b->out && b->in_off == b->out_off &&
+                  dt->rx_uniform == 0xffffffffu && dt->rx_mask &&
+                  (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
+                  (dt->rx_mask & 0xfc00u) == dt->rx_mask;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_unprotect(ctx->gpu, &pb, &fallback))

@@ -560,7 +560,9 @@ DEV void icm_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
 // lanes of one stream merged by ballots before their atomics.  In-place
 // packets save the bytes their tag will overwrite.
 constexpr uint32_t FZ_NOCHAIN = 0xffffffffu;
-constexpr uint32_t FZ_AB_UNKNOWN = 1, FZ_AB_INELIGIBLE = 2, FZ_AB_ORDER = 8;
+// srtp_prepass.hip AB_* bits
+constexpr uint32_t FZ_AB_UNKNOWN = 1, FZ_AB_INELIGIBLE = 2, FZ_AB_ORDER = 8,
+                   FZ_AB_STATIC = 16, FZ_AB_MKI = 32;
 
 // What a lane keeps between its packets: the last stream it looked up
 // (a lane's packets of a batch are often one stream's: the persistent grid's
@@ -571,29 +573,72 @@ constexpr uint32_t FZ_AB_UNKNOWN = 1, FZ_AB_INELIGIBLE = 2, FZ_AB_ORDER = 8;
 // vmcnt for ~3000 cycles under load, MI355X_MICROARCH.md); the one
 // per-packet atomic left, the bitmap bit, returns nothing and is not waited
 // on.
+// Unprotect (the receive side's order-free form, pp_unprotect_fused): the
+// run counts authenticated packets (low 32 bits) and candidates (high), the
+// highest authenticated index (run_max), the lowest and highest candidate
+// index (run_min, run_cmax); candidates set a bit in `bmap`, authenticated
+// packets one in `bmap2`.
 struct FzLane {
     uint32_t ssrc, sid;            // cached lookup (sid ~0: none)
     uint32_t key, variant, flags, trailer, dir;
     uint32_t boff, bmask;          // bitmap word offset, M - 1
+    uint32_t mki;                  // unprotect: srtp_dev_stream_t.mki
     uint64_t index;
     uint32_t run_sid;              // current run (run_sid ~0: none)
-    uint64_t run_cnt;              // packets | chain packets << 32
+    uint64_t run_cnt;              // protect: packets | chain packets << 32
     uint64_t run_max, run_min;
+    uint64_t run_cmax;             // unprotect only
 };
 
+template <bool PROTECT>
 DEV void fz_flush(const IcmFused &F, FzLane &z)
 {
     if (z.run_sid != FZ_NOCHAIN) {
         atomicAdd(&F.cnt[z.run_sid], (unsigned long long)z.run_cnt);
-        if (z.run_cnt >> 32) {
-            atomicMax(&F.new_index[z.run_sid], (unsigned long long)z.run_max);
-            atomicMin(&F.emin[z.run_sid], (unsigned long long)z.run_min);
+        if (PROTECT) {
+            if (z.run_cnt >> 32) {
+                atomicMax(&F.new_index[z.run_sid],
+                          (unsigned long long)z.run_max);
+                atomicMin(&F.emin[z.run_sid], (unsigned long long)z.run_min);
+            }
+        } else {
+            if (z.run_cnt >> 32) {
+                atomicMax(&F.hicand[z.run_sid], (unsigned long long)z.run_cmax);
+                atomicMin(&F.emin[z.run_sid], (unsigned long long)z.run_min);
+            }
+            if ((uint32_t)z.run_cnt)
+                atomicMax(&F.new_index[z.run_sid],
+                          (unsigned long long)z.run_max);
         }
     }
     z.run_sid = FZ_NOCHAIN;
     z.run_cnt = 0;
     z.run_max = 0;
     z.run_min = ~0ull;
+    z.run_cmax = 0;
+}
+
+// unprotect: candidate e of stream sid
+DEV void fzu_cand(const IcmFused &F, FzLane &z, uint32_t sid, uint64_t e)
+{
+    if (sid != z.run_sid) {
+        fz_flush<false>(F, z);
+        z.run_sid = sid;
+    }
+    z.run_cnt += 1ull << 32;
+    z.run_cmax = e > z.run_cmax ? e : z.run_cmax;
+    z.run_min = e < z.run_min ? e : z.run_min;
+    const uint32_t r = (uint32_t)e & z.bmask;
+    atomicOr(&F.bmap[z.boff + (r >> 5)], 1u << (r & 31));
+}
+
+// ... which authenticated (same run: right after its fzu_cand)
+DEV void fzu_auth(const IcmFused &F, FzLane &z, uint64_t e)
+{
+    z.run_cnt += 1;
+    z.run_max = e > z.run_max ? e : z.run_max;
+    const uint32_t r = (uint32_t)e & z.bmask;
+    atomicOr(&F.bmap2[z.boff + (r >> 5)], 1u << (r & 31));
 }
 
 // a packet of stream sid; chain packets (index e) also set their bitmap bit
@@ -601,7 +646,7 @@ DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, bool chain,
                   uint64_t e)
 {
     if (sid != z.run_sid) {
-        fz_flush(F, z);
+        fz_flush<true>(F, z);
         z.run_sid = sid;
     }
     z.run_cnt += chain ? 1ull | (1ull << 32) : 1ull;
@@ -645,6 +690,28 @@ DEV void fz_tail_save(const uint8_t *t, uint32_t tn, u32x4 &w)
     }
 }
 
+// the lane's stream for SSRC ssrc: its cached one, else a map lookup and
+// the stream record's fields
+DEV void fz_lookup(const IcmFused &F, FzLane &z, uint32_t ssrc)
+{
+    if (ssrc == z.ssrc && z.sid != FZ_NOCHAIN)
+        return;
+    z.ssrc = ssrc;
+    z.sid = srtp_map_lookup(F.hkey, F.hval, F.hmask, ssrc);
+    if (z.sid == FZ_NOCHAIN)
+        return;
+    const srtp_dev_stream_t S = F.st[z.sid];
+    z.key = S.key;
+    z.variant = S.variant;
+    z.flags = S.flags;
+    z.trailer = S.trailer;
+    z.dir = S.dir;
+    z.index = S.index;
+    z.boff = 2 * S.win_off;
+    z.mki = S.mki;
+    z.bmask = (S.win_bits > 32 ? 2u << (31 - __clz(S.win_bits - 1)) : 32u) - 1;
+}
+
 DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
 {
     const IcmFused &F = A.fz;
@@ -661,22 +728,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
     if (h.enc_start >> 24) {
         code = h.enc_start >> 24;   // header does not parse: no stream touched
     } else {
-        if (h.ssrc != z.ssrc || z.sid == FZ_NOCHAIN) {
-            z.ssrc = h.ssrc;
-            z.sid = srtp_map_lookup(F.hkey, F.hval, F.hmask, h.ssrc);
-            if (z.sid != FZ_NOCHAIN) {
-                const srtp_dev_stream_t S = F.st[z.sid];
-                z.key = S.key;
-                z.variant = S.variant;
-                z.flags = S.flags;
-                z.trailer = S.trailer;
-                z.dir = S.dir;
-                z.index = S.index;
-                z.boff = 2 * S.win_off;
-                z.bmask = (S.win_bits > 32 ? 2u << (31 - __clz(S.win_bits - 1))
-                                           : 32u) - 1;
-            }
-        }
+        fz_lookup(F, z, h.ssrc);
         const uint32_t sid = z.sid;
         if (sid == FZ_NOCHAIN) {
             ab |= FZ_AB_UNKNOWN;    // template clone: host
@@ -757,6 +809,122 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
     return m;
 }
 
+// The receive side's order-free classification inside the crypto kernel
+// (pp_unprotect_fused; srtp_prepass.hip k_pu_classify restated): header
+// parse, stream lookup, receive eligibility, the length / capacity checks of
+// srtp_host.c un_static (srtp.c:2905-2990; a failing packet sends the batch
+// to the host: its status would depend on the replay check), the MKI of the
+// device key, and the index guessed from the stored index (rdbx.c:112-145).
+// A candidate is decrypted and verified by icm_packet; fzu_verdict then
+// writes its status and length.  `e` / `sid` out: the candidate's index and
+// stream (sid ~0: not a candidate).
+DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
+                                 uint64_t &e, uint32_t &sid)
+{
+    const IcmFused &F = A.fz;
+    const uint64_t off = A.in_off[i];
+    const uint32_t len = F.in_len[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
+    uint32_t code = 0, ab = 0;
+    e = 0;
+    sid = FZ_NOCHAIN;
+    srtp_dev_meta_t m;
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;   // no crypto
+    if (h.enc_start >> 24) {
+        code = h.enc_start >> 24;   // header does not parse: no stream touched
+    } else {
+        fz_lookup(F, z, h.ssrc);
+        if (z.sid == FZ_NOCHAIN) {
+            ab |= FZ_AB_UNKNOWN;    // template clone: host
+        } else {
+            if (!(z.flags & SRTP_DS_RX_ELIGIBLE) || (z.dir & SRTP_DIR_TX))
+                ab |= FZ_AB_INELIGIBLE;
+            const uint32_t tag = z.trailer;   // tag + MKI
+            const uint32_t es = h.enc_start;
+            if (len < tag || es > len - tag ||
+                ((z.flags & SRTP_DS_AEAD) && len - es < tag) ||
+                F.cap[i] < len - tag ||
+                ((z.flags & SRTP_DS_ICM_CONF) &&
+                 (len - tag - es + 15) / 16 > 0xffffu)) {
+                ab |= FZ_AB_STATIC;
+            } else {
+                if (z.mki) {
+                    // srtp_prepass.hip mki_is_device_key
+                    const uint32_t sz = z.mki & 0xffffu;
+                    const uint8_t *p = A.in + off + len - (z.mki >> 16);
+                    const uint8_t *mk = A.keys[z.key].mki;
+                    uint32_t d = 0;
+                    for (uint32_t b = 0; b < sz; b++)
+                        d |= p[b] ^ mk[b];
+                    if (d)
+                        ab |= FZ_AB_MKI;
+                }
+                const uint64_t idx = z.index;
+                const uint32_t seq = h.seq_len & 0xffffu;
+                // srtp_prepass.hip guess_index (rdbx.c:112-145)
+                int64_t delta;
+                if (idx > 32768) {
+                    const uint32_t lroc = (uint32_t)(idx >> 16);
+                    const uint32_t lseq = (uint32_t)(idx & 0xffffu);
+                    uint32_t roc = lroc;
+                    delta = (int64_t)seq - (int64_t)lseq;
+                    if (lseq < 32768) {
+                        if ((int)seq - (int)lseq > 32768) {
+                            roc = lroc - 1;
+                            delta -= 65536;
+                        }
+                    } else if ((int)lseq - 32768 > (int)seq) {
+                        roc = lroc + 1;
+                        delta += 65536;
+                    }
+                    e = ((uint64_t)roc << 16) | seq;
+                } else {
+                    e = seq;
+                    delta = (int64_t)seq - (int64_t)idx;
+                }
+                if (delta < 1)
+                    ab |= FZ_AB_ORDER;   // the sorted path decides
+                sid = z.sid;
+                fzu_cand(F, z, sid, e);
+                m.key = z.key;
+                m.roc = (uint32_t)(e >> 16);
+                m.info = es | (z.variant << 24);
+                m.len = len - tag;
+            }
+        }
+    }
+    const uint32_t cap = F.cap[i];
+    *(u32x4 *)&F.rec[i] =
+        u32x4{ (uint32_t)e, (uint32_t)(e >> 32) | (code << 16), sid, cap };
+    if (sid == FZ_NOCHAIN)
+        F.status[i] = (int32_t)code;   // a header error's status (any other
+                                       // non-candidate aborts the batch)
+    if (ab)
+        atomicOr(F.abort, ab);
+    return m;
+}
+
+// ... after icm_packet: the candidate's verdict (status, length; an
+// authenticated packet's index into the run and the second bitmap)
+DEV void fzu_verdict(const IcmArgs &A, uint32_t i, FzLane &z,
+                     const srtp_dev_meta_t &m, uint64_t e, uint32_t sid)
+{
+    if (sid == FZ_NOCHAIN)
+        return;
+    const IcmFused &F = A.fz;
+    if (A.auth_ok[i]) {
+        F.status[i] = 0;
+        F.cap[i] = m.len;
+        fzu_auth(F, z, e);
+    } else {
+        F.status[i] = 7;   // srtp_err_status_auth_fail
+        atomicAdd(F.nfail, 1u);
+    }
+}
+
 // All four T-tables (128 KiB of LDS, one 512-lane workgroup per CU).  The
 // AES schedule sits in SGPRs (KM_UNI / KM_WAVE) or VGPRs (KM_LANE).  With
 // per-lane keys the kernel needs 230-256 VGPRs, so two waves per SIMD is
@@ -813,13 +981,22 @@ void k_icm_hmac(IcmArgs A)
             z.run_cnt = 0;
             z.run_max = 0;
             z.run_min = ~0ull;
+            z.run_cmax = 0;
             for (uint32_t i = first; i < A.n; i += stride) {
-                const srtp_dev_meta_t m = fz_classify(A, i, z);
-                icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                    A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
-
+                if constexpr (PROTECT) {
+                    const srtp_dev_meta_t m = fz_classify(A, i, z);
+                    icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
+                        A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+                } else {
+                    uint64_t e;
+                    uint32_t sid;
+                    const srtp_dev_meta_t m = fzu_classify(A, i, z, e, sid);
+                    icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
+                        A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+                    fzu_verdict(A, i, z, m, e, sid);
+                }
             }
-            fz_flush(A.fz, z);
+            fz_flush<PROTECT>(A.fz, z);
             return;
         }
         for (uint32_t i = first; i < A.n; i += stride)
@@ -876,7 +1053,7 @@ static void icm_go(const IcmArgs &A, int ncu, hipStream_t st)
     const size_t cap = (size_t)ncu;
     if (wgs > cap)
         wgs = cap;
-    if constexpr (KM == KM_LANE && PR && NR > 0) {
+    if constexpr (KM == KM_LANE && NR > 0) {
         if (A.fused) {
             hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM, true>),
                                dim3((unsigned)wgs), dim3((unsigned)T), 0, st, A);

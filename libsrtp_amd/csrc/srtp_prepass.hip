@@ -129,8 +129,10 @@ struct PpState {
     uint32_t (*tsave)[4] = nullptr;
     // per stream: counts, lowest chain index; index bitmaps (2 x nwords)
     unsigned long long *fz_cnt = nullptr, *fz_emin = nullptr;
-    uint32_t *fz_bmap = nullptr;
+    uint32_t *fz_bmap = nullptr;   // 4 x nwords + 4: candidates | authenticated
     uint32_t bmap_cap = 0;
+    unsigned long long *fz_hicand = nullptr;   // unprotect: highest candidate
+    uint32_t *fz_nfail = nullptr;              // unprotect: failed tag checks
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -701,16 +703,23 @@ __global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
 // zero / empty (the bitmaps are zero between batches)
 __global__ void k_fz_reset(uint32_t *abort, unsigned long long *cnt,
                            unsigned long long *new_index,
-                           unsigned long long *emin, uint32_t ns)
+                           unsigned long long *emin,
+                           unsigned long long *hicand, uint32_t *nfail,
+                           uint32_t ns)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s == 0)
+    if (s == 0) {
         *abort = 0;
+        if (nfail)
+            *nfail = 0;
+    }
     if (s >= ns)
         return;
     cnt[s] = 0;
     new_index[s] = 0;
     emin[s] = ~0ull;
+    if (hicand)
+        hicand[s] = 0;
 }
 
 // ... per stream, after the crypto: the conditions of the order-free form
@@ -792,12 +801,107 @@ __global__ void k_fz_commit(srtp_dev_stream_t *st, uint32_t ns,
         win[off + w] = wnew[off + w];
 }
 
+// Fused order-free unprotect (pp_unprotect_fused), per stream after the
+// crypto: k_pp_usetbits' conditions over the candidates (every index above
+// the stored one -- checked in the kernel -- and within one window of the
+// highest candidate, else AB_ORDER; as many distinct indices as candidates,
+// else AB_SEQUENCE: a duplicate, whose verdict depends on the order), then
+// the window (rdbx_add after the tag check, srtp.c:3157-3167): the stored
+// one shifted to the highest AUTHENTICATED index, one bit per authenticated
+// packet; both bitmaps cleared
+__global__ void k_fzu_stream(const srtp_dev_stream_t *st, uint32_t ns,
+                             const unsigned long long *cnt,
+                             const unsigned long long *new_index,
+                             const unsigned long long *hicand,
+                             const unsigned long long *emin, uint32_t *bmap,
+                             uint32_t *bmap2, const uint32_t *win,
+                             uint32_t *wnew, uint32_t *abort)
+{
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= ns)
+        return;
+    const uint32_t cand = (uint32_t)(cnt[s] >> 32), acc = (uint32_t)cnt[s];
+    if (!cand)
+        return;
+    const srtp_dev_stream_t S = st[s];
+    const uint32_t bits = S.win_bits, words = bits >> 5;
+    const uint32_t M = bits > 32 ? 2u << (31 - __clz(bits - 1)) : 32u;
+    const uint32_t mw = M >> 5;
+    uint32_t *bc = bmap + 2 * S.win_off, *ba = bmap2 + 2 * S.win_off;
+    // candidates: distinct within one window of the highest
+    const uint64_t hc = hicand[s];
+    uint32_t seen = 0;
+    {
+        const uint32_t base = (uint32_t)(hc - bits + 1);
+        for (uint32_t j = 0; j < words; j++) {
+            const uint32_t r0 = (base + 32 * j) & (M - 1), sh = r0 & 31;
+            const uint32_t b0 = bc[r0 >> 5], b1 = bc[((r0 >> 5) + 1) & (mw - 1)];
+            seen += __popc(sh ? (b0 >> sh) | (b1 << (32 - sh)) : b0);
+        }
+    }
+    if (hc - emin[s] >= bits)
+        atomicOr(abort, AB_ORDER);
+    else if (seen != cand)
+        atomicOr(abort, AB_SEQUENCE);
+    if (acc) {
+        const uint64_t hi = new_index[s], adv = hi - S.index;
+        const uint32_t base = (uint32_t)(hi - bits + 1);
+        const uint32_t *w = win + S.win_off;
+        uint32_t *o = wnew + S.win_off;
+        for (uint32_t j = 0; j < words; j++) {
+            uint32_t v = 0;
+            if (adv < bits) {
+                const uint32_t q = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+                const uint32_t a = j + q < words ? w[j + q] : 0u;
+                const uint32_t b = j + q + 1 < words ? w[j + q + 1] : 0u;
+                v = bi ? (a >> bi) | (b << (32 - bi)) : a;
+            }
+            const uint32_t r0 = (base + 32 * j) & (M - 1), sh = r0 & 31;
+            const uint32_t b0 = ba[r0 >> 5], b1 = ba[((r0 >> 5) + 1) & (mw - 1)];
+            o[j] = v | (sh ? (b0 >> sh) | (b1 << (32 - sh)) : b0);
+        }
+    }
+    for (uint32_t j = 0; j < mw; j++) {
+        bc[j] = 0;
+        ba[j] = 0;
+    }
+}
+
+// ... and unless the batch was declined, the streams (k_pu_commit_stream:
+// key uses -- AES-GCM every candidate, AES-ICM the authenticated ones --,
+// index and window when something authenticated)
+__global__ void k_fzu_commit(srtp_dev_stream_t *st, uint32_t ns,
+                             const unsigned long long *cnt,
+                             const unsigned long long *new_index,
+                             const uint32_t *wnew, uint32_t *win,
+                             const uint32_t *abort, uint32_t *pub)
+{
+    publish_abort(pub, abort);
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (*abort || s >= ns)
+        return;
+    const uint64_t c = cnt[s];
+    if (!c)
+        return;
+    st[s].uses += (st[s].flags & SRTP_DS_AEAD) ? (uint32_t)(c >> 32)
+                                               : (uint32_t)c;
+    const uint64_t ni = new_index[s];
+    if (ni == 0)
+        return;
+    st[s].dir |= SRTP_DIR_RX;
+    st[s].index = ni;
+    const uint32_t off = st[s].win_off, words = st[s].win_bits >> 5;
+    for (uint32_t w = 0; w < words; w++)
+        win[off + w] = wnew[off + w];
+}
+
 // ... and a declined batch's descriptors, as k_icm_hmac had them, for the
 // undo (k_undo_wave re-applies the keystream); the capacities come back
 __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
                           const uint32_t *in_len, const FzRec *rec,
                           const srtp_dev_stream_t *st, uint32_t n,
-                          srtp_dev_meta_t *meta, uint32_t *cap)
+                          srtp_dev_meta_t *meta, uint32_t *cap,
+                          int unprotect, const int32_t *only_status)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
@@ -809,14 +913,18 @@ __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
     m.info = 0xff0000u;
     const uint4 r = *(const uint4 *)&rec[i];
     const uint32_t s = r.z, code = r.y >> 16;
-    if (s != NOCHAIN && code == 0) {
+    // only_status: just the packets with that status (unprotect: the
+    // candidates whose tag check failed, status 7), capacities untouched
+    if (s != NOCHAIN && code == 0 &&
+        (!only_status || only_status[i] == 7)) {
         const uint64_t off = in_off[i];
         const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
         m.key = st[s].key;
         m.roc = (r.x >> 16) | ((r.y & 0xffffu) << 16);
         m.info = h.enc_start | (st[s].variant << 24);
-        m.len = in_len[i];
-        cap[i] = r.w;
+        m.len = in_len[i] - (unprotect ? st[s].trailer : 0u);
+        if (!only_status)
+            cap[i] = r.w;
     }
     meta[i] = m;
 }
@@ -2373,7 +2481,7 @@ void srtp_gpu_pp_free(void *p)
                      P->rec, P->rec_idx, P->bk_range, P->ch_tile,
                      P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
                      P->pu_first, P->fzrec, P->tsave, P->fz_cnt,
-                     P->fz_emin, P->fz_bmap };
+                     P->fz_emin, P->fz_bmap, P->fz_hicand, P->fz_nfail };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2391,7 +2499,8 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
     uint32_t c1 = P->ns_cap, c2 = P->ns_cap, c5 = P->ns_cap,
              c6 = P->ns_cap, c7 = P->ns_cap, c8 = P->ns_cap, c9 = P->ns_cap,
-             c10 = P->ns_cap, c11 = P->ns_cap, c3 = P->nwords_cap;
+             c10 = P->ns_cap, c11 = P->ns_cap, c13 = P->ns_cap,
+             c3 = P->nwords_cap;
     if (regrow(&P->st, &P->ns_cap, ns + 1) ||
         regrow(&P->bcount, &c1, ns + 1) || regrow(&P->new_index, &c2, ns + 1) ||
         regrow(&P->seg_first, &c5, ns + 1) ||
@@ -2401,8 +2510,11 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
         regrow(&P->fz_cnt, &c10, ns + 1) || regrow(&P->fz_emin, &c11, ns + 1) ||
         regrow(&P->win, &P->nwords_cap, nwords + 1) ||
         regrow(&P->wnew, &c3, nwords + 1) ||
-        regrow(&P->fz_bmap, &P->bmap_cap, 2 * nwords + 2))
+        regrow(&P->fz_bmap, &P->bmap_cap, 4 * nwords + 4) ||
+        regrow(&P->fz_hicand, &c13, ns + 1))
         return -1;
+    if (!P->fz_nfail)
+        PPCHK(hipMalloc((void **)&P->fz_nfail, 4));
     if (hcap > P->hcap_cap || !P->hkey) {
         uint32_t c4 = P->hcap_cap;
         if (regrow(&P->hkey, &P->hcap_cap, hcap) || regrow(&P->hval, &c4, hcap))
@@ -2428,7 +2540,7 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
     P->ns = ns;
     P->nwords = nwords;
     P->hcap = hcap;
-    PPCHK(hipMemsetAsync(P->fz_bmap, 0, (2ull * nwords + 2) * 4, stream));
+    PPCHK(hipMemsetAsync(P->fz_bmap, 0, (4ull * nwords + 4) * 4, stream));
     PPCHK(hipMemcpyAsync(P->st, streams, ns * sizeof *streams,
                          hipMemcpyHostToDevice, stream));
     if (nwords) {
@@ -2723,7 +2835,8 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
     unsigned long long *hi = (unsigned long long *)P->new_index;
     hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
-                       P->abort, P->fz_cnt, hi, P->fz_emin, ns);
+                       P->abort, P->fz_cnt, hi, P->fz_emin, nullptr, nullptr,
+                       ns);
     IcmFused F;
     F.in_len = b->in_len;
     F.cap = b->out_len;
@@ -2754,7 +2867,7 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     cb.fused = &F;
     // a failed step may leave bitmap bits behind: clear them all
     auto fail = [&]() {
-        (void)hipMemsetAsync(P->fz_bmap, 0, (2ull * P->nwords + 2) * 4, stream);
+        (void)hipMemsetAsync(P->fz_bmap, 0, (4ull * P->nwords + 4) * 4, stream);
         return -1;
     };
     if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "fused crypto"))
@@ -2774,7 +2887,8 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
         return 0;
     // declined: the input comes back exactly
     hipLaunchKernelGGL(k_fz_meta, gp, blk, 0, stream, b->in, b->in_off,
-                       b->in_len, P->fzrec, P->st, N, P->meta, b->out_len);
+                       b->in_len, P->fzrec, P->st, N, P->meta, b->out_len, 0,
+                       nullptr);
     PPCHK(hipGetLastError());
     if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
         return -1;
@@ -3108,6 +3222,94 @@ static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
     return 0;
 }
 
+// The order-free receive form with its classification inside the AES-ICM
+// kernel (IcmFused, srtp_icm.hip fzu_classify / fzu_verdict): no separate
+// header, meta, accept or set-bits passes.  The conditions are checked on
+// per-stream aggregates afterwards (k_fzu_stream); a batch outside them
+// comes back exactly (every candidate's decryption undone, capacities
+// restored) and, for AB_ORDER, *sorted is set: the sorted chain form runs
+// it, else the host does.  Only in place, per-lane keys, one AES-ICM kernel
+// variant, several streams (fused_ok).
+static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
+                              srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                              int *fallback, bool *sorted)
+{
+    const uint32_t N = (uint32_t)b->n, ns = P->ns;
+    const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
+    *sorted = false;
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    unsigned long long *hi = (unsigned long long *)P->new_index;
+    hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
+                       P->abort, P->fz_cnt, hi, P->fz_emin, P->fz_hicand,
+                       P->fz_nfail, ns);
+    IcmFused F;
+    F.in_len = b->in_len;
+    F.cap = b->out_len;
+    F.status = b->status;
+    F.st = P->st;
+    F.hkey = P->hkey;
+    F.hval = P->hval;
+    F.hmask = P->hcap - 1;
+    F.rec = P->fzrec;
+    F.tsave = nullptr;
+    F.cnt = P->fz_cnt;
+    F.new_index = hi;
+    F.emin = P->fz_emin;
+    F.bmap = P->fz_bmap;
+    F.abort = P->abort;
+    F.hicand = P->fz_hicand;
+    F.bmap2 = P->fz_bmap + 2 * P->nwords + 2;
+    F.nfail = P->fz_nfail;
+    srtp_gpu_batch_t cb = {};
+    cb.n = b->n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;
+    cb.auth_ok = P->auth;
+    cb.uniform_key = 0xffffffffu;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = nullptr;   // the kernel itself classifies: it always runs
+    cb.fused = &F;
+    auto fail = [&]() {
+        (void)hipMemsetAsync(P->fz_bmap, 0, (4ull * P->nwords + 4) * 4, stream);
+        return -1;
+    };
+    if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "fused unprotect crypto"))
+        return fail();
+    hipLaunchKernelGGL(k_fzu_stream, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
+                       hi, P->fz_hicand, P->fz_emin, P->fz_bmap, F.bmap2,
+                       P->win, P->wnew, P->abort);
+    hipLaunchKernelGGL(k_fzu_commit, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
+                       hi, P->wnew, P->win, P->abort, P->h_abort_dev);
+    if (hipGetLastError() != hipSuccess ||
+        pp_step(stream, "fused unprotect commit"))
+        return fail();
+    uint32_t nfail = 0;
+    PPCHK(hipMemcpyAsync(&nfail, P->fz_nfail, 4, hipMemcpyDeviceToHost,
+                         stream));
+    PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    const uint32_t ab = *(volatile uint32_t *)P->h_abort;
+    *fallback = (int)ab;
+    if (!ab && !nfail)
+        return 0;
+    // declined: every candidate back to its ciphertext, the capacities
+    // back; accepted: the candidates whose tag failed back to ciphertext
+    hipLaunchKernelGGL(k_fz_meta, gp, blk, 0, stream, b->in, b->in_off,
+                       b->in_len, P->fzrec, P->st, N, P->meta, b->out_len, 1,
+                       ab ? nullptr : (const int32_t *)b->status);
+    PPCHK(hipGetLastError());
+    if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
+        return -1;
+    PPCHK(hipStreamSynchronize(stream));
+    *sorted = ab == AB_ORDER;
+    return 0;
+}
+
 int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                           int *fallback)
 {
@@ -3135,6 +3337,17 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     if (ns == 1 && fused_on())
         return pp_unprotect_chain1(g, P, b, stream, fallback);
     bool unordered = ns > 1 && !force_sorted;
+    if (unordered && b->fused_ok && fused_of_on() &&
+        !(b->uniform_key == 0xffffffffu && buckets_on())) {
+        bool sorted = false;
+        if (pp_unprotect_fused(g, P, b, stream, fallback, &sorted))
+            return -1;
+        if (!sorted) {
+            b->sorted = 0;
+            return 0;
+        }
+        unordered = false;   // restored, nothing committed: the chain form
+    }
     for (;;) {
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
     hipLaunchKernelGGL(k_pp_reset, dim3(ns / 256 + 1), blk, 0, stream, P->abort, P->bcount,

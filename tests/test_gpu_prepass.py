@@ -635,3 +635,113 @@ def test_mki_streams_on_device_prepass(name):
     for s in ssrcs[::5]:
         assert snd.get_roc(s)[1] == orc.get_roc(s)[1]
         assert rcv.get_roc(s)[1] == orc_r.get_roc(s)[1]
+
+
+# --------------------------------------------------------------------------
+# the receive side's order-free form classified inside the AES-ICM kernel
+# (srtp_prepass.hip pp_unprotect_fused): several streams, in place
+
+def _send_batches(snd, ssrcs, seq0, per, nb, rng, payloads=(0, 7, 160)):
+    out = []
+    for _ in range(nb):
+        pk = _interleaved(rng, ssrcs, seq0, per, payloads=payloads)
+        sent = []
+        for p in pk:
+            rc, ref = snd.protect(p, len(p) + 32)
+            assert rc == 0
+            sent.append(ref)
+        out.append(sent)
+    return out
+
+
+def _receive_check(lib, orc, pkts):
+    st, out = _device_run(lib, pkts, [len(p) for p in pkts], "unprotect")
+    for i, p in enumerate(pkts):
+        rc, ref = orc.unprotect(p, len(p))
+        assert st[i] == rc, (i, st[i], rc)
+        assert rc or out[i] == ref, i
+    return st
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
+                                  "icm128_nullauth"])
+def test_fused_unprotect_clean_forged_and_declined(name):
+    """clean batches, reordered inside the window, with forgeries (auth_fail,
+    undone in place), then a duplicate (-> host), an unknown SSRC (-> host),
+    a stream past its window (-> sorted form): statuses, bytes and the
+    stream state against the oracle's srtp_unprotect per packet"""
+    _gpu()
+    rng = random.Random(614)
+    ssrcs = [0x23000000 + 7 * k for k in range(40)]
+    pols = [policy(name, ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    lib, orc, snd = L.Session(pols), O.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
+    batches = _send_batches(snd, ssrcs, seq0, 20, 3, rng)
+    forge = name != "icm128_nullauth"
+    d0, h0 = lib.prepass_stats()
+    for b, sent in enumerate(batches):
+        rx = list(sent)
+        rng.shuffle(rx)     # every stream's 20 packets span < 64 indices
+        if forge and b == 1:
+            for k in rng.sample(range(len(rx)), 25):
+                x = bytearray(rx[k])
+                x[-1] ^= 0x20
+                rx[k] = bytes(x)
+        st = _receive_check(lib, orc, rx)
+        if forge and b == 1:
+            assert st.count(7) == 25
+    d, h = lib.prepass_stats()
+    assert (d - d0, h - h0) == (3, 0), lib.prepass_last_abort()
+    # declined batches: duplicate -> host, unknown SSRC -> host
+    sent = _send_batches(snd, ssrcs, seq0, 10, 1, rng)[0]
+    dup = sent[:50] + [sent[20]] + sent[50:]
+    _receive_check(lib, orc, dup)
+    unk_pol = policy(name, ssrc=0x0bad0bad, seed=99)
+    unk = O.Session([unk_pol]).protect(rtp_packet(rng, 0x0bad0bad, 5, 20), 64)[1]
+    sent = _send_batches(snd, ssrcs, seq0, 10, 1, rng)[0]
+    _receive_check(lib, orc, sent[:30] + [unk] + sent[30:])
+    d2, h2 = lib.prepass_stats()
+    assert h2 - h == 2, (d2 - d, h2 - h)
+    # long chains: the sorted chain form takes the batch after the restore
+    sent = _send_batches(snd, ssrcs[:4], seq0, 150, 1, rng)[0]
+    _receive_check(lib, orc, sent)
+    assert lib.prepass_stats()[1] == h2
+    for s in ssrcs[::3]:
+        assert lib.get_roc(s)[1] == orc.get_roc(s)[1]
+
+
+def test_fused_unprotect_windows_and_state():
+    """window sizes 64 / 96 / 160 / 1024, streams jumping past their window
+    between batches; afterwards old, replayed and skipped indices probed
+    one by one through the host path against the oracle"""
+    _gpu()
+    rng = random.Random(615)
+    wins = [64, 96, 160, 1024]
+    ssrcs = [0x24000000 + 5 * k for k in range(32)]
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k, window=wins[k % 4])
+            for k, s in enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    snd = O.Session(pols)
+    seq0 = {s: rng.randrange(100, 0xf000) for s in ssrcs}
+    kept = {s: [] for s in ssrcs}
+    for b in range(3):
+        if b == 1:
+            for s in ssrcs[::3]:
+                seq0[s] += rng.randrange(70, 3000)
+        pk = _interleaved(rng, ssrcs, seq0, 16, shuffle_within=0.3,
+                          payloads=(0, 5, 160))
+        rx = []
+        for p in pk:
+            rc, ref = snd.protect(p, len(p) + 32)
+            assert rc == 0
+            rx.append(ref)
+            kept[int.from_bytes(p[8:12], "big")].append(ref)
+        _receive_check(lib, orc, rx)
+        assert lib.prepass_last_abort() == 0, (b, lib.prepass_last_abort())
+    assert lib.prepass_stats() == (3, 0)
+    for k, s in enumerate(ssrcs):
+        assert lib.get_roc(s)[1] == orc.get_roc(s)[1]
+        for p in rng.sample(kept[s], 4):   # replays: host path, one by one
+            st, out = lib.unprotect(p, len(p))
+            rc, ref = orc.unprotect(p, len(p))
+            assert st == rc, (k, st, rc)
