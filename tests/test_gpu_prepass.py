@@ -745,3 +745,64 @@ def test_fused_unprotect_windows_and_state():
             st, out = lib.unprotect(p, len(p))
             rc, ref = orc.unprotect(p, len(p))
             assert st == rc, (k, st, rc)
+
+
+@pytest.mark.parametrize("step", ["max", "mixed"])
+def test_one_stream_chain_over_many_tiles_with_large_advances(step):
+    """one stream, 300,000 packets (73 look-back tiles of 4096) whose
+    sequence numbers advance by up to 2^15 - 1 each: the index sum crosses
+    2^32 inside the batch (the look-back's advance sum must not
+    wrap).  Protect on the device chain form and unprotect on the device
+    receive chain, every packet against the C oracle."""
+    _gpu()
+    import numpy as np
+    import torch
+    n, slot = 300000, 48
+    rng = np.random.default_rng(77 if step == "max" else 78)
+    if step == "max":
+        adv = np.full(n, 32767, dtype=np.int64)
+    else:
+        adv = np.where(rng.random(n) < 0.5, 32767, rng.integers(1, 32768, n))
+    adv[0] = 0
+    idx = 5 + np.cumsum(adv)
+    assert idx[-1] > 1 << 32
+    pol = policy("icm128_hmac80", ssrc=0x31415926, seed=9)
+    a = rng.integers(0, 256, (n, slot), dtype=np.uint8)
+    plen = rng.integers(0, 17, n)
+    seq = idx & 0xffff
+    a[:, 0], a[:, 1] = 0x80, 96
+    a[:, 2], a[:, 3] = seq >> 8, seq & 0xff
+    a[:, 8:12] = np.frombuffer((0x31415926).to_bytes(4, "big"), dtype=np.uint8)
+    ln = (12 + plen).astype(np.uint32)
+    orc = O.Session([pol])
+    bad, ref, rlen = orc.protect_many(a.reshape(-1),
+                                      np.arange(n, dtype=np.uint64) * slot,
+                                      ln, slot)
+    assert bad == 0
+    lib = L.Session([pol])
+    d = torch.from_numpy(a.copy()).cuda().view(-1)
+    off = (torch.arange(n, dtype=torch.int64) * slot).cuda()
+    tl = torch.from_numpy(ln.astype(np.int32)).cuda()
+    cap = torch.full((n,), slot, dtype=torch.int32).cuda()
+    st = torch.full((n,), -1, dtype=torch.int32).cuda()
+    assert lib.protect_device(d, off, tl, d, off, cap, st) == 0
+    assert lib.prepass_stats() == (1, 0), lib.prepass_last_abort()
+    assert int((st != 0).sum()) == 0
+    got = d.cpu().numpy().reshape(n, slot)
+    cap = cap.cpu().numpy()
+    assert (cap == rlen).all()
+    used = np.arange(slot)[None, :] < rlen[:, None]   # each packet's bytes
+    diff = np.nonzero(((got != ref) & used).any(axis=1))[0]
+    assert len(diff) == 0, diff[:8]
+    assert lib.get_roc(0x31415926)[1] == orc.get_roc(0x31415926)[1]
+    # the receiver, same batch, device chain
+    rcv = L.Session([pol])
+    cap2 = torch.full((n,), slot, dtype=torch.int32).cuda()
+    st2 = torch.full((n,), -1, dtype=torch.int32).cuda()
+    srl = torch.from_numpy(rlen.astype(np.int32)).cuda()
+    assert rcv.unprotect_device(d, off, srl, d, off, cap2, st2) == 0
+    assert rcv.prepass_stats() == (1, 0), rcv.prepass_last_abort()
+    assert int((st2 != 0).sum()) == 0
+    back = d.cpu().numpy().reshape(n, slot)
+    used = np.arange(slot)[None, :] < ln[:, None].astype(np.int64)
+    assert not ((back != a) & used).any()
