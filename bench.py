@@ -14,14 +14,23 @@ before the timed region.
 --op unprotect: the receive side of the same workload -- the batches are
 protected (untimed) by a sender session, and one step is
 srtp_unprotect_device() over one batch, in place, on the receiver session.
+--reorder P / --dup Q (unprotect): the receive batches arrive in network
+order -- a fraction P of arrivals swapped with one up to 32 places later,
+a fraction Q replaced by a copy of a packet up to 64 places earlier
+(replay_fail) -- built in HBM before the timed region.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
                   [--config icm128|gcm256|g711] [--op protect|unprotect]
+                  [--reorder P] [--dup Q]
 
 Multi-GPU: one process per GPU (torch.distributed.run, nccl = RCCL), each
 rank protects its own 2^20-packet batch of its own stream (weak scaling).
-The master keys are rank 0's and reach the other ranks in one broadcast over
-xGMI (the session (re)key step); the data path has no collective.  value =
+Rank 0 creates the session and the others receive a replica through the
+library's C ABI (srtp_mi355x_session_broadcast: one ncclBroadcast of the
+exported session over xGMI on torch's own communicator; under gloo the
+exported blob goes through the process group); the data path has no
+collective.  SRTP_BENCH_DEVICE=d puts every rank on device d (the N > 1
+path on a one-GPU box, with SRTP_DIST_BACKEND=gloo).  value =
 all ranks' packets / max rank time.  `--gpus N` with N > 1 and no
 WORLD_SIZE in the environment starts the N ranks itself (a
 torch.distributed.run child, before this process touches the GPU) and exits
@@ -35,8 +44,11 @@ max over ranks, the one JSON line) over gloo on the CPU with a stub step
 (rank r sleeps (r + 1) ms), for tests without a GPU.
 
 Extra fields: roofline (dominant kernel, HIP-event timed on the stream the
-kernels ran on), cpu_baseline (the reference, cisco/libsrtp built from its
-own sources, srtp_protect() per packet on host threads, rank 0 only).
+kernels ran on; `traffic` = FETCH_SIZE + WRITE_SIZE per launch from
+separate rocprofv3 PMC passes, `traffic_shape` = those counters against a
+byte-exact copy of the kernel's access shape, `issue` = VALU / LDS
+instruction floors), cpu_baseline (the reference, cisco/libsrtp built from
+its own sources, srtp_protect() per packet on host threads, rank 0 only).
 """
 import argparse
 import ctypes as C
