@@ -588,11 +588,16 @@ struct FzLane {
     uint64_t run_cnt;              // protect: packets | chain packets << 32
     uint64_t run_max, run_min;
     uint64_t run_cmax;             // unprotect only
+    uint32_t bw_idx, bw_bits;      // protect: pending bits of one bitmap word
 };
 
 template <bool PROTECT>
 DEV void fz_flush(const IcmFused &F, FzLane &z)
 {
+    if (PROTECT && z.bw_bits) {
+        atomicOr(&F.bmap[z.bw_idx], z.bw_bits);
+        z.bw_bits = 0;
+    }
     if (z.run_sid != FZ_NOCHAIN) {
         atomicAdd(&F.cnt[z.run_sid], (unsigned long long)z.run_cnt);
         if (PROTECT) {
@@ -653,8 +658,21 @@ DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, bool chain,
     if (chain) {
         z.run_max = e > z.run_max ? e : z.run_max;
         z.run_min = e < z.run_min ? e : z.run_min;
+        // a lane's packets of one stream are often a few indices apart:
+        // their bits are merged per bitmap word before the atomic
         const uint32_t r = (uint32_t)e & z.bmask;
-        atomicOr(&F.bmap[z.boff + (r >> 5)], 1u << (r & 31));
+        const uint32_t w = z.boff + (r >> 5);
+#ifdef FZ_EXP_NO_WMERGE   // timing: one atomic per packet (round-4 s10)
+        atomicOr(&F.bmap[w], 1u << (r & 31));
+        return;
+#endif
+        if (w != z.bw_idx) {
+            if (z.bw_bits)
+                atomicOr(&F.bmap[z.bw_idx], z.bw_bits);
+            z.bw_idx = w;
+            z.bw_bits = 0;
+        }
+        z.bw_bits |= 1u << (r & 31);
     }
 }
 
@@ -982,6 +1000,8 @@ void k_icm_hmac(IcmArgs A)
             z.run_max = 0;
             z.run_min = ~0ull;
             z.run_cmax = 0;
+            z.bw_idx = 0;
+            z.bw_bits = 0;
             for (uint32_t i = first; i < A.n; i += stride) {
                 if constexpr (PROTECT) {
                     const srtp_dev_meta_t m = fz_classify(A, i, z);
