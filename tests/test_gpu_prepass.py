@@ -806,3 +806,68 @@ def test_one_stream_chain_over_many_tiles_with_large_advances(step):
     back = d.cpu().numpy().reshape(n, slot)
     used = np.arange(slot)[None, :] < ln[:, None].astype(np.int64)
     assert not ((back != a) & used).any()
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_fused_paths_random_traffic(seed):
+    """randomised batches through the device pre-passes (order-free forms in
+    the AES-ICM kernel, sorted chain form, host fallbacks), protect and
+    unprotect, in place: streams with windows 64..1024, payloads 0..300 B,
+    reordering inside and beyond the window, duplicates, unknown SSRCs,
+    forged packets, jumps.  Every status and byte of both sides against the
+    oracle, and the stream state at the end."""
+    _gpu()
+    rng = random.Random(700 + seed)
+    ns = rng.choice([3, 17, 64])
+    ssrcs = [0x25000000 + 11 * k + seed for k in range(ns)]
+    pols = [policy(rng.choice(["icm128_hmac80", "icm128_hmac80",
+                               "icm256_hmac32"]) if seed == 3 else
+                   "icm128_hmac80", ssrc=s, seed=k,
+                   window=rng.choice([64, 128, 128, 256, 1024]))
+            for k, s in enumerate(ssrcs)]
+    slib, sorc = L.Session(pols), O.Session(pols)
+    rlib, rorc = L.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(1, 0xffff) for s in ssrcs}
+    for b in range(8):
+        per = rng.choice([1, 5, 20, 40])
+        pk = _interleaved(rng, ssrcs, seq0, per,
+                          shuffle_within=rng.choice([0, 0.1, 0.5]),
+                          payloads=(0, 1, 13, 160, 300))
+        event = rng.choice(["none", "none", "dup", "unknown", "jump"])
+        if event == "dup" and len(pk) > 10:
+            pk.insert(rng.randrange(5, len(pk)), pk[rng.randrange(0, 5)])
+        elif event == "unknown":
+            pk.insert(rng.randrange(0, len(pk)),
+                      rtp_packet(rng, 0x0badf00d, 7, 30))
+        elif event == "jump":
+            s = rng.choice(ssrcs)
+            seq0[s] += rng.randrange(100, 20000)
+        caps = [len(p) + rng.choice([10, 16, 40]) for p in pk]
+        st, out = _device_run(slib, pk, caps, "protect")
+        sent = []
+        for i, p in enumerate(pk):
+            rc, ref = sorc.protect(p, caps[i])
+            assert st[i] == rc, (b, event, i, st[i], rc)
+            assert rc or out[i] == ref, (b, event, i)
+            if rc == 0:
+                sent.append(ref)
+        # the receiver: the sent packets shuffled, some forged / repeated
+        rx = list(sent)
+        if rng.random() < 0.5:
+            rng.shuffle(rx)
+        for k in rng.sample(range(len(rx)), min(len(rx), rng.choice([0, 3]))):
+            x = bytearray(rx[k])
+            x[-1] ^= 0x11
+            rx[k] = bytes(x)
+        if rx and rng.random() < 0.3:
+            rx.append(rx[rng.randrange(len(rx))])
+        if not rx:
+            continue
+        st, out = _device_run(rlib, rx, [len(p) for p in rx], "unprotect")
+        for i, p in enumerate(rx):
+            rc, ref = rorc.unprotect(p, len(p))
+            assert st[i] == rc, ("rx", b, i, st[i], rc)
+            assert rc or out[i] == ref, ("rx", b, i)
+    for s in ssrcs:
+        assert slib.get_roc(s)[1] == sorc.get_roc(s)[1]
+        assert rlib.get_roc(s)[1] == rorc.get_roc(s)[1]
