@@ -349,6 +349,11 @@ int srtp_gpu_h2d(srtp_gpu_t *g, void *dst, const void *src, size_t n,
 int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
                  void *stream);
 int srtp_gpu_sync(srtp_gpu_t *g, void *stream);
+/* a marker on `stream` after the work queued so far (slot < SRTP_GPU_MARKS),
+ * and a host wait for it */
+#define SRTP_GPU_MARKS 16
+int srtp_gpu_mark(srtp_gpu_t *g, int slot, void *stream);
+int srtp_gpu_mark_wait(srtp_gpu_t *g, int slot);
 
 /* timing of the last srtp_gpu_run kernels (ms, from HIP events) */
 double srtp_gpu_last_kernel_ms(srtp_gpu_t *g);

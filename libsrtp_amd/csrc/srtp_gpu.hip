@@ -1352,6 +1352,9 @@ void srtp_gpu_close(srtp_gpu_t *g)
     (void)hipFree(g->d_ghash);
     (void)hipFree(g->d_raw);
     (void)hipFree(g->d_undo);
+    for (int k = 0; k < SRTP_GPU_MARKS; k++)
+        if (g->marks[k])
+            (void)hipEventDestroy(g->marks[k]);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);
     (void)hipStreamDestroy(g->stream);
@@ -1610,6 +1613,26 @@ int srtp_gpu_sync(srtp_gpu_t *g, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;   // NULL = the null stream
     HIPCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+// events of the host-batch staging pipeline (srtp_host.c
+// batch_device_fast): slot k marks "chunk k's copy is done" on a stream
+int srtp_gpu_mark(srtp_gpu_t *g, int slot, void *stream)
+{
+    if (slot < 0 || slot >= SRTP_GPU_MARKS)
+        return srtp_gpu_fail(hipErrorInvalidValue, "mark slot");
+    if (!g->marks[slot])
+        HIPCHK(hipEventCreateWithFlags(&g->marks[slot], hipEventDisableTiming));
+    HIPCHK(hipEventRecord(g->marks[slot], (hipStream_t)stream));
+    return 0;
+}
+
+int srtp_gpu_mark_wait(srtp_gpu_t *g, int slot)
+{
+    if (slot < 0 || slot >= SRTP_GPU_MARKS || !g->marks[slot])
+        return srtp_gpu_fail(hipErrorInvalidValue, "mark slot");
+    HIPCHK(hipEventSynchronize(g->marks[slot]));
     return 0;
 }
 

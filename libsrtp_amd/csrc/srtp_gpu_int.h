@@ -33,6 +33,7 @@ struct srtp_gpu {
     // srtp_gpu_undo: the compacted list of packets to undo (+ its count)
     uint32_t *d_undo;
     size_t undo_cap;
+    hipEvent_t marks[SRTP_GPU_MARKS];   // srtp_gpu_mark / _mark_wait
 };
 
 // The order-free protect pre-pass's classification done by k_icm_hmac

@@ -2535,13 +2535,20 @@ static void *par_run(void *p)
     return NULL;
 }
 
-static void par_for(size_t n, void (*fn)(void *, size_t, size_t), void *arg)
+static void par_for_range(size_t lo, size_t hi,
+                          void (*fn)(void *, size_t, size_t), void *arg);
+#define STAGE_CHUNKS 8   /* < SRTP_GPU_MARKS */
+
+/* fn over [lo, hi) on up to 8 host threads */
+static void par_for_range(size_t lo0, size_t hi0,
+                          void (*fn)(void *, size_t, size_t), void *arg)
 {
+    const size_t n = hi0 - lo0;
     size_t t = n / 16384;
     if (t > 8)
         t = 8;
     if (t < 2) {
-        fn(arg, 0, n);
+        fn(arg, lo0, hi0);
         return;
     }
     pthread_t th[8];
@@ -2550,8 +2557,8 @@ static void par_for(size_t n, void (*fn)(void *, size_t, size_t), void *arg)
     for (size_t k = 0; k < t; k++) {
         jobs[k].fn = fn;
         jobs[k].arg = arg;
-        jobs[k].lo = n * k / t;
-        jobs[k].hi = n * (k + 1) / t;
+        jobs[k].lo = lo0 + n * k / t;
+        jobs[k].hi = lo0 + n * (k + 1) / t;
         if (k > 0 && pthread_create(&th[k], NULL, par_run, &jobs[k]) == 0)
             started |= (size_t)1 << k;
         else if (k > 0)
@@ -2621,13 +2628,22 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
         off += r16(in_len[i] + extra);
     }
     gather_t g = { sg, in, in_len, out, out_len, status, extra };
-    par_for(n, gather_part, &g);
     void *hs = HS(ctx);
-    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, hs) ||
-        srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, hs) ||
+    /* the gather of chunk c+1 on the host threads overlaps the copy of
+     * chunk c (the arena is pinned: the copies are asynchronous) */
+    const size_t nck = n >= 65536 ? STAGE_CHUNKS : 1;
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, hs) ||
         srtp_gpu_h2d(ctx->gpu, sg->d_len, sg->h_len, n * 4, hs) ||
         srtp_gpu_h2d(ctx->gpu, sg->d_cap, sg->h_cap, n * 4, hs))
         return -1;
+    for (size_t c = 0; c < nck; c++) {
+        const size_t lo = n * c / nck, hi = n * (c + 1) / nck;
+        const size_t b0 = sg->h_off[lo], b1 = hi < n ? sg->h_off[hi] : off;
+        par_for_range(lo, hi, gather_part, &g);
+        if (srtp_gpu_h2d(ctx->gpu, sg->d_arena + b0, sg->h_arena + b0,
+                         b1 - b0, hs))
+            return -1;
+    }
     srtp_device_batch_t b;
     memset(&b, 0, sizeof b);
     b.n = n;
@@ -2646,12 +2662,28 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
     if (fast <= 0)
         return fast;
     ctx->dt.fast_batches++;
-    if (srtp_gpu_d2h(ctx->gpu, sg->h_arena, sg->d_arena, off, hs) ||
-        srtp_gpu_d2h(ctx->gpu, sg->h_cap, sg->d_cap, n * 4, hs) ||
+    /* statuses and lengths first, then the arena chunk by chunk: the
+     * scatter of chunk c overlaps the copy of chunk c+1 */
+    if (srtp_gpu_d2h(ctx->gpu, sg->h_cap, sg->d_cap, n * 4, hs) ||
         srtp_gpu_d2h(ctx->gpu, sg->h_st, sg->d_st, n * 4, hs) ||
-        srtp_gpu_sync(ctx->gpu, hs))
+        srtp_gpu_mark(ctx->gpu, 0, hs))
         return -1;
-    par_for(n, scatter_part, &g);
+    for (size_t c = 0; c < nck; c++) {
+        const size_t lo = n * c / nck, hi = n * (c + 1) / nck;
+        const size_t b0 = sg->h_off[lo], b1 = hi < n ? sg->h_off[hi] : off;
+        if (srtp_gpu_d2h(ctx->gpu, sg->h_arena + b0, sg->d_arena + b0,
+                         b1 - b0, hs) ||
+            srtp_gpu_mark(ctx->gpu, (int)c + 1, hs))
+            return -1;
+    }
+    if (srtp_gpu_mark_wait(ctx->gpu, 0))
+        return -1;
+    for (size_t c = 0; c < nck; c++) {
+        const size_t lo = n * c / nck, hi = n * (c + 1) / nck;
+        if (srtp_gpu_mark_wait(ctx->gpu, (int)c + 1))
+            return -1;
+        par_for_range(lo, hi, scatter_part, &g);
+    }
     for (size_t i = 0; i < n; i++)
         status[i] = (srtp_err_status_t)sg->h_st[i];
     return 1;
