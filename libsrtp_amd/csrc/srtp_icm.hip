@@ -730,7 +730,12 @@ DEV void fz_lookup(const IcmFused &F, FzLane &z, uint32_t ssrc)
     z.bmask = (S.win_bits > 32 ? 2u << (31 - __clz(S.win_bits - 1)) : 32u) - 1;
 }
 
-DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
+// `vid`: the kernel variant this launch runs (every eligible stream's, by
+// fused_ok); a packet of another variant (only an ineligible stream can
+// have one) is not encrypted here, so it must not count as done: the
+// batch is declined without it
+DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
+                                uint32_t vid)
 {
     const IcmFused &F = A.fz;
     const uint64_t off = A.in_off[i];
@@ -750,6 +755,8 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
         const uint32_t sid = z.sid;
         if (sid == FZ_NOCHAIN) {
             ab |= FZ_AB_UNKNOWN;    // template clone: host
+        } else if (z.variant != vid) {
+            ab |= FZ_AB_INELIGIBLE;
         } else {
             if (!(z.flags & SRTP_DS_ELIGIBLE) || (z.dir & SRTP_DIR_RX))
                 ab |= FZ_AB_INELIGIBLE;
@@ -837,7 +844,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z)
 // writes its status and length.  `e` / `sid` out: the candidate's index and
 // stream (sid ~0: not a candidate).
 DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
-                                 uint64_t &e, uint32_t &sid)
+                                 uint32_t vid, uint64_t &e, uint32_t &sid)
 {
     const IcmFused &F = A.fz;
     const uint64_t off = A.in_off[i];
@@ -857,6 +864,8 @@ DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
         fz_lookup(F, z, h.ssrc);
         if (z.sid == FZ_NOCHAIN) {
             ab |= FZ_AB_UNKNOWN;    // template clone: host
+        } else if (z.variant != vid) {
+            ab |= FZ_AB_INELIGIBLE;  // not decrypted here (fz_classify)
         } else {
             if (!(z.flags & SRTP_DS_RX_ELIGIBLE) || (z.dir & SRTP_DIR_TX))
                 ab |= FZ_AB_INELIGIBLE;
@@ -1004,13 +1013,15 @@ void k_icm_hmac(IcmArgs A)
             z.bw_bits = 0;
             for (uint32_t i = first; i < A.n; i += stride) {
                 if constexpr (PROTECT) {
-                    const srtp_dev_meta_t m = fz_classify(A, i, z);
+                    const srtp_dev_meta_t m =
+                        fz_classify(A, i, z, icm_vid<NR, AUTH>());
                     icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
                         A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
                 } else {
                     uint64_t e;
                     uint32_t sid;
-                    const srtp_dev_meta_t m = fzu_classify(A, i, z, e, sid);
+                    const srtp_dev_meta_t m =
+                        fzu_classify(A, i, z, icm_vid<NR, AUTH>(), e, sid);
                     icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
                         A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
                     fzu_verdict(A, i, z, m, e, sid);

@@ -871,3 +871,42 @@ def test_fused_paths_random_traffic(seed):
     for s in ssrcs:
         assert slib.get_roc(s)[1] == sorc.get_roc(s)[1]
         assert rlib.get_roc(s)[1] == rorc.get_roc(s)[1]
+
+
+def test_fused_paths_ineligible_stream_of_another_variant():
+    """a stream the device pre-pass cannot take (pending ROC after
+    srtp_stream_set_roc) whose cipher is not the batch's AES-ICM kernel
+    variant (AES-GCM): its packets must not be counted as processed by the
+    fused kernel, so the declined batch's undo leaves them alone and the
+    host path produces the reference's bytes (protect and unprotect)"""
+    _gpu()
+    rng = random.Random(616)
+    ssrcs = [0x26000000 + 3 * k for k in range(24)]
+    g_ssrc = 0x26ffff01
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    pols.append(policy("gcm256_16", ssrc=g_ssrc, seed=77))
+    for op in ("protect", "unprotect"):
+        lib, orc = L.Session(pols), O.Session(pols)
+        snd = O.Session(pols)
+        seq0 = {s: rng.randrange(1, 0xf000) for s in ssrcs + [g_ssrc]}
+        # a clean batch first (device), then set_roc on the GCM stream
+        for b in range(2):
+            pk = _interleaved(rng, ssrcs + [g_ssrc], seq0, 6,
+                              payloads=(0, 20, 160))
+            if b == 1:
+                assert lib.set_roc(g_ssrc, 3) == 0
+                assert orc.set_roc(g_ssrc, 3) == 0
+            if op == "protect":
+                caps = [len(p) + 32 for p in pk]
+                st, out = _device_run(lib, pk, caps, "protect")
+                for i, p in enumerate(pk):
+                    rc, ref = orc.protect(p, caps[i])
+                    assert st[i] == rc, (b, i, st[i], rc)
+                    assert rc or out[i] == ref, (b, i)
+            else:
+                if b == 1:
+                    assert snd.set_roc(g_ssrc, 3) == 0
+                rx = [snd.protect(p, len(p) + 32)[1] for p in pk]
+                _receive_check(lib, orc, rx)
+        d, h = lib.prepass_stats()
+        assert h >= 1, (op, d, h)
