@@ -772,29 +772,9 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                 if ((z.flags & SRTP_DS_ICM_CONF) &&
                     (len - h.enc_start + 15) / 16 > 0xffffu)
                     code = 8;        // srtp_err_status_cipher_fail
-                const uint64_t idx = z.index;
                 const uint32_t seq = h.seq_len & 0xffffu;
-                // srtp_prepass.hip guess_index (rdbx.c:112-145)
-                int64_t delta;
-                if (idx > 32768) {
-                    const uint32_t lroc = (uint32_t)(idx >> 16);
-                    const uint32_t lseq = (uint32_t)(idx & 0xffffu);
-                    uint32_t roc = lroc;
-                    delta = (int64_t)seq - (int64_t)lseq;
-                    if (lseq < 32768) {
-                        if ((int)seq - (int)lseq > 32768) {
-                            roc = lroc - 1;
-                            delta -= 65536;
-                        }
-                    } else if ((int)lseq - 32768 > (int)seq) {
-                        roc = lroc + 1;
-                        delta += 65536;
-                    }
-                    e = ((uint64_t)roc << 16) | seq;
-                } else {
-                    e = seq;
-                    delta = (int64_t)seq - (int64_t)idx;
-                }
+                // rdbx.c:112-145 (srtp_rtp_hdr.h)
+                const int64_t delta = srtp_guess_index(z.index, seq, &e);
                 if (delta < 1)
                     ab |= FZ_AB_ORDER;   // the sorted path decides
                 fz_count(F, z, sid, true, e);
@@ -889,29 +869,9 @@ DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                     if (d)
                         ab |= FZ_AB_MKI;
                 }
-                const uint64_t idx = z.index;
                 const uint32_t seq = h.seq_len & 0xffffu;
-                // srtp_prepass.hip guess_index (rdbx.c:112-145)
-                int64_t delta;
-                if (idx > 32768) {
-                    const uint32_t lroc = (uint32_t)(idx >> 16);
-                    const uint32_t lseq = (uint32_t)(idx & 0xffffu);
-                    uint32_t roc = lroc;
-                    delta = (int64_t)seq - (int64_t)lseq;
-                    if (lseq < 32768) {
-                        if ((int)seq - (int)lseq > 32768) {
-                            roc = lroc - 1;
-                            delta -= 65536;
-                        }
-                    } else if ((int)lseq - 32768 > (int)seq) {
-                        roc = lroc + 1;
-                        delta += 65536;
-                    }
-                    e = ((uint64_t)roc << 16) | seq;
-                } else {
-                    e = seq;
-                    delta = (int64_t)seq - (int64_t)idx;
-                }
+                // rdbx.c:112-145 (srtp_rtp_hdr.h)
+                const int64_t delta = srtp_guess_index(z.index, seq, &e);
                 if (delta < 1)
                     ab |= FZ_AB_ORDER;   // the sorted path decides
                 sid = z.sid;

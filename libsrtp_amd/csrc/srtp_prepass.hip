@@ -220,25 +220,7 @@ __device__ __forceinline__ bool mki_is_device_key(const srtp_dev_key_t *keys,
 __device__ __forceinline__ int64_t guess_index(uint64_t idx, uint32_t seq,
                                                uint64_t *est)
 {
-    if (idx > SEQ_MEDIAN) {
-        const uint32_t lroc = (uint32_t)(idx >> 16);
-        const uint32_t lseq = (uint32_t)(idx & 0xffffu);
-        uint32_t roc = lroc;
-        int64_t diff = (int64_t)seq - (int64_t)lseq;
-        if (lseq < SEQ_MEDIAN) {
-            if ((int)seq - (int)lseq > (int)SEQ_MEDIAN) {
-                roc = lroc - 1;
-                diff -= 65536;
-            }
-        } else if ((int)lseq - (int)SEQ_MEDIAN > (int)seq) {
-            roc = lroc + 1;
-            diff += 65536;
-        }
-        *est = ((uint64_t)roc << 16) | seq;
-        return diff;
-    }
-    *est = seq;
-    return (int64_t)seq - (int64_t)idx;
+    return srtp_guess_index(idx, seq, est);   // srtp_rtp_hdr.h
 }
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m)

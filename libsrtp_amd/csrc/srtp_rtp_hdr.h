@@ -94,4 +94,31 @@ __device__ __forceinline__ uint32_t srtp_rtp_xinfo(const uint8_t *p,
     return v;
 }
 
+// index_guess against a stream's stored index (srtp_host.c estimate /
+// index_guess = crypto/replay/rdbx.c:112-145, 280-299): the 48-bit index
+// of sequence number seq and the signed distance from idx
+__device__ __forceinline__ int64_t srtp_guess_index(uint64_t idx, uint32_t seq,
+                                                    uint64_t *est)
+{
+    if (idx > 32768) {
+        const uint32_t lroc = (uint32_t)(idx >> 16);
+        const uint32_t lseq = (uint32_t)(idx & 0xffffu);
+        uint32_t roc = lroc;
+        int64_t diff = (int64_t)seq - (int64_t)lseq;
+        if (lseq < 32768) {
+            if ((int)seq - (int)lseq > 32768) {
+                roc = lroc - 1;
+                diff -= 65536;
+            }
+        } else if ((int)lseq - 32768 > (int)seq) {
+            roc = lroc + 1;
+            diff += 65536;
+        }
+        *est = ((uint64_t)roc << 16) | seq;
+        return diff;
+    }
+    *est = seq;
+    return (int64_t)seq - (int64_t)idx;
+}
+
 #endif
