@@ -354,6 +354,11 @@ int srtp_gpu_sync(srtp_gpu_t *g, void *stream);
 #define SRTP_GPU_MARKS 16
 int srtp_gpu_mark(srtp_gpu_t *g, int slot, void *stream);
 int srtp_gpu_mark_wait(srtp_gpu_t *g, int slot);
+/* `stream` waits for the marker (device side) */
+int srtp_gpu_mark_stream_wait(srtp_gpu_t *g, void *stream, int slot);
+/* copy streams of the host-batch pipeline (k = 0 in, 1 out), created on
+ * first use; NULL on failure */
+void *srtp_gpu_aux_stream(srtp_gpu_t *g, int k);
 
 /* timing of the last srtp_gpu_run kernels (ms, from HIP events) */
 double srtp_gpu_last_kernel_ms(srtp_gpu_t *g);

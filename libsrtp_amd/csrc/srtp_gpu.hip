@@ -1355,6 +1355,9 @@ void srtp_gpu_close(srtp_gpu_t *g)
     for (int k = 0; k < SRTP_GPU_MARKS; k++)
         if (g->marks[k])
             (void)hipEventDestroy(g->marks[k]);
+    for (int k = 0; k < 2; k++)
+        if (g->aux[k])
+            (void)hipStreamDestroy(g->aux[k]);
     (void)hipEventDestroy(g->ev0);
     (void)hipEventDestroy(g->ev1);
     (void)hipStreamDestroy(g->stream);
@@ -1626,6 +1629,26 @@ int srtp_gpu_mark(srtp_gpu_t *g, int slot, void *stream)
         HIPCHK(hipEventCreateWithFlags(&g->marks[slot], hipEventDisableTiming));
     HIPCHK(hipEventRecord(g->marks[slot], (hipStream_t)stream));
     return 0;
+}
+
+int srtp_gpu_mark_stream_wait(srtp_gpu_t *g, void *stream, int slot)
+{
+    if (slot < 0 || slot >= SRTP_GPU_MARKS || !g->marks[slot])
+        return srtp_gpu_fail(hipErrorInvalidValue, "mark slot");
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, g->marks[slot], 0));
+    return 0;
+}
+
+void *srtp_gpu_aux_stream(srtp_gpu_t *g, int k)
+{
+    if (k < 0 || k >= 2)
+        return nullptr;
+    if (!g->aux[k] &&
+        hipStreamCreateWithFlags(&g->aux[k], hipStreamNonBlocking) != hipSuccess) {
+        g->aux[k] = nullptr;
+        return nullptr;
+    }
+    return g->aux[k];
 }
 
 int srtp_gpu_mark_wait(srtp_gpu_t *g, int slot)

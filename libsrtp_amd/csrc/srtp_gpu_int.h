@@ -34,6 +34,7 @@ struct srtp_gpu {
     uint32_t *d_undo;
     size_t undo_cap;
     hipEvent_t marks[SRTP_GPU_MARKS];   // srtp_gpu_mark / _mark_wait
+    hipStream_t aux[2];                 // srtp_gpu_aux_stream: copy streams
 };
 
 // The order-free protect pre-pass's classification done by k_icm_hmac

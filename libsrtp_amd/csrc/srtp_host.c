@@ -2689,6 +2689,147 @@ static int batch_device_fast(srtp_t ctx, int unprotect, size_t n,
     return 1;
 }
 
+/* Large host-buffer batches: STAGE_CHUNKS consecutive device batches (the
+ * reference's sequential semantics: chunk c's pre-pass runs on the state
+ * chunk c-1 committed) with the copies on two copy streams, so that the
+ * host threads gather chunk c+1 and scatter chunk c-1 while chunk c+1
+ * goes to HBM and chunk c comes back (PCIe both ways at once).  *done
+ * receives the packets completed, a prefix of whole chunks; when a chunk
+ * is declined by the device pre-pass the pipeline drains and the caller
+ * runs the rest on the host path.  Returns 1 when all n are done, 0
+ * otherwise (see *done), -1 on a device error. */
+#define PIPE_MIN (1u << 17)
+static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
+                                  const uint8_t *const *in,
+                                  const size_t *in_len, uint8_t *const *out,
+                                  size_t *out_len, const size_t *mki_index,
+                                  srtp_err_status_t *status, size_t *done)
+{
+    *done = 0;
+    const size_t extra = unprotect ? 0 : SRTP_MAX_TRAILER_LEN;
+    size_t arena = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (in_len[i] > 0xffff || out_len[i] > 0xffffffffu)
+            return 0;
+        arena += r16(in_len[i] + extra);
+    }
+    void *cin = srtp_gpu_aux_stream(ctx->gpu, 0);
+    void *cout = srtp_gpu_aux_stream(ctx->gpu, 1);
+    if (!cin || !cout)
+        return 0;
+    if (async_drain(ctx) || stage_reserve(ctx, n, arena))
+        return -1;
+    stage_t *sg = &ctx->st;
+    size_t off = 0;
+    for (size_t i = 0; i < n; i++) {
+        sg->h_off[i] = off;
+        sg->h_len[i] = (uint32_t)in_len[i];
+        sg->h_cap[i] = (uint32_t)out_len[i];
+        off += r16(in_len[i] + extra);
+    }
+    gather_t g = { sg, in, in_len, out, out_len, status, extra };
+    void *hs = HS(ctx);
+    const size_t nck = STAGE_CHUNKS;
+    size_t lo[STAGE_CHUNKS + 1];
+    for (size_t c = 0; c <= nck; c++)
+        lo[c] = n * c / nck;
+#define CK_B0(c) (sg->h_off[lo[c]])
+#define CK_B1(c) (lo[(c) + 1] < n ? sg->h_off[lo[(c) + 1]] : off)
+    /* marks: 0..7 chunk c in HBM, 8..15 chunk c back in host memory */
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, cin) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_len, sg->h_len, n * 4, cin) ||
+        srtp_gpu_h2d(ctx->gpu, sg->d_cap, sg->h_cap, n * 4, cin))
+        return -1;
+    par_for_range(lo[0], lo[1], gather_part, &g);
+    if (srtp_gpu_h2d(ctx->gpu, sg->d_arena + CK_B0(0), sg->h_arena + CK_B0(0),
+                     CK_B1(0) - CK_B0(0), cin) ||
+        srtp_gpu_mark(ctx->gpu, 0, cin))
+        return -1;
+    int rc = 1;
+    size_t c = 0;
+    for (; c < nck; c++) {
+        if (c + 1 < nck) {
+            par_for_range(lo[c + 1], lo[c + 2], gather_part, &g);
+            if (srtp_gpu_h2d(ctx->gpu, sg->d_arena + CK_B0(c + 1),
+                             sg->h_arena + CK_B0(c + 1),
+                             CK_B1(c + 1) - CK_B0(c + 1), cin) ||
+                srtp_gpu_mark(ctx->gpu, (int)c + 1, cin))
+                return -1;
+        }
+        const size_t a = lo[c], k = lo[c + 1] - lo[c];
+        srtp_device_batch_t b;
+        memset(&b, 0, sizeof b);
+        b.n = k;
+        b.in = sg->d_arena;
+        b.in_off = sg->d_off + a;
+        b.in_len = sg->d_len + a;
+        b.out = sg->d_arena;
+        b.out_off = sg->d_off + a;
+        b.out_len = sg->d_cap + a;
+        b.status = sg->d_st + a;
+        b.stream = hs;
+        if (srtp_gpu_mark_stream_wait(ctx->gpu, hs, (int)c))
+            return -1;
+        const int fast = unprotect
+            ? unprotect_device_fast(ctx, &b)
+            : protect_device_fast(ctx, &b, 0, mki_index ? mki_index + a : NULL);
+        if (fast < 0)
+            return -1;
+        if (!fast) {
+            rc = 0;
+            break;
+        }
+        ctx->dt.fast_batches++;
+        /* chunk c is complete on the compute stream (the synchronous
+         * pre-pass waited for it): back to host memory on the other copy
+         * stream */
+        if (srtp_gpu_d2h(ctx->gpu, sg->h_cap + a, sg->d_cap + a, k * 4, cout) ||
+            srtp_gpu_d2h(ctx->gpu, sg->h_st + a, sg->d_st + a, k * 4, cout) ||
+            srtp_gpu_d2h(ctx->gpu, sg->h_arena + CK_B0(c),
+                         sg->d_arena + CK_B0(c), CK_B1(c) - CK_B0(c), cout) ||
+            srtp_gpu_mark(ctx->gpu, 8 + (int)c, cout))
+            return -1;
+        if (c > 0) {
+            if (srtp_gpu_mark_wait(ctx->gpu, 8 + (int)c - 1))
+                return -1;
+            par_for_range(lo[c - 1], lo[c], scatter_part, &g);
+        }
+    }
+    /* the last chunk that went through (c - 1), and whatever copy is still
+     * in flight before the staging buffers are used again */
+    if (c > 0) {
+        if (srtp_gpu_mark_wait(ctx->gpu, 8 + (int)c - 1))
+            return -1;
+        par_for_range(lo[c - 1], lo[c], scatter_part, &g);
+    }
+    if (srtp_gpu_sync(ctx->gpu, cin) || srtp_gpu_sync(ctx->gpu, cout))
+        return -1;
+    for (size_t i = 0; i < lo[c]; i++)
+        status[i] = (srtp_err_status_t)sg->h_st[i];
+    *done = lo[c];
+#undef CK_B0
+#undef CK_B1
+    return rc;
+}
+
+/* the device paths of a host-buffer batch: pipelined chunks for large ones */
+static int batch_device_run(srtp_t ctx, int unprotect, size_t n,
+                            const uint8_t *const *in, const size_t *in_len,
+                            uint8_t *const *out, size_t *out_len,
+                            const size_t *mki_index,
+                            srtp_err_status_t *status, size_t *done)
+{
+    *done = 0;
+    if (n >= PIPE_MIN && n <= 0x7fffffffu)
+        return batch_device_pipelined(ctx, unprotect, n, in, in_len, out,
+                                      out_len, mki_index, status, done);
+    const int fast = batch_device_fast(ctx, unprotect, n, in, in_len, out,
+                                       out_len, mki_index, status);
+    if (fast > 0)
+        *done = n;
+    return fast;
+}
+
 srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
                                      const uint8_t *const *rtp,
                                      const size_t *rtp_len,
@@ -2704,14 +2845,24 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
     {
         /* MKI: one mki_index for the whole batch runs on the device
          * (protect_device_fast, dev_mki_select) */
-        int fast = batch_device_fast(ctx, 0, n, rtp, rtp_len, srtp, srtp_len,
-                                     mki_index, status);
+        size_t done = 0;
+        int fast = batch_device_run(ctx, 0, n, rtp, rtp_len, srtp, srtp_len,
+                                    mki_index, status, &done);
         if (fast < 0) {
             log_msg(srtp_log_level_error, srtp_gpu_last_error());
             return srtp_err_status_fail;
         }
         if (fast)
             return srtp_err_status_ok;
+        /* a declined chunk: the rest on the host path */
+        n -= done;
+        rtp += done;
+        rtp_len += done;
+        srtp += done;
+        srtp_len += done;
+        status += done;
+        if (mki_index)
+            mki_index += done;
     }
     dev_pull(ctx);
     size_t arena = 0;
@@ -2965,14 +3116,22 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
     ASYNC_DRAIN_CHECK(ctx);
     if (!n)
         return srtp_err_status_ok;
-    int fast = batch_device_fast(ctx, 1, n, srtp, srtp_len, rtp, rtp_len, NULL,
-                                 status);
+    size_t done = 0;
+    int fast = batch_device_run(ctx, 1, n, srtp, srtp_len, rtp, rtp_len, NULL,
+                                status, &done);
     if (fast < 0) {
         log_msg(srtp_log_level_error, srtp_gpu_last_error());
         return srtp_err_status_fail;
     }
     if (fast)
         return srtp_err_status_ok;
+    /* a declined chunk: the rest on the host path */
+    n -= done;
+    srtp += done;
+    srtp_len += done;
+    rtp += done;
+    rtp_len += done;
+    status += done;
     dev_pull(ctx);
     size_t arena = 0;
     for (size_t i = 0; i < n; i++)

@@ -910,3 +910,46 @@ def test_fused_paths_ineligible_stream_of_another_variant():
                 _receive_check(lib, orc, rx)
         d, h = lib.prepass_stats()
         assert h >= 1, (op, d, h)
+
+
+@pytest.mark.parametrize("declined", [False, True], ids=["clean", "declined"])
+def test_large_host_batch_pipelined_chunks(declined):
+    """srtp_protect_batch / srtp_unprotect_batch over 2^18 host packets run
+    as 8 consecutive device batches with the copies overlapped
+    (srtp_host.c batch_device_pipelined); "declined": a duplicate inside
+    the fifth chunk sends that chunk and the rest to the host path.  Every
+    status and byte against the oracle, both directions."""
+    _gpu()
+    rng = random.Random(617 + declined)
+    ssrcs = [0x27000000 + k for k in range(4)]
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
+    n = 1 << 18
+    pk = []
+    for i in range(n):
+        s = ssrcs[i % 4]
+        pk.append(rtp_packet(rng, s, seq0[s] & 0xffff, rng.randrange(0, 40)))
+        seq0[s] += 1
+    if declined:
+        j = 5 * n // 8 - 100
+        pk[j + 40] = pk[j]          # a replay inside chunk 4
+    lib, orc = L.Session(pols), O.Session(pols)
+    caps = [len(p) + 16 for p in pk]
+    st, out = lib.protect_batch(pk, caps)
+    sent = []
+    for i, p in enumerate(pk):
+        rc, ref = orc.protect(p, caps[i])
+        assert st[i] == rc, (i, st[i], rc)
+        assert rc or out[i] == ref, i
+        if rc == 0:
+            sent.append(ref)
+    # device batches: every chunk, or the four before the declined one
+    # (host-buffer batches that fall back are not counted as host batches)
+    assert lib.prepass_stats() == ((4 if declined else 8), 0)
+    rlib, rorc = L.Session(pols), O.Session(pols)
+    st, out = rlib.unprotect_batch(sent)
+    for i, p in enumerate(sent):
+        rc, ref = rorc.unprotect(p, len(p))
+        assert st[i] == rc, ("rx", i, st[i], rc)
+        assert rc or out[i] == ref, ("rx", i)
+    assert rlib.prepass_stats() == (8, 0)
