@@ -2539,20 +2539,22 @@ static void par_for_range(size_t lo, size_t hi,
                           void (*fn)(void *, size_t, size_t), void *arg);
 #define STAGE_CHUNKS 8   /* < SRTP_GPU_MARKS */
 
-/* fn over [lo, hi) on up to 8 host threads */
+/* fn over [lo, hi) on up to PAR_THREADS host threads (the GPU box grants
+ * 16 CPUs per GPU) */
+#define PAR_THREADS 16
 static void par_for_range(size_t lo0, size_t hi0,
                           void (*fn)(void *, size_t, size_t), void *arg)
 {
     const size_t n = hi0 - lo0;
     size_t t = n / 16384;
-    if (t > 8)
-        t = 8;
+    if (t > PAR_THREADS)
+        t = PAR_THREADS;
     if (t < 2) {
         fn(arg, lo0, hi0);
         return;
     }
-    pthread_t th[8];
-    par_job_t jobs[8];
+    pthread_t th[PAR_THREADS];
+    par_job_t jobs[PAR_THREADS];
     size_t started = 0;
     for (size_t k = 0; k < t; k++) {
         jobs[k].fn = fn;
