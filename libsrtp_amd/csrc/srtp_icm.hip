@@ -790,7 +790,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                     // [len, len + trailer), so no read leaves the pages the
                     // packet's buffer is in), then a byte-aligned extract
                     u32x4 w;
-                    fz_tail_save(A.out + A.out_off[i] + len,
+                    fz_tail_save(A.out + off + len,   // in place: out_off = in_off
                                  z.trailer < 16 ? z.trailer : 16, w);
                     *(u32x4 *)F.tsave[i] = w;
 #endif
@@ -975,15 +975,19 @@ void k_icm_hmac(IcmArgs A)
                 if constexpr (PROTECT) {
                     const srtp_dev_meta_t m =
                         fz_classify(A, i, z, icm_vid<NR, AUTH>());
+                    // fused batches are in place (fused_ok): one offset
+                    const uint64_t off = A.in_off[i];
                     icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                        A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+                        A, m, off, off, i, A.uni, T, rk);
                 } else {
                     uint64_t e;
                     uint32_t sid;
                     const srtp_dev_meta_t m =
                         fzu_classify(A, i, z, icm_vid<NR, AUTH>(), e, sid);
+                    // fused batches are in place (fused_ok): one offset
+                    const uint64_t off = A.in_off[i];
                     icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                        A, m, A.in_off[i], A.out_off[i], i, A.uni, T, rk);
+                        A, m, off, off, i, A.uni, T, rk);
                     fzu_verdict(A, i, z, m, e, sid);
                 }
             }
