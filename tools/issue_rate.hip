@@ -68,8 +68,35 @@ __device__ __forceinline__ void body(uint32_t &a0, uint32_t &a1, uint32_t &a2,
     }
 }
 
+// overlap probe (round 4): LDS-only, VALU-only and both, in one wave or in
+// different waves of a SIMD -- does an LDS read stream overlap a VALU
+// stream, or do the two add up?
+#define LDS8(a, b)                                                              \
+    asm volatile("ds_read_b32 %0, %8\n ds_read_b32 %1, %8 offset:4096\n"       \
+                 "ds_read_b32 %2, %8 offset:8192\n ds_read_b32 %3, %8 offset:12288\n" \
+                 "ds_read_b32 %4, %8 offset:16384\n ds_read_b32 %5, %8 offset:20480\n" \
+                 "ds_read_b32 %6, %8 offset:24576\n ds_read_b32 %7, %8 offset:28672\n" \
+                 "s_waitcnt lgkmcnt(0)"                                         \
+                 : "=&v"(b[0]), "=&v"(b[1]), "=&v"(b[2]), "=&v"(b[3]),          \
+                   "=&v"(b[4]), "=&v"(b[5]), "=&v"(b[6]), "=&v"(b[7])           \
+                 : "v"(a))
+template <int K>
+__device__ __forceinline__ void body2(uint32_t &a0, uint32_t &a1, uint32_t &a2,
+                                      uint32_t &a3, uint32_t &a4, uint32_t &a5,
+                                      uint32_t &a6, uint32_t &a7, uint32_t addr)
+{
+    uint32_t b[8];
+    const bool lw = (threadIdx.x >> 6) & 1;   // K == 11: odd waves read LDS
+    if (K == 8 || K == 10 || (K == 11 && lw)) {
+        LDS8(addr, b);
+        a0 ^= b[0] + b[1] + b[2] + b[3] + b[4] + b[5] + b[6] + b[7];
+    }
+    if (K == 9 || K == 10 || (K == 11 && !lw))
+        body<2>(a0, a1, a2, a3, a4, a5, a6, a7, 0, 0, 0);
+}
+
 // instructions per body() call
-static const int NI[] = { 8, 8, 8, 8, 8, 8, 8, 20 };
+static const int NI[] = { 8, 8, 8, 8, 8, 8, 8, 20, 8, 8, 16, 8 };
 static const char *NAMES[] = { "v_xor_b32 (2 src, fixed x)",
                                "v_bitop3 (3 src, 2 fixed)",
                                "v_bitop3 (3 src, all changing)",
@@ -77,7 +104,11 @@ static const char *NAMES[] = { "v_xor_b32 (2 src, fixed x)",
                                "v_xor_b32 (2 src, changing)",
                                "v_alignbit rotate",
                                "v_add3 (changing)",
-                               "AES-like mix (12 VALU + 4 ds_read_b32 + 4 VALU)" };
+                               "AES-like mix (12 VALU + 4 ds_read_b32 + 4 VALU)",
+                               "LDS only: 8 ds_read_b32 (+8 VALU to consume)",
+                               "VALU only: 8 v_bitop3",
+                               "both in every wave: 8 LDS + 8+8 VALU",
+                               "odd waves LDS (+8 VALU), even waves VALU" };
 
 template <int K>
 __global__ __launch_bounds__(1024) void k_rate(uint32_t *out, int iters,
@@ -91,11 +122,17 @@ __global__ __launch_bounds__(1024) void k_rate(uint32_t *out, int iters,
              a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
     uint32_t x = blockIdx.x | 0x10203, y = 0x0c0c0504u;
     uint32_t lds = (uint32_t)(uintptr_t)s;
+    // K >= 8: lane l reads copy l & 31 of a 128-B row (the T-table layout)
+    const uint32_t addr = lds + ((threadIdx.x * 2654435761u >> 24) & 31) * 128 +
+                          (threadIdx.x & 31) * 4;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     for (int i = 0; i < iters; i++) {
 #pragma unroll
         for (int r = 0; r < 8; r++)
-            body<K>(a0, a1, a2, a3, a4, a5, a6, a7, x, y, lds);
+            if constexpr (K >= 8)
+                body2<K>(a0, a1, a2, a3, a4, a5, a6, a7, addr);
+            else
+                body<K>(a0, a1, a2, a3, a4, a5, a6, a7, x, y, lds);
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * blockDim.x + threadIdx.x] =
@@ -129,8 +166,8 @@ static void one(uint32_t *out, uint64_t *clk, int threads)
     const int wps = threads / 256;   // waves per SIMD
     const double ni = (double)wps * iters * 8 * NI[K];
     printf("%-48s %d waves/SIMD: %.3f ns per wave-instruction per SIMD "
-           "(wall), %.2f s_memtime ticks\n", NAMES[K], wps, ms * 1e6 / ni,
-           m / ni);
+           "(wall), %.2f s_memtime ticks, %.3f ms\n", NAMES[K], wps,
+           ms * 1e6 / ni, m / ni, ms);
 }
 
 template <int K>
@@ -155,5 +192,9 @@ int main()
     both<5>(out, clk);
     both<6>(out, clk);
     both<7>(out, clk);
+    both<8>(out, clk);
+    both<9>(out, clk);
+    both<10>(out, clk);
+    both<11>(out, clk);
     return 0;
 }
