@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 
 // T-table form: T0..T3 (Te tables, LE words), 32 copies, lane reads copy
 // lane & 31; one v_perm per lookup address
-__global__ __launch_bounds__(256) void k_tt(const uint32_t *iv, const uint32_t *rkw,
+__global__ __launch_bounds__(512) void k_tt(const uint32_t *iv, const uint32_t *rkw,
                                              const uint32_t *te, uint32_t *ks,
                                              uint32_t *acc_out, uint32_t n, int store)
 {
@@ -412,7 +412,7 @@ int main(int argc, char **argv)
         if (kern == 0)
             hipLaunchKernelGGL(k_bs, dim3(nchk / 256), dim3(256), 0, 0, d_iv, d_km, d_ks, d_acc, nchk, 1);
         else
-            hipLaunchKernelGGL(k_tt, dim3(nchk / 256), dim3(256), 0, 0, d_iv, d_rk, d_te, d_ks, d_acc, nchk, 1);
+            hipLaunchKernelGGL(k_tt, dim3(nchk / 512), dim3(512), 0, 0, d_iv, d_rk, d_te, d_ks, d_acc, nchk, 1);
         if (hipDeviceSynchronize() != hipSuccess) {
             printf("kernel %d failed\n", kern);
             return 1;
@@ -442,7 +442,7 @@ int main(int argc, char **argv)
             if (kern == 0)
                 hipLaunchKernelGGL(k_bs, dim3(n / 256), dim3(256), 0, 0, d_iv, d_km, d_ks, d_acc, n, 0);
             else
-                hipLaunchKernelGGL(k_tt, dim3(n / 256), dim3(256), 0, 0, d_iv, d_rk, d_te, d_ks, d_acc, n, 0);
+                hipLaunchKernelGGL(k_tt, dim3(n / 512), dim3(512), 0, 0, d_iv, d_rk, d_te, d_ks, d_acc, n, 0);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms;
