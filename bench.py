@@ -45,9 +45,9 @@ max over ranks, the one JSON line) over gloo on the CPU with a stub step
 
 Extra fields: roofline (dominant kernel, HIP-event timed on the stream the
 kernels ran on; `traffic` = FETCH_SIZE + WRITE_SIZE per launch from
-separate rocprofv3 PMC passes, `traffic_shape` = those counters against a
-byte-exact copy of the kernel's access shape, `issue` = VALU / LDS
-instruction floors), cpu_baseline (the reference, cisco/libsrtp built from
+separate rocprofv3 PMC passes, `traffic_over_algorithmic` = that over the
+algorithmic bytes, `issue` = VALU / LDS instruction floors, `additive_frac`
+their sum over the launch), cpu_baseline (the reference, cisco/libsrtp built from
 its own sources, srtp_protect() per packet on host threads, rank 0 only).
 """
 import argparse
@@ -75,11 +75,18 @@ CONFIGS = {
              1 << 23, 10),
 }
 WORKLOAD = {
-    "icm128": "AES-128-ICM + HMAC-SHA1-80 protect, 1M packets x 1400B, 1 stream",
-    "gcm256": "AES-256-GCM-16 protect, 1M packets x 1400B per GPU, 1 stream",
-    "g711": "AES-128-ICM + HMAC-SHA1-80 protect, 8M packets x 160B, "
+    "icm128": "AES-128-ICM + HMAC-SHA1-80 {op}, 1M packets x 1400B, 1 stream",
+    "gcm256": "AES-256-GCM-16 {op}, 1M packets x 1400B per GPU, 1 stream",
+    "g711": "AES-128-ICM + HMAC-SHA1-80 {op}, 8M packets x 160B, "
             "64k SSRC streams (distinct keys, round-robin)",
 }
+
+
+def workload(a):
+    """config.workload: the configuration and the operation timed"""
+    return WORKLOAD[a.config].format(op=a.op)
+
+
 # master key: test/srtp_driver.c test_key (46 bytes) -- any key works
 TEST_KEY = ("e1f97a0d3e018be0d64fa32c06de41390ec675ad498afeebb6960b3aabe6"
             "c173c317f2dabe357793b6960b3aabe6")
@@ -172,38 +179,18 @@ DIST_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
              "SRTP_FORCE_DIST")
 
 
-# FETCH_SIZE / WRITE_SIZE of a byte-exact copy in the kernel's own access
-# shape, per byte moved (tools/fetch_cal.hip on MI355X, profiles/r04/fcal,
-# profiles/r04_fetch_calibration.md): read-only streams count 0.50-0.70 of
-# their bytes (the guide's 1/2 for 128-B requests), copies 0.83-1.95 of the
-# reads and 1.03-2.82 of the writes depending on the shape.
-SHAPE_CAL = {
-    # in-place lane quads, 64-B-aligned stores (k_icm_hmac, uniform key)
-    "lane_quad_inplace": (0.833, 1.134),
-    # in-place, every lane its own packet, 16-B pieces (k_gcm; k_icm_hmac
-    # with per-lane keys)
-    "lane_inplace": (1.954, 2.822),
-}
-KERNEL_SHAPE = {"icm128": "lane_quad_inplace", "gcm256": "lane_inplace",
-                "g711": "lane_inplace"}
-
-
-def traffic_shape(a, n, rtp_len, tag, pmc):
-    """the counters against what a byte-exact copy of the same shape and
-    size shows: `ratio` near 1 means the kernel moves no more than its
-    access shape forces; raw FETCH_SIZE is not corrected by one global
-    factor because the calibration shows none fits every shape"""
+def traffic_split(a, n, rtp_len, tag, pmc):
+    """FETCH_SIZE and WRITE_SIZE per launch as counted, each against the
+    algorithmic bytes of its direction (profiles/r04_fetch_calibration.md
+    measures what a byte-exact copy of each access shape counts: 16-B
+    per-lane pieces count up to 2-2.8x their bytes)"""
     if "FETCH_SIZE" not in pmc or "WRITE_SIZE" not in pmc:
         return None
-    shape = KERNEL_SHAPE[a.config]
-    fr, fw = SHAPE_CAL[shape]
     rd = n * (rtp_len + (tag if a.op == "unprotect" else 0))
     wr = n * (rtp_len + (0 if a.op == "unprotect" else tag))
-    base = fr * rd + fw * wr
     f, w = pmc["FETCH_SIZE"] * 1024.0, pmc["WRITE_SIZE"] * 1024.0
-    return {"shape": shape, "fetch": f, "write": w,
-            "fetch_over_shape": f / (fr * rd), "write_over_shape": w / (fw * wr),
-            "shape_baseline": base, "ratio": (f + w) / base}
+    return {"fetch": f, "write": w, "fetch_over_read_bytes": f / rd,
+            "write_over_written_bytes": w / wr}
 
 
 def measure_pmc(a, kname, device=0):
@@ -211,8 +198,7 @@ def measure_pmc(a, kname, device=0):
     this same workload, one rocprofv3 --pmc pass per entry of PMC_PASSES,
     each a child process started before this process touches the GPU.
     FETCH_SIZE is TCC_EA0_RDREQ x 64 B.  `traffic` is FETCH_SIZE +
-    WRITE_SIZE as counted; traffic_shape() sets it against the calibrated
-    counts of a byte-exact copy in the kernel's access shape (SHAPE_CAL)."""
+    WRITE_SIZE as counted (traffic_split() per direction)."""
     import glob
     import shutil
     import subprocess
@@ -272,9 +258,15 @@ def issue_roofline(pmc, kernel_ms):
         return None
     fv = v * VALU_NS_PER_SIMD / SIMDS * 1e-6      # ms
     fl = l * LDS_NS_PER_CU / CUS * 1e-6
+    # profiles/r04_icm_wavespec.md §6: an LDS read stream and a VALU stream
+    # on one SIMD add up almost linearly, so the floor the kernel can reach
+    # is their SUM (additive_frac, the headline); max_frac (the larger floor
+    # alone) is kept as a secondary figure
     return {"bound": "valu+lds issue", "valu_insts": v, "lds_insts": l,
             "valu_floor_ms": fv, "lds_floor_ms": fl,
-            "frac": max(fv, fl) / kernel_ms,
+            "additive_frac": (fv + fl) / kernel_ms,
+            "frac": (fv + fl) / kernel_ms,
+            "max_frac": max(fv, fl) / kernel_ms,
             "valu_ns_per_simd": VALU_NS_PER_SIMD,
             "lds_ns_per_cu": LDS_NS_PER_CU}
 
@@ -646,7 +638,7 @@ def result_line(a, world, n, payload, tag, dt, roofline, cpu, prepass):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (random payloads, seq advanced per step)",
-        "config": {"workload": WORKLOAD[a.config], "packets_per_gpu": n,
+        "config": {"workload": workload(a), "packets_per_gpu": n,
                    "packets_total": n * world,
                    "streams_per_gpu": STREAMS[a.config],
                    "payload_bytes": payload, "rtp_bytes": rtp_len,
@@ -884,7 +876,9 @@ def run_gpu(a, world, rank, local, json_out):
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
-                "traffic_shape": traffic_shape(a, n, rtp_len, tag, pmc),
+                "traffic_over_algorithmic":
+                    traffic / algo_bytes if traffic else None,
+                "traffic_split": traffic_split(a, n, rtp_len, tag, pmc),
                 "kernel": kname, "kernel_ms": kernel_ms,
                 "algorithmic_bytes_per_launch": algo_bytes,
                 "issue": issue_roofline(pmc, kernel_ms)}

@@ -349,6 +349,8 @@ int srtp_gpu_h2d(srtp_gpu_t *g, void *dst, const void *src, size_t n,
 int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
                  void *stream);
 int srtp_gpu_sync(srtp_gpu_t *g, void *stream);
+/* n bytes at dst (device) set to v, stream-ordered */
+int srtp_gpu_memset(void *dst, int v, size_t n, void *stream);
 /* a marker on `stream` after the work queued so far (slot < SRTP_GPU_MARKS),
  * and a host wait for it */
 #define SRTP_GPU_MARKS 16

@@ -1612,6 +1612,14 @@ int srtp_gpu_d2h(srtp_gpu_t *g, void *dst, const void *src, size_t n,
     return 0;
 }
 
+int srtp_gpu_memset(void *dst, int v, size_t n, void *stream)
+{
+    if (!n)
+        return 0;
+    HIPCHK(hipMemsetAsync(dst, v, n, (hipStream_t)stream));
+    return 0;
+}
+
 int srtp_gpu_sync(srtp_gpu_t *g, void *stream)
 {
     hipStream_t st = (hipStream_t)stream;   // NULL = the null stream

@@ -2720,7 +2720,7 @@ static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
     if (!cin || !cout)
         return 0;
     if (async_drain(ctx) || stage_reserve(ctx, n, arena))
-        return -1;
+        goto fail;
     stage_t *sg = &ctx->st;
     size_t off = 0;
     for (size_t i = 0; i < n; i++) {
@@ -2741,12 +2741,12 @@ static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
     if (srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, cin) ||
         srtp_gpu_h2d(ctx->gpu, sg->d_len, sg->h_len, n * 4, cin) ||
         srtp_gpu_h2d(ctx->gpu, sg->d_cap, sg->h_cap, n * 4, cin))
-        return -1;
+        goto fail;
     par_for_range(lo[0], lo[1], gather_part, &g);
     if (srtp_gpu_h2d(ctx->gpu, sg->d_arena + CK_B0(0), sg->h_arena + CK_B0(0),
                      CK_B1(0) - CK_B0(0), cin) ||
         srtp_gpu_mark(ctx->gpu, 0, cin))
-        return -1;
+        goto fail;
     int rc = 1;
     size_t c = 0;
     for (; c < nck; c++) {
@@ -2756,7 +2756,7 @@ static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
                              sg->h_arena + CK_B0(c + 1),
                              CK_B1(c + 1) - CK_B0(c + 1), cin) ||
                 srtp_gpu_mark(ctx->gpu, (int)c + 1, cin))
-                return -1;
+                goto fail;
         }
         const size_t a = lo[c], k = lo[c + 1] - lo[c];
         srtp_device_batch_t b;
@@ -2771,12 +2771,12 @@ static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
         b.status = sg->d_st + a;
         b.stream = hs;
         if (srtp_gpu_mark_stream_wait(ctx->gpu, hs, (int)c))
-            return -1;
+            goto fail;
         const int fast = unprotect
             ? unprotect_device_fast(ctx, &b)
             : protect_device_fast(ctx, &b, 0, mki_index ? mki_index + a : NULL);
         if (fast < 0)
-            return -1;
+            goto fail;
         if (!fast) {
             rc = 0;
             break;
@@ -2790,10 +2790,10 @@ static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
             srtp_gpu_d2h(ctx->gpu, sg->h_arena + CK_B0(c),
                          sg->d_arena + CK_B0(c), CK_B1(c) - CK_B0(c), cout) ||
             srtp_gpu_mark(ctx->gpu, 8 + (int)c, cout))
-            return -1;
+            goto fail;
         if (c > 0) {
             if (srtp_gpu_mark_wait(ctx->gpu, 8 + (int)c - 1))
-                return -1;
+                goto fail;
             par_for_range(lo[c - 1], lo[c], scatter_part, &g);
         }
     }
@@ -2801,17 +2801,24 @@ static int batch_device_pipelined(srtp_t ctx, int unprotect, size_t n,
      * in flight before the staging buffers are used again */
     if (c > 0) {
         if (srtp_gpu_mark_wait(ctx->gpu, 8 + (int)c - 1))
-            return -1;
+            goto fail;
         par_for_range(lo[c - 1], lo[c], scatter_part, &g);
     }
     if (srtp_gpu_sync(ctx->gpu, cin) || srtp_gpu_sync(ctx->gpu, cout))
-        return -1;
+        goto fail;
     for (size_t i = 0; i < lo[c]; i++)
         status[i] = (srtp_err_status_t)sg->h_st[i];
     *done = lo[c];
 #undef CK_B0
 #undef CK_B1
     return rc;
+fail:
+    /* no copy on either copy stream, nor a kernel reading the staging
+     * arena, may outlive the call: the next batch reuses the buffers */
+    (void)srtp_gpu_sync(ctx->gpu, cin);
+    (void)srtp_gpu_sync(ctx->gpu, cout);
+    (void)srtp_gpu_sync(ctx->gpu, HS(ctx));
+    return -1;
 }
 
 /* the device paths of a host-buffer batch: pipelined chunks for large ones */
@@ -4921,11 +4928,17 @@ srtp_err_status_t srtp_mi355x_session_import(srtp_t *session, const void *blob,
     return srtp_err_status_ok;
 }
 
-/* RCCL, resolved at run time: whatever the process already links (the
- * caller's communicator must come from that library), else librccl.so.1 */
+/* RCCL, resolved at run time from a copy the process has ALREADY loaded --
+ * the one the caller's communicator comes from (PyTorch's bundled
+ * librccl.so, soname librccl.so.1, is loaded privately, so RTLD_DEFAULT does
+ * not see it; RTLD_NOLOAD finds it by soname).  A fresh dlopen would be a
+ * second library instance, possibly another version, handed a communicator
+ * it did not create: no such load is made, the call fails instead. */
 
 typedef int (*rccl_bcast_fn)(const void *, void *, size_t, int, int, void *,
                              void *);
+typedef int (*rccl_allred_fn)(const void *, void *, size_t, int, int, void *,
+                              void *);
 typedef int (*rccl_rank_fn)(void *, int *);
 typedef const char *(*rccl_err_fn)(int);
 
@@ -4934,48 +4947,59 @@ static void *rccl_sym(const char *name)
     void *f = dlsym(RTLD_DEFAULT, name);
     if (f)
         return f;
-    /* a copy already loaded privately (PyTorch's bundled librccl.so, the
-     * one its communicators come from), else ROCm's */
-    static void *h;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
     if (!h)
         h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
     if (!h)
-        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h)
-        h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-    return h ? dlsym(h, name) : NULL;
+        return NULL;
+    f = dlsym(h, name);
+    dlclose(h);   /* drops the reference NOLOAD took; the library stays */
+    return f;
 }
 
+/* Every step below is collective: each rank makes the same sequence of
+ * calls whatever happens locally, so no rank is left waiting in RCCL.
+ *   1. the root exports; the blob length is broadcast (0: export failed,
+ *      every rank returns srtp_err_status_fail);
+ *   2. every rank allocates; a max-reduction of the failure flags makes
+ *      every rank return srtp_err_status_alloc_fail if any failed;
+ *   3. the blob is broadcast, the other ranks import it.
+ * Secrets (derived keys, HMAC midstates, salts) are wiped from the host
+ * and device copies of the blob on every exit path. */
 srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
                                                 void *nccl_comm, int root,
                                                 void *stream)
 {
-    enum { NCCL_UINT8 = 1 }; /* rccl.h ncclDataType_t ncclUint8 */
+    /* rccl.h: ncclUint8 = 1, ncclUint64 = 5, ncclMax = 2 */
+    enum { NCCL_UINT8 = 1, NCCL_UINT64 = 5, NCCL_MAX = 2 };
     if (!session || !nccl_comm)
         return srtp_err_status_bad_param;
     rccl_bcast_fn bcast = (rccl_bcast_fn)rccl_sym("ncclBroadcast");
+    rccl_allred_fn allred = (rccl_allred_fn)rccl_sym("ncclAllReduce");
     rccl_rank_fn urank = (rccl_rank_fn)rccl_sym("ncclCommUserRank");
     rccl_err_fn estr = (rccl_err_fn)rccl_sym("ncclGetErrorString");
-    if (!bcast || !urank) {
-        log_msg(srtp_log_level_error, "session broadcast: RCCL not found\n");
+    if (!bcast || !allred || !urank) {
+        log_msg(srtp_log_level_error,
+                "session broadcast: no RCCL loaded in this process\n");
         return srtp_err_status_init_fail;
     }
     int rank = -1;
     if (urank(nccl_comm, &rank))
         return srtp_err_status_bad_param;
     const int is_root = rank == root;
-    if (is_root && !*session)
-        return srtp_err_status_bad_param;
     srtp_err_status_t st = srtp_err_status_ok;
-    uint64_t hlen = 0;
+    uint64_t hlen = 0, flag;
     size_t blen = 0;   /* bytes of blob to wipe */
     uint8_t *blob = NULL, *dblob = NULL;
     uint64_t *dlen = (uint64_t *)srtp_gpu_malloc(sizeof(uint64_t));
     if (!dlen)
-        return srtp_err_status_alloc_fail;
+        return srtp_err_status_alloc_fail;   /* before any collective: the
+                                              * same as RCCL's own allocation
+                                              * failures, fatal for the comm */
     if (is_root) {
         size_t n = 0;
-        st = srtp_mi355x_session_export(*session, NULL, 0, &n);
+        st = *session ? srtp_mi355x_session_export(*session, NULL, 0, &n)
+                      : srtp_err_status_bad_param;
         blob = st ? NULL : (uint8_t *)malloc(n);
         blen = blob ? n : 0;
         if (!st && !blob)
@@ -5005,11 +5029,17 @@ srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
         blob = (uint8_t *)malloc(hlen);
         blen = blob ? hlen : 0;
     }
-    if (!dblob || !blob) {
-        /* every rank must still take part: a rank that cannot allocate
-         * leaves the others in the collective, so this is fatal for the
-         * communicator, as any RCCL allocation failure is */
-        st = srtp_err_status_alloc_fail;
+    flag = (!dblob || !blob) ? 1 : 0;
+    if (srtp_gpu_h2d(NULL, dlen, &flag, sizeof flag, stream) ||
+        (nr = allred(dlen, dlen, 1, NCCL_UINT64, NCCL_MAX, nccl_comm,
+                     stream)) ||
+        srtp_gpu_d2h(NULL, &flag, dlen, sizeof flag, stream) ||
+        srtp_gpu_sync(NULL, stream)) {
+        st = srtp_err_status_fail;
+        goto out;
+    }
+    if (flag) {
+        st = srtp_err_status_alloc_fail;   /* on some rank: all return */
         goto out;
     }
     if ((is_root && srtp_gpu_h2d(NULL, dblob, blob, hlen, stream)) ||
@@ -5024,13 +5054,19 @@ srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
 out:
     if (nr && estr) {
         char m[160];
-        snprintf(m, sizeof m, "session broadcast: ncclBroadcast: %s\n",
-                 estr(nr));
+        snprintf(m, sizeof m, "session broadcast: RCCL: %s\n", estr(nr));
         log_msg(srtp_log_level_error, m);
     }
     if (blob) {
         memset(blob, 0, blen);
         free(blob);
+    }
+    if (dblob) {
+        /* the device copy holds the same secrets: cleared before the free
+         * (stream-ordered behind any copy still reading it) */
+        if (srtp_gpu_memset(dblob, 0, hlen, stream) ||
+            srtp_gpu_sync(NULL, stream))
+            (void)srtp_gpu_sync(NULL, NULL);
     }
     srtp_gpu_free(dblob);
     srtp_gpu_free(dlen);

@@ -662,10 +662,6 @@ DEV void fz_count(const IcmFused &F, FzLane &z, uint32_t sid, bool chain,
         // their bits are merged per bitmap word before the atomic
         const uint32_t r = (uint32_t)e & z.bmask;
         const uint32_t w = z.boff + (r >> 5);
-#ifdef FZ_EXP_NO_WMERGE   // timing: one atomic per packet (round-4 s10)
-        atomicOr(&F.bmap[w], 1u << (r & 31));
-        return;
-#endif
         if (w != z.bw_idx) {
             if (z.bw_bits)
                 atomicOr(&F.bmap[z.bw_idx], z.bw_bits);
@@ -758,7 +754,12 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
         } else if (z.variant != vid) {
             ab |= FZ_AB_INELIGIBLE;
         } else {
-            if (!(z.flags & SRTP_DS_ELIGIBLE) || (z.dir & SRTP_DIR_RX))
+            // an ineligible stream of this variant (its trailer may exceed
+            // the 16 saved bytes) is neither encrypted nor recorded as done:
+            // the batch is declined, and its bytes stay as they were
+            const bool inel =
+                !(z.flags & SRTP_DS_ELIGIBLE) || (z.dir & SRTP_DIR_RX);
+            if (inel)
                 ab |= FZ_AB_INELIGIBLE;
             if (F.cap[i] < len + z.trailer) {
                 code = 28;           // srtp_err_status_buffer_small
@@ -767,7 +768,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                 code = 21;           // srtp_err_status_parse_err
                 fz_count(F, z, sid, false, 0);
             } else {
-                key = sid;
+                key = inel ? FZ_NOCHAIN : sid;
                 // aes_icm.c:317-322: at most 0xffff keystream blocks
                 if ((z.flags & SRTP_DS_ICM_CONF) &&
                     (len - h.enc_start + 15) / 16 > 0xffffu)
@@ -778,12 +779,11 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                 if (delta < 1)
                     ab |= FZ_AB_ORDER;   // the sorted path decides
                 fz_count(F, z, sid, true, e);
-                if (code == 0) {
+                if (code == 0 && !inel) {
                     m.key = z.key;
                     m.roc = (uint32_t)(e >> 16);
                     m.info = h.enc_start | (z.variant << 24);
                     m.len = len;
-#ifndef FZ_EXP_NO_TSAVE
                     // the bytes the tag overwrites (in place), for the undo:
                     // at most two loads of the 8-byte-aligned span around
                     // them (each 8-byte half read holds a byte of
@@ -793,7 +793,6 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                     fz_tail_save(A.out + off + len,   // in place: out_off = in_off
                                  z.trailer < 16 ? z.trailer : 16, w);
                     *(u32x4 *)F.tsave[i] = w;
-#endif
                 }
             }
         }
@@ -942,12 +941,6 @@ void k_icm_hmac(IcmArgs A)
         load_aes_tables<TAB4>(s_tab, s_t0);
     __syncthreads();
     const AesLds T = make_aes_lds(s_tab);
-#ifdef ICM_PRIO
-    // timing experiment: static priority for the second half of the waves
-    // (MI355X_MICROARCH.md, two waves per SIMD, item 4)
-    if ((threadIdx.x >> 6) >= (blockDim.x >> 7))
-        __builtin_amdgcn_s_setprio(1);
-#endif
 
     typename std::conditional<KM == KM_LANE, LaneKey<NRK>, UniKey<NRK>>::type rk;
     if (KM == KM_UNI && NR)

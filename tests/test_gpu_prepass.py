@@ -370,8 +370,8 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     every stream's batch spans hi - est = 127 against its 128-bit window --
     the order-free form's acceptance boundary -- and the crypto runs from
     the key buckets (one key per wave).  Two consecutive batches.  Every
-    packet of 1,024 sampled streams (131,072 per batch) is compared byte
-    for byte with the C oracle in stream order; every packet of the batch
+    packet of 978 sampled streams covering all 64 lane positions (125,184
+    per batch) is compared byte for byte with the C oracle in stream order; every packet of the batch
     must come back bit-identical through srtp_unprotect_device."""
     _gpu()
     import numpy as np
@@ -384,7 +384,12 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     pols = [policy("icm128_hmac80", ssrc=base + k, seed=k) for k in range(ns)]
     snd, rcv = L.Session(pols), L.Session(pols)
     snd.L.srtp_mi355x_set_key_buckets(buckets)
-    sample = list(range(0, ns, 64))
+    # packet i runs on lane i mod 64 of its wave and i = k * ns + s, so
+    # stream s always runs on lane s mod 64: a step of 67 samples every lane
+    # position (978 streams), each lane's cached stream record and round
+    # keys reused across its 64 packets of one stream at this shape
+    sample = list(range(0, ns, 67))
+    assert len({s % 64 for s in sample}) == 64
     orc = O.Session([pols[s] for s in sample])
     # sampled packets in stream order: stream s, its packets k = 0..per-1
     rows = torch.tensor([k * ns + s for s in sample for k in range(per)],
@@ -425,6 +430,78 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
     assert snd.prepass_sorted_batches() == 0
     snd.L.srtp_mi355x_set_key_buckets(0)
+
+
+@pytest.mark.parametrize("lengths", ["uniform160", "mixed"])
+def test_fused_midsize_every_packet_lane_reuse(lengths):
+    """The fused order-free path at a size where the persistent grid's
+    stride (256 CUs x 512 lanes = 2^17) is below the batch: 2^18 packets
+    over 2,048 distinct-key streams, round-robin, so every lane runs two
+    packets of ONE stream -- the second takes fz_lookup's cached stream
+    record and LaneKey::reload's kept round keys.  EVERY packet is compared
+    with the C oracle, protect and then unprotect, both in place; two
+    consecutive batches (the second across a ROC boundary)."""
+    _gpu()
+    import numpy as np
+    import torch
+    ns, per, tag = 2048, 128, 10
+    n = ns * per
+    slot = 320
+    base = 0x20000000
+    pols = [policy("icm128_hmac80", ssrc=base + k, seed=7000 + k)
+            for k in range(ns)]
+    snd, rcv = L.Session(pols), L.Session(pols)
+    osnd, orcv = O.Session(pols), O.Session(pols)
+    gen = torch.Generator(device="cuda").manual_seed(404)
+    off = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+    rng = np.random.default_rng(405)
+    seq0 = 0xffc0
+    for batch in range(2):
+        a = _rr_arena(ns, per, 0, seq0, base, gen, slot)
+        if lengths == "uniform160":
+            lens = np.full(n, 12 + 160, dtype=np.int64)
+        else:
+            lens = rng.integers(12, slot - tag - 16, n)
+        orig = a.clone()
+        d = a.view(-1)
+        ln = torch.from_numpy(lens.astype(np.int32)).cuda()
+        cap = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+        st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        assert snd.protect_device(d, off, ln, d, off, cap, st) == 0
+        assert int((st != 0).sum()) == 0
+        assert torch.equal(cap, ln + tag)
+        host_in = orig.cpu().numpy().reshape(-1)
+        offs = np.arange(n, dtype=np.uint64) * slot
+        bad, ref, rlen = osnd.protect_many(host_in, offs, lens, slot)
+        assert bad == 0 and (rlen == lens + tag).all()
+        got = a.cpu().numpy()
+        for i in range(0, n, 1 << 15):      # every packet, in slices
+            g = got[i:i + (1 << 15)]
+            r = ref[i:i + (1 << 15)]
+            ln_i = lens[i:i + (1 << 15)] + tag
+            mask = np.arange(slot)[None, :] < ln_i[:, None]
+            diff = np.nonzero(((g != r) & mask).any(axis=1))[0]
+            assert len(diff) == 0, ("protect mismatch", batch, i + diff[:8])
+        # receive side, in place, against the oracle's receiver
+        cap2 = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+        st2 = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        assert rcv.unprotect_device(d, off, cap.clone(), d, off, cap2, st2) == 0
+        ost, oref, olen = orcv.unprotect_many(got.reshape(-1), offs,
+                                              lens + tag, slot)
+        assert (ost == 0).all() and (olen == lens).all()
+        assert int((st2 != 0).sum()) == 0 and torch.equal(cap2, ln)
+        back = a.cpu().numpy()
+        mask = np.arange(slot)[None, :] < lens[:, None]
+        diff = np.nonzero(((back != oref) & mask).any(axis=1))[0]
+        assert len(diff) == 0, ("unprotect mismatch", batch, diff[:8])
+        assert not ((back != orig.cpu().numpy()) & mask).any()
+        del a, orig, d
+        seq0 = (seq0 + per) & 0xffff
+    assert snd.prepass_stats() == (2, 0), snd.prepass_last_abort()
+    assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
+    assert snd.prepass_sorted_batches() == 0
+    for s in (base, base + 1, base + 63, base + ns - 1):
+        assert snd.get_roc(s)[1] == osnd.get_roc(s)[1]
 
 
 # --------------------------------------------------------------------------
