@@ -455,7 +455,11 @@ def test_fused_midsize_every_packet_lane_reuse(lengths):
     gen = torch.Generator(device="cuda").manual_seed(404)
     off = torch.arange(n, dtype=torch.int64, device="cuda") * slot
     rng = np.random.default_rng(405)
-    seq0 = 0xffc0
+    # batch 1: 0xff40..0xffbf; batch 2 wraps (0xffc0..0x003f) from a stored
+    # index above 2^15 (a fresh stream's first batch must not wrap: from
+    # index 0 the reference takes seq as the index, srtp.c:2038-2071, and
+    # the packets after the wrap then go through the sorted chain form)
+    seq0 = 0xff40
     for batch in range(2):
         a = _rr_arena(ns, per, 0, seq0, base, gen, slot)
         if lengths == "uniform160":
