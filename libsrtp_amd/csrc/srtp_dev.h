@@ -283,6 +283,8 @@ typedef struct srtp_gpu_pp_batch {
     int fused_ok;           /* protect: in place, one AES-ICM kernel variant,
                                trailers <= 16 bytes: the order-free form may
                                classify inside the crypto kernel */
+    uint32_t max_trailer;   /* protect: the largest tag + MKI of the streams
+                               the device may encrypt */
 } srtp_gpu_pp_batch_t;
 
 /* pre-pass + crypto for protect.  *fallback != 0: nothing was written (no

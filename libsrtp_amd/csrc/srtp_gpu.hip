@@ -1241,6 +1241,11 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.fused = b->fused != nullptr;
     if (A.fused)
         A.fz = *(const IcmFused *)b->fused;
+    static const bool stg = [] {
+        const char *e = getenv("SRTP_ICM_STG");
+        return !(e && e[0] == '0');
+    }();
+    A.stg = stg;
     if (A.rec) {
         // key buckets: the wave-aligned groups with a key per wave, then
         // the streams with few packets with a key per lane

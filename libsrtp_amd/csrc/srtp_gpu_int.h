@@ -77,6 +77,11 @@ struct IcmFused {
     unsigned long long *hicand;
     uint32_t *bmap2;
     uint32_t *nfail;
+    // k_icm_stg: the largest trailer a protected packet of the batch gets,
+    // and the list of wave groups (64 consecutive packets) it leaves to the
+    // per-lane form: glist[0] = count, group ids from glist[1]
+    uint32_t max_trailer;
+    uint32_t *glist;
 };
 
 // AES-ICM (+ HMAC-SHA1) kernel arguments
@@ -100,6 +105,9 @@ struct IcmArgs {
     // fz valid when fused, meta then written, not read
     bool fused;
     IcmFused fz;
+    // fused batches through the LDS-staged kernel (k_icm_stg; default on,
+    // SRTP_ICM_STG=0 selects the per-lane form for A/B runs)
+    bool stg;
 };
 
 // AES-GCM kernel arguments

@@ -3551,6 +3551,7 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
                   (dt->mask & (dt->mask - 1)) == 0 &&
                   (dt->mask & 0xfc00u) == dt->mask && dt->max_trailer <= 16 &&
                   !async;
+    pb.max_trailer = dt->max_trailer;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))

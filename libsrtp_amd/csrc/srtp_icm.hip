@@ -730,13 +730,16 @@ DEV void fz_lookup(const IcmFused &F, FzLane &z, uint32_t ssrc)
 // fused_ok); a packet of another variant (only an ineligible stream can
 // have one) is not encrypted here, so it must not count as done: the
 // batch is declined without it
+// `S`: where the packet's bytes are read (GlbSrc: the arena, StgImg: the
+// wave's staged image); off / len / cap: the packet's offset, length and
+// capacity, loaded by the caller
+template <class SRC>
 DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
-                                uint32_t vid)
+                                uint32_t vid, uint64_t off, uint32_t len,
+                                uint32_t cap, const SRC &S)
 {
     const IcmFused &F = A.fz;
-    const uint64_t off = A.in_off[i];
-    const uint32_t len = F.in_len[i];
-    const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
+    const srtp_dev_hdr_t h = S.hdr(off, len);
     uint32_t code = 0, key = FZ_NOCHAIN, ab = 0;
     uint64_t e = 0;
     srtp_dev_meta_t m;
@@ -761,7 +764,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                 !(z.flags & SRTP_DS_ELIGIBLE) || (z.dir & SRTP_DIR_RX);
             if (inel)
                 ab |= FZ_AB_INELIGIBLE;
-            if (F.cap[i] < len + z.trailer) {
+            if (cap < len + z.trailer) {
                 code = 28;           // srtp_err_status_buffer_small
                 fz_count(F, z, sid, false, 0);
             } else if (h.enc_start > len) {
@@ -790,8 +793,7 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                     // [len, len + trailer), so no read leaves the pages the
                     // packet's buffer is in), then a byte-aligned extract
                     u32x4 w;
-                    fz_tail_save(A.out + off + len,   // in place: out_off = in_off
-                                 z.trailer < 16 ? z.trailer : 16, w);
+                    S.tail(len, z.trailer < 16 ? z.trailer : 16, w);
                     *(u32x4 *)F.tsave[i] = w;
                 }
             }
@@ -802,7 +804,6 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
     // written now (the commit of an accepted batch); a declined batch gets
     // its capacities back from the record and its statuses from the path
     // that then runs it
-    const uint32_t cap = F.cap[i];
     *(u32x4 *)&F.rec[i] =
         u32x4{ (uint32_t)e, (uint32_t)(e >> 32) | (code << 16), key, cap };
     F.status[i] = (int32_t)code;
@@ -822,13 +823,14 @@ DEV srtp_dev_meta_t fz_classify(const IcmArgs &A, uint32_t i, FzLane &z,
 // A candidate is decrypted and verified by icm_packet; fzu_verdict then
 // writes its status and length.  `e` / `sid` out: the candidate's index and
 // stream (sid ~0: not a candidate).
+template <class SRC>
 DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
-                                 uint32_t vid, uint64_t &e, uint32_t &sid)
+                                 uint32_t vid, uint64_t off, uint32_t len,
+                                 uint32_t cap, const SRC &S, uint64_t &e,
+                                 uint32_t &sid)
 {
     const IcmFused &F = A.fz;
-    const uint64_t off = A.in_off[i];
-    const uint32_t len = F.in_len[i];
-    const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
+    const srtp_dev_hdr_t h = S.hdr(off, len);
     uint32_t code = 0, ab = 0;
     e = 0;
     sid = FZ_NOCHAIN;
@@ -852,7 +854,7 @@ DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
             const uint32_t es = h.enc_start;
             if (len < tag || es > len - tag ||
                 ((z.flags & SRTP_DS_AEAD) && len - es < tag) ||
-                F.cap[i] < len - tag ||
+                cap < len - tag ||
                 ((z.flags & SRTP_DS_ICM_CONF) &&
                  (len - tag - es + 15) / 16 > 0xffffu)) {
                 ab |= FZ_AB_STATIC;
@@ -860,11 +862,11 @@ DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
                 if (z.mki) {
                     // srtp_prepass.hip mki_is_device_key
                     const uint32_t sz = z.mki & 0xffffu;
-                    const uint8_t *p = A.in + off + len - (z.mki >> 16);
+                    const uint32_t x = len - (z.mki >> 16);
                     const uint8_t *mk = A.keys[z.key].mki;
                     uint32_t d = 0;
                     for (uint32_t b = 0; b < sz; b++)
-                        d |= p[b] ^ mk[b];
+                        d |= S.byte(x + b) ^ mk[b];
                     if (d)
                         ab |= FZ_AB_MKI;
                 }
@@ -882,7 +884,6 @@ DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
             }
         }
     }
-    const uint32_t cap = F.cap[i];
     *(u32x4 *)&F.rec[i] =
         u32x4{ (uint32_t)e, (uint32_t)(e >> 32) | (code << 16), sid, cap };
     if (sid == FZ_NOCHAIN)
@@ -896,18 +897,58 @@ DEV srtp_dev_meta_t fzu_classify(const IcmArgs &A, uint32_t i, FzLane &z,
 // ... after icm_packet: the candidate's verdict (status, length; an
 // authenticated packet's index into the run and the second bitmap)
 DEV void fzu_verdict(const IcmArgs &A, uint32_t i, FzLane &z,
-                     const srtp_dev_meta_t &m, uint64_t e, uint32_t sid)
+                     const srtp_dev_meta_t &m, uint64_t e, uint32_t sid,
+                     bool ok)
 {
     if (sid == FZ_NOCHAIN)
         return;
     const IcmFused &F = A.fz;
-    if (A.auth_ok[i]) {
+    if (ok) {
         F.status[i] = 0;
         F.cap[i] = m.len;
         fzu_auth(F, z, e);
     } else {
         F.status[i] = 7;   // srtp_err_status_auth_fail
         atomicAdd(F.nfail, 1u);
+    }
+}
+
+// The packet's bytes read from the arena (the fused classification's
+// header, trailer save and MKI; srtp_parse_rtp's 16-byte header load)
+struct GlbSrc {
+    const uint8_t *p;   // the packet (in place: input and output)
+    DEV srtp_dev_hdr_t hdr(uint64_t off, uint32_t len) const
+    {
+        return srtp_parse_rtp(p, off, len);
+    }
+    DEV void tail(uint32_t x, uint32_t tn, u32x4 &w) const
+    {
+        fz_tail_save(p + x, tn, w);
+    }
+    DEV uint32_t byte(uint32_t x) const { return p[x]; }
+};
+
+// one packet of a fused batch from the arena: classification, crypto, and
+// (unprotect) the verdict
+template <int NR, bool TAB4, bool AUTH, bool PROTECT, int KM, class KEY>
+DEV void fz_one(const IcmArgs &A, uint32_t i, FzLane &z, uint64_t off,
+                uint32_t len, uint32_t cap, const GlbSrc &S, const AesLds &T,
+                KEY &rk)
+{
+    if constexpr (PROTECT) {
+        const srtp_dev_meta_t m =
+            fz_classify(A, i, z, icm_vid<NR, AUTH>(), off, len, cap, S);
+        icm_packet<NR, TAB4, AUTH, PROTECT, KM>(A, m, off, off, i, A.uni, T,
+                                                rk);
+    } else {
+        uint64_t e;
+        uint32_t sid;
+        const srtp_dev_meta_t m = fzu_classify(A, i, z, icm_vid<NR, AUTH>(),
+                                               off, len, cap, S, e, sid);
+        icm_packet<NR, TAB4, AUTH, PROTECT, KM>(A, m, off, off, i, A.uni, T,
+                                                rk);
+        if (sid != FZ_NOCHAIN)
+            fzu_verdict(A, i, z, m, e, sid, A.auth_ok[i] != 0);
     }
 }
 
@@ -926,7 +967,9 @@ constexpr int ICM_THREADS_UNI = ICM_THREADS_UNI_N;
 constexpr int ICM_THREADS_LANE = 512;
 constexpr uint32_t ICM_SKIP = 0xffffffffu;
 
-template <int NR, bool AUTH, bool PROTECT, int KM, bool FUSED = false>
+// FUSED: 0 = meta descriptors, 1 = the order-free classification in the
+// kernel, 2 = that over the wave groups k_icm_stg listed (fz.glist)
+template <int NR, bool AUTH, bool PROTECT, int KM, int FUSED = 0>
 __global__ __launch_bounds__(KM == KM_LANE ? ICM_THREADS_LANE : ICM_THREADS_UNI)
 void k_icm_hmac(IcmArgs A)
 {
@@ -936,6 +979,9 @@ void k_icm_hmac(IcmArgs A)
     __shared__ u32x4 s_tab[LDSB / 16];
     __shared__ uint32_t s_t0[256];   // the S-box row during the table build
     if (A.abort && *A.abort)
+        return;
+    // after k_icm_stg: only the groups it listed (usually none)
+    if (FUSED == 2 && *(volatile const uint32_t *)A.fz.glist == 0)
         return;
     if (NR)
         load_aes_tables<TAB4>(s_tab, s_t0);
@@ -964,25 +1010,23 @@ void k_icm_hmac(IcmArgs A)
             z.run_cmax = 0;
             z.bw_idx = 0;
             z.bw_bits = 0;
-            for (uint32_t i = first; i < A.n; i += stride) {
-                if constexpr (PROTECT) {
-                    const srtp_dev_meta_t m =
-                        fz_classify(A, i, z, icm_vid<NR, AUTH>());
-                    // fused batches are in place (fused_ok): one offset
-                    const uint64_t off = A.in_off[i];
-                    icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                        A, m, off, off, i, A.uni, T, rk);
-                } else {
-                    uint64_t e;
-                    uint32_t sid;
-                    const srtp_dev_meta_t m =
-                        fzu_classify(A, i, z, icm_vid<NR, AUTH>(), e, sid);
-                    // fused batches are in place (fused_ok): one offset
-                    const uint64_t off = A.in_off[i];
-                    icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                        A, m, off, off, i, A.uni, T, rk);
-                    fzu_verdict(A, i, z, m, e, sid);
-                }
+            // wave groups of 64 consecutive packets: every group in turn,
+            // or (glmode) the groups k_icm_stg listed
+            const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+            constexpr bool GL = FUSED == 2;
+            const uint32_t cnt = GL ? A.fz.glist[0] : 0u;
+            for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);;
+                 w += nw) {
+                if (GL ? w >= cnt : 64ull * w >= A.n)
+                    break;
+                const uint32_t i = 64 * (GL ? A.fz.glist[1 + w] : w) + lpos;
+                if (i >= A.n)
+                    continue;
+                // fused batches are in place (fused_ok): one offset
+                const uint64_t off = A.in_off[i];
+                const GlbSrc S{ A.in + off };
+                fz_one<NR, TAB4, AUTH, PROTECT, KM>(
+                    A, i, z, off, A.fz.in_len[i], A.fz.cap[i], S, T, rk);
             }
             fz_flush<PROTECT>(A.fz, z);
             return;
@@ -1030,6 +1074,435 @@ void k_icm_hmac(IcmArgs A)
     }
 }
 
+// ---------------------------------------------------------------------------
+// Staged fused kernel (k_icm_stg): per-lane keys, the order-free
+// classification inside the kernel, small packets in contiguous slots --
+// BASELINE configs[3]'s shape (8M x 172-byte packets in 192-byte slots).
+//
+// The per-lane form moves every packet through 16-byte per-lane accesses:
+// each wave instruction touches 64 packets 192 B apart, and a 172-byte
+// packet costs its lane ~28 loads and ~18 stores, most to lines no other
+// lane of the wave touches, behind two dependent steps (offset -> header,
+// offset -> data).  Measured: the waves wait on memory 41 % of their
+// cycles, and the counted traffic is 1.67x the algorithmic bytes
+// (profiles/r04_g711_protect.md).  Here a wave takes 64 CONSECUTIVE packets
+// (a group) and, when their slots tile one span [off0, off0 + 64 D) with
+// D <= 192, moves the span through LDS:
+//   * in: 4D/64 (12 for D = 192) global_load_lds_dwordx4 sweeps, 1 KiB of
+//     contiguous bytes per wave-instruction, no VGPRs;
+//   * every lane classifies, encrypts / decrypts and authenticates its
+//     packet out of the image and writes the result (output words, tag,
+//     MKI) back into it;
+//   * out: the span is stored back with the same 1-KiB sweeps.  Bytes of
+//     a slot past the packet (its capacity: cap >= D) go back unchanged.
+// Granule k (16 B) of the span sits at LDS granule stg_swz(k) = k ^ ((k /
+// 48) & 3): for D = 192 (packet p's granule q is k = 12p + q) every
+// ds_read_b128 lane group of 16 reads 16 distinct banks (lanes p, p' of a
+// group with equal p mod 4 differ in (p >> 2) & 3, and the XOR of those
+// bits separates them; p mod 4 separates the rest through bits 2-3 of k).
+// The swizzle changes only bits 0-1 of k as a function of bits >= 4, so it
+// is its own inverse and each quarter-wave of a sweep still covers one
+// 256-byte block.
+// LDS: the image, 12 KiB per wave (96 KiB for 8 waves), leaves 64 KiB for
+// the AES tables: (T0, T1) with T2 / T3 as rotations (TAB4 = false).
+// A group outside the conditions runs the per-lane form from the arena.
+constexpr uint32_t STG_GRAN = 768;   // granules per wave image (12 KiB)
+constexpr uint32_t STG_WAVES = 8;    // 512 lanes per workgroup
+
+DEV uint32_t stg_swz(uint32_t k) { return k ^ ((k / 48u) & 3u); }
+
+// the wave's image, seen from one lane's packet (first granule k0)
+struct StgImg {
+    u32x4 *w;
+    uint32_t k0;
+    uint32_t D;              // slot bytes
+    const uint8_t *p;        // the packet in the arena (reads past the slot)
+    DEV u32x4 *gp(uint32_t x) const { return w + stg_swz(k0 + (x >> 4)); }
+    DEV u32x4 ld(uint32_t q) const { return w[stg_swz(k0 + q)]; }
+    DEV void st(uint32_t q, const u32x4 &v) const { w[stg_swz(k0 + q)] = v; }
+    // 4-aligned word / byte at byte offset x of the packet
+    DEV uint32_t ldw(uint32_t x) const
+    {
+        return ((const uint32_t *)gp(x))[(x >> 2) & 3];
+    }
+    DEV void stw(uint32_t x, uint32_t v) const
+    {
+        ((uint32_t *)gp(x))[(x >> 2) & 3] = v;
+    }
+    DEV uint32_t byte(uint32_t x) const
+    {
+        return ((const uint8_t *)gp(x))[x & 15];
+    }
+    DEV void stb(uint32_t x, uint32_t v) const
+    {
+        ((uint8_t *)gp(x))[x & 15] = (uint8_t)v;
+    }
+    // srtp_parse_rtp (srtp_rtp_hdr.h) over the image
+    DEV srtp_dev_hdr_t hdr(uint64_t off, uint32_t len) const
+    {
+        srtp_dev_hdr_t h;
+        h.len = len;
+        h.ssrc = 0;
+        h.seq_len = 0;
+        uint32_t err = 0, es = 0;
+        if ((off & 15) != 0 || len < 12) {
+            err = 2;
+        } else {
+            const u32x4 q = ld(0);
+            const uint32_t w0 = bswap(q.x);
+            h.ssrc = bswap(q.z);
+            h.seq_len = w0 & 0xffffu;
+            es = 12 + 4 * ((w0 >> 24) & 0xfu);
+            if (len < es) {
+                err = 2;
+            } else if ((w0 >> 28) & 1) {
+                if (len < es + 4) {
+                    err = 2;
+                } else {
+                    es += ((bswap(ldw(es)) & 0xffffu) + 1) * 4;
+                    if (len < es)
+                        err = 2;
+                }
+            }
+        }
+        h.enc_start = err ? (err << 24) : es;
+        return h;
+    }
+    // the tn (<= 16) bytes at x, little-endian words (fz_tail_save); past
+    // the slot (a trailer longer than the slot holds: the group then runs
+    // from the arena) from the arena
+    DEV void tail(uint32_t x, uint32_t tn, u32x4 &w4) const
+    {
+        if (x + tn > D) {
+            fz_tail_save(p + x, tn, w4);
+            return;
+        }
+        const uint32_t a = x & ~3u, r = x & 3;
+        uint32_t W[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++)
+            W[k] = a + 4 * k < x + tn ? ldw(a + 4 * k) : 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            w4[k] = __builtin_amdgcn_alignbyte(W[k + 1], W[k], r);
+    }
+    // the first n bytes of the little-endian words w at byte offset x
+    template <int NW>
+    DEV void put(uint32_t x, const uint32_t (&w4)[NW], uint32_t n) const
+    {
+        const bool al = (x & 3) == 0;
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const int r = (int)n - 4 * j;
+            if (r <= 0)
+                break;
+            if (r >= 4 && al) {
+                stw(x + 4 * j, w4[j]);
+                continue;
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (b < r)
+                    stb(x + 4 * j + b, w4[j] >> (8 * b));
+        }
+    }
+    template <int NW>
+    DEV uint32_t diff(uint32_t x, const uint32_t (&w4)[NW], uint32_t n) const
+    {
+        const bool al = (x & 3) == 0;
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < NW; j++) {
+            const int r = (int)n - 4 * j;
+            if (r <= 0)
+                break;
+            if (r >= 4 && al) {
+                d |= ldw(x + 4 * j) ^ w4[j];
+                continue;
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (b < r)
+                    d |= byte(x + 4 * j + b) ^ ((w4[j] >> (8 * b)) & 0xffu);
+        }
+        return d;
+    }
+};
+
+// icm_chunk over the image: chunk b's quads read from and written back to
+// the lane's granules; the partial last quad keeps the image's bytes past
+// the data (what follows the packet in its slot, or the tag on unprotect)
+template <int NR, bool AUTH, bool PROTECT, class KEY>
+DEV void stg_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
+                   const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
+                   uint32_t hst[5], const StgImg &I)
+{
+    constexpr bool TAB4 = false;
+    const uint32_t q0 = 4 * b;
+    u32x4 v[4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        v[t] = u32x4{ 0, 0, 0, 0 };
+        if (q0 + t < p.nq)
+            v[t] = I.ld(q0 + t);
+    }
+    uint32_t ks[4][4];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t jj = q0 + t - p.qoff;
+        ks[t][0] = p.cb[0];
+        ks[t][1] = p.cb[1];
+        ks[t][2] = p.cb[2];
+        ks[t][3] = p.cb[3] ^ ((jj >> 8) << 16) ^ ((jj & 0xffu) << 24);
+    }
+    if (p.conf) {
+#pragma unroll
+        for (int g = 0; g < 4; g += ICM_NB) {
+            const int jf = (int)(q0 + g) - (int)p.qoff;
+            if (jf + ICM_NB - 1 < 0 || 16 * jf >= (int)p.P)
+                continue;
+            auto &kg = *reinterpret_cast<uint32_t(*)[ICM_NB][4]>(&ks[g]);
+            if (jf >= 0 && jf + ICM_NB - 1 < 256) {
+                uint32_t jb[ICM_NB];
+#pragma unroll
+                for (int j = 0; j < ICM_NB; j++)
+                    jb[j] = (uint32_t)(jf + j) << 8;
+                aes_ctr<ICM_NB, NR, TAB4>(kg, jb, C, rk, T);
+            } else {
+                aes_blocks<ICM_NB, NR, TAB4>(kg, rk, T);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int t = 0; t < 4; t++)
+            ks[t][0] = ks[t][1] = ks[t][2] = ks[t][3] = 0;
+    }
+    uint32_t wv[16];
+#pragma unroll
+    for (int t = 0; t < 4; t++) {
+        const uint32_t q = q0 + t;
+        uint32_t kk[4];
+        ks_shift(ks_prev, ks[t], p.s, kk);
+        if (b < p.bclean) {
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                if (4 * q + u < p.hw)
+                    kk[u] = 0;   // header words are never encrypted
+        }
+        u32x4 o;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            o[u] = v[t][u] ^ kk[u];
+        if (16 * q + 16 <= p.L) {
+            I.st(q, o);
+        } else if (16 * q < p.L) {
+            // bytes [L, 16q + 16) keep what the image holds
+            const uint32_t n = p.L - 16 * q;
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int r = (int)n - 4 * u;
+                const uint32_t m = r >= 4 ? ~0u
+                                          : (r <= 0 ? 0u : (1u << (8 * r)) - 1);
+                o[u] = bsel(m, o[u], v[t][u]);
+            }
+            I.st(q, o);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
+            ks_prev[u] = ks[t][u];
+        }
+    }
+    if (AUTH) {
+        if (64 * b + 64 > p.L) {
+#pragma unroll
+            for (int g = 0; g < 16; g++)
+                wv[g] = tail_word(wv[g], (int)p.L - (int)(64 * b + 4 * g),
+                                  p.roc);
+            if (b == p.nb - 1) {
+                wv[14] = 0;
+                wv[15] = (64 + p.L + 4) * 8;
+            }
+        }
+        sha1_compress(hst, wv);
+    }
+}
+
+// one packet out of the image (icm_packet restated over it); returns the
+// tag verdict (unprotect; true on protect)
+template <int NR, bool AUTH, bool PROTECT>
+DEV bool stg_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
+                    const StgImg &I, const AesLds &T, LaneKey<NR> &rk)
+{
+    constexpr bool TAB4 = false;
+    const uint32_t slot = m.key;
+    const srtp_dev_key_t *key = A.keys + slot;
+    rk.reload(A.keys, slot);
+
+    IcmPkt p;
+    p.in = nullptr;
+    p.out = nullptr;
+    const uint32_t enc_start = SRTP_META_ENC_START(m.info);
+    p.L = m.len;
+    p.hw = enc_start >> 2;
+    p.s = p.hw & 3;
+    p.qoff = p.hw >> 2;
+    p.P = p.L - enc_start;
+    p.roc = m.roc;
+    p.conf = key->conf != 0;
+    p.nq = (p.L + 15) >> 4;
+    p.nb = AUTH ? ((p.L + 12) >> 6) + 1 : ((p.nq + 3) >> 2);
+    p.bclean = (p.qoff + 4) >> 2;
+    // counter block (aes_icm.c:236-258, srtp.c:2694-2707)
+    const uint32_t seq = bswap(I.ldw(0)) & 0xffffu;
+    p.cb[0] = key->salt[0];
+    p.cb[1] = key->salt[1] ^ I.ldw(8);   // SSRC bytes
+    p.cb[2] = key->salt[2] ^ bswap(m.roc);
+    p.cb[3] = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
+
+    uint32_t hst[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        hst[k] = AUTH ? key->ipad[k] : 0;
+    uint32_t ks_prev[4] = { 0, 0, 0, 0 };
+    CtrCache C{};
+    if (p.conf)
+        C = ctr_cache<NR, TAB4>(p.cb, rk, T);
+    for (uint32_t b = 0; b < p.nb; b++)
+        stg_chunk<NR, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, I);
+
+    const uint32_t tag_len = key->tag_len;
+    const uint32_t mki_size = key->mki_size;
+    if (!AUTH) {
+        if (PROTECT && mki_size) {
+            for (uint32_t u = 0; u < mki_size; u++)
+                I.stb(p.L + u, key->mki[u]);
+        }
+        return true;
+    }
+    // outer hash: SHA1(opad || inner)  (hmac.c:181-229)
+    uint32_t ow[16];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        ow[k] = hst[k];
+    ow[5] = 0x80000000u;
+#pragma unroll
+    for (int k = 6; k < 15; k++)
+        ow[k] = 0;
+    ow[15] = (64 + 20) * 8;
+    uint32_t oh[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        oh[k] = key->opad[k];
+    sha1_compress(oh, ow);
+    uint32_t tw[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        tw[k] = bswap(oh[k]);
+    if (PROTECT) {
+        for (uint32_t u = 0; u < mki_size; u++)
+            I.stb(p.L + u, key->mki[u]);
+        I.put(p.L + mki_size, tw, tag_len);
+        return true;
+    }
+    return I.diff(p.L + mki_size, tw, tag_len) == 0;
+}
+
+template <int NR, bool AUTH, bool PROTECT>
+__global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
+{
+    constexpr bool TAB4 = false;
+    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
+    __shared__ u32x4 s_img[STG_WAVES][STG_GRAN];
+    if (A.abort && *A.abort)
+        return;
+    // the S-box row of the table build sits in the image area
+    load_aes_tables<TAB4>(s_tab, (uint32_t *)&s_img[0][0]);
+    __syncthreads();
+    const AesLds T = make_aes_lds(s_tab);
+    LaneKey<NR> rk;
+    const IcmFused &F = A.fz;
+    FzLane z;
+    z.ssrc = 0;
+    z.sid = FZ_NOCHAIN;
+    z.run_sid = FZ_NOCHAIN;
+    z.run_cnt = 0;
+    z.run_max = 0;
+    z.run_min = ~0ull;
+    z.run_cmax = 0;
+    z.bw_idx = 0;
+    z.bw_bits = 0;
+    const uint32_t L = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32x4 *img = s_img[wv];
+    constexpr uint32_t vid = icm_vid<NR, AUTH>();
+    const uint32_t nw = gridDim.x * STG_WAVES;
+    for (uint32_t g = blockIdx.x * STG_WAVES + wv; 64ull * g < A.n; g += nw) {
+        const uint32_t i = 64 * g + L;
+        const bool live = i < A.n;
+        const uint64_t off = live ? A.in_off[i] : 0;
+        const uint32_t len = live ? F.in_len[i] : 0;
+        const uint32_t cap = live ? F.cap[i] : 0;
+        // the group's slots tile one span: off = off0 + L * D
+        const uint32_t olo = (uint32_t)off, ohi = (uint32_t)(off >> 32);
+        const uint64_t off0 =
+            ((uint64_t)__builtin_amdgcn_readfirstlane(ohi) << 32) |
+            (uint32_t)__builtin_amdgcn_readfirstlane(olo);
+        const uint32_t D =
+            (uint32_t)__builtin_amdgcn_readlane((int)olo, 1) - (uint32_t)off0;
+        // (protect: with the largest trailer of the batch's streams, so no
+        // tag written into the image leaves the packet's slot)
+        const bool fit = live && (off0 & 15) == 0 && (D & 15) == 0 && D >= 16 &&
+                         D <= 16 * STG_GRAN / 64 && off == off0 + (uint64_t)L * D &&
+                         cap >= D && len + (PROTECT ? F.max_trailer : 0u) <= D;
+        if (__builtin_amdgcn_ballot_w64(fit) != ~0ull) {
+            // the per-lane form runs this group after the launch (its
+            // registers, inlined here, would spill the staged form's)
+            if (L == 0)
+                F.glist[1 + atomicAdd(&F.glist[0], 1u)] = g;
+            continue;
+        }
+        // fill the image: sweep j, lane L -> image granule 64 j + L, span
+        // granule stg_swz(64 j + L)
+        const uint32_t G = 4 * D;   // granules of the span
+        const uint8_t *span = A.in + off0;
+        for (uint32_t j = 0; 64 * j < G; j++) {
+            const uint32_t P = 64 * j + L;
+            if (P < G)
+                __builtin_amdgcn_global_load_lds(
+                    (const void __attribute__((address_space(1))) *)(span + 16ull * stg_swz(P)),
+                    (void __attribute__((address_space(3))) *)(img + 64 * j), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const StgImg I{ img, (uint32_t)(L * D) >> 4, D, A.in + off };
+        srtp_dev_meta_t m;
+        uint64_t e = 0;
+        uint32_t sid = FZ_NOCHAIN;
+        if constexpr (PROTECT)
+            m = fz_classify(A, i, z, vid, off, len, cap, I);
+        else
+            m = fzu_classify(A, i, z, vid, off, len, cap, I, e, sid);
+        // a packet runs only for an eligible stream of this variant, whose
+        // trailer is at most max_trailer: tag and MKI stay in the slot
+        const bool run = SRTP_META_STATUS(m.info) == 0 &&
+                         SRTP_META_VARIANT(m.info) == vid;
+        bool ok = false;
+        if (run)
+            ok = stg_packet<NR, AUTH, PROTECT>(A, m, I, T, rk);
+        if (!PROTECT && run && A.auth_ok)
+            A.auth_ok[i] = ok ? 1 : 0;
+        if (!PROTECT && sid != FZ_NOCHAIN)
+            fzu_verdict(A, i, z, m, e, sid, ok);
+        // the image back to the span: the same sweeps
+        uint8_t *ospan = A.out + off0;
+        for (uint32_t j = 0; 64 * j < G; j++) {
+            const uint32_t P = 64 * j + L;
+            if (P < G)
+                *(gptr)(ospan + 16ull * stg_swz(P)) = img[P];
+        }
+    }
+    fz_flush<PROTECT>(F, z);
+}
+
 }   // namespace
 
 template <int NR, int KM, bool AU, bool PR>
@@ -1042,8 +1515,17 @@ static void icm_go(const IcmArgs &A, int ncu, hipStream_t st)
     if (wgs > cap)
         wgs = cap;
     if constexpr (KM == KM_LANE && NR > 0) {
+        if (A.fused && A.stg) {
+            // the staged kernel, then the per-lane form over the groups it
+            // left (a persistent grid that returns at once when none)
+            hipLaunchKernelGGL((k_icm_stg<NR, AU, PR>), dim3((unsigned)wgs),
+                               dim3(512), 0, st, A);
+            hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM, 2>),
+                               dim3((unsigned)wgs), dim3((unsigned)T), 0, st, A);
+            return;
+        }
         if (A.fused) {
-            hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM, true>),
+            hipLaunchKernelGGL((k_icm_hmac<NR, AU, PR, KM, 1>),
                                dim3((unsigned)wgs), dim3((unsigned)T), 0, st, A);
             return;
         }

@@ -133,6 +133,7 @@ struct PpState {
     uint32_t bmap_cap = 0;
     unsigned long long *fz_hicand = nullptr;   // unprotect: highest candidate
     uint32_t *fz_nfail = nullptr;              // unprotect: failed tag checks
+    uint32_t *fz_glist = nullptr;              // k_icm_stg's per-lane groups
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -687,13 +688,14 @@ __global__ void k_fz_reset(uint32_t *abort, unsigned long long *cnt,
                            unsigned long long *new_index,
                            unsigned long long *emin,
                            unsigned long long *hicand, uint32_t *nfail,
-                           uint32_t ns)
+                           uint32_t *glist, uint32_t ns)
 {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s == 0) {
         *abort = 0;
         if (nfail)
             *nfail = 0;
+        glist[0] = 0;
     }
     if (s >= ns)
         return;
@@ -2422,6 +2424,9 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     if (P->tsave)
         PPCHK(hipFree(P->tsave));
     PPCHK(hipMalloc((void **)&P->tsave, c * 16));
+    if (P->fz_glist)
+        PPCHK(hipFree(P->fz_glist));
+    PPCHK(hipMalloc((void **)&P->fz_glist, (c / 64 + 2) * 4));
     // buckets: region A <= 2 x its packets (>= BK_MIN per stream, padded
     // to 64), region B <= its packets
     PPCHK(hipMalloc((void **)&P->rec, 2 * c * sizeof(srtp_dev_rec_t)));
@@ -2463,7 +2468,8 @@ void srtp_gpu_pp_free(void *p)
                      P->rec, P->rec_idx, P->bk_range, P->ch_tile,
                      P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
                      P->pu_first, P->fzrec, P->tsave, P->fz_cnt,
-                     P->fz_emin, P->fz_bmap, P->fz_hicand, P->fz_nfail };
+                     P->fz_emin, P->fz_bmap, P->fz_hicand, P->fz_nfail,
+                     P->fz_glist };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2818,7 +2824,7 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     unsigned long long *hi = (unsigned long long *)P->new_index;
     hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
                        P->abort, P->fz_cnt, hi, P->fz_emin, nullptr, nullptr,
-                       ns);
+                       P->fz_glist, ns);
     IcmFused F;
     F.in_len = b->in_len;
     F.cap = b->out_len;
@@ -2829,6 +2835,8 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     F.hmask = P->hcap - 1;
     F.rec = P->fzrec;
     F.tsave = P->tsave;
+    F.max_trailer = b->max_trailer;
+    F.glist = P->fz_glist;
     F.cnt = P->fz_cnt;
     F.new_index = hi;
     F.emin = P->fz_emin;
@@ -3223,7 +3231,7 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
     unsigned long long *hi = (unsigned long long *)P->new_index;
     hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
                        P->abort, P->fz_cnt, hi, P->fz_emin, P->fz_hicand,
-                       P->fz_nfail, ns);
+                       P->fz_nfail, P->fz_glist, ns);
     IcmFused F;
     F.in_len = b->in_len;
     F.cap = b->out_len;
@@ -3234,6 +3242,8 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
     F.hmask = P->hcap - 1;
     F.rec = P->fzrec;
     F.tsave = nullptr;
+    F.max_trailer = 0;
+    F.glist = P->fz_glist;
     F.cnt = P->fz_cnt;
     F.new_index = hi;
     F.emin = P->fz_emin;

@@ -432,21 +432,48 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     snd.L.srtp_mi355x_set_key_buckets(0)
 
 
-@pytest.mark.parametrize("lengths", ["uniform160", "mixed"])
-def test_fused_midsize_every_packet_lane_reuse(lengths):
+def _rtp_headers(a, lens, rng):
+    """CSRCs and RFC 8285 extensions in the configs[3]-shaped arena `a`
+    (uint8 (n, slot) on the GPU; SSRC and sequence numbers kept): 0, 1 or
+    3 CSRCs, and for a third of the packets a 0xBEDE extension of 0..2
+    words; returns the lengths raised to hold each header"""
+    import numpy as np
+    import torch
+    n = a.shape[0]
+    cc = rng.choice(np.array([0, 0, 1, 3]), n)
+    x = rng.random(n) < 0.3
+    xw = rng.integers(0, 3, n)
+    hl = 12 + 4 * cc + np.where(x, 4 + 4 * xw, 0)
+    host = a.cpu().numpy()
+    host[:, 0] = 0x80 | cc | (x.astype(np.int64) << 4)
+    idx = np.nonzero(x)[0]
+    e = 12 + 4 * cc[idx]
+    host[idx, e] = 0xbe
+    host[idx, e + 1] = 0xde
+    host[idx, e + 2] = 0
+    host[idx, e + 3] = xw[idx]
+    a.copy_(torch.from_numpy(host).cuda())
+    return np.maximum(lens, hl)
+
+
+@pytest.mark.parametrize("lengths,slot", [("uniform160", 192), ("mixed", 192),
+                                          ("mixed", 320)])
+def test_fused_midsize_every_packet_lane_reuse(lengths, slot):
     """The fused order-free path at a size where the persistent grid's
     stride (256 CUs x 512 lanes = 2^17) is below the batch: 2^18 packets
     over 2,048 distinct-key streams, round-robin, so every lane runs two
     packets of ONE stream -- the second takes fz_lookup's cached stream
-    record and LaneKey::reload's kept round keys.  EVERY packet is compared
-    with the C oracle, protect and then unprotect, both in place; two
-    consecutive batches (the second across a ROC boundary)."""
+    record and LaneKey::reload's kept round keys.  192-byte slots take the
+    LDS-staged kernel (k_icm_stg: every wave group's slots tile one span),
+    320-byte slots the per-lane form.  "mixed": lengths 12..166 with CSRCs
+    and header extensions.  EVERY packet is compared with the C oracle,
+    protect and then unprotect, both in place; two consecutive batches (the
+    second across a ROC boundary)."""
     _gpu()
     import numpy as np
     import torch
     ns, per, tag = 2048, 128, 10
     n = ns * per
-    slot = 320
     base = 0x20000000
     pols = [policy("icm128_hmac80", ssrc=base + k, seed=7000 + k)
             for k in range(ns)]
@@ -465,7 +492,7 @@ def test_fused_midsize_every_packet_lane_reuse(lengths):
         if lengths == "uniform160":
             lens = np.full(n, 12 + 160, dtype=np.int64)
         else:
-            lens = rng.integers(12, slot - tag - 16, n)
+            lens = _rtp_headers(a, rng.integers(12, 192 - tag - 16, n), rng)
         orig = a.clone()
         d = a.view(-1)
         ln = torch.from_numpy(lens.astype(np.int32)).cuda()
@@ -506,6 +533,61 @@ def test_fused_midsize_every_packet_lane_reuse(lengths):
     assert snd.prepass_sorted_batches() == 0
     for s in (base, base + 1, base + 63, base + ns - 1):
         assert snd.get_roc(s)[1] == osnd.get_roc(s)[1]
+
+
+@pytest.mark.parametrize("case", ["duplicate", "unknown_ssrc", "long_chain"])
+def test_staged_declined_batch_is_restored(case):
+    """A batch of the LDS-staged kernel's shape (192-byte slots, capacity =
+    slot) that the order-free form declines: the staged kernel has written
+    every slot back (protected packets, tags, the rest of each slot as it
+    was); the decline restores it, then the host path (duplicate, unknown
+    SSRC) or the sorted chain form (a stream with more packets than its
+    window) runs.  Every status and byte equal to the oracle's, and every
+    slot byte past each protected packet exactly as it was."""
+    _gpu()
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(900 + len(case))
+    ns, per, slot, tag = 256, 64, 192, 10
+    base = 0x30000000
+    pols = [policy("icm128_hmac80", ssrc=base + k, seed=9000 + k)
+            for k in range(ns)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    gen = torch.Generator(device="cuda").manual_seed(901)
+    a = _rr_arena(ns, per, 0, 0x1000, base, gen, slot)
+    n = ns * per
+    lens = rng.integers(12, slot - tag, n)
+    if case == "duplicate":
+        a[5000] = a[300]
+        lens[5000] = lens[300]
+    elif case == "unknown_ssrc":
+        a[777, 8:12] = torch.tensor([0x0b, 0xad, 0x0b, 0xad], dtype=torch.uint8)
+    else:
+        # stream 3's packets advance past its 128-packet window
+        k = np.arange(3, n, ns)
+        seqs = 0x1000 + 3 * np.arange(len(k))
+        h = a[torch.from_numpy(k).cuda(), :4].cpu().numpy()
+        h[:, 2] = (seqs >> 8) & 0xff
+        h[:, 3] = seqs & 0xff
+        a[torch.from_numpy(k).cuda(), :4] = torch.from_numpy(h).cuda()
+    orig = a.cpu().numpy().copy()
+    d = a.view(-1)
+    off = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+    ln = torch.from_numpy(lens.astype(np.int32)).cuda()
+    cap = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+    st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    assert lib.protect_device(d, off, ln, d, off, cap, st) == 0
+    st, cap, got = st.cpu().numpy(), cap.cpu().numpy(), a.cpu().numpy()
+    for i in range(n):
+        rc, ref = orc.protect(bytes(orig[i, :lens[i]]), slot)
+        assert st[i] == rc, (i, st[i], rc)
+        if rc == 0:
+            assert bytes(got[i, :cap[i]]) == ref, i
+            assert (got[i, cap[i]:] == orig[i, cap[i]:]).all(), i
+        else:
+            assert cap[i] == slot and (got[i] == orig[i]).all(), i
+    want = {"duplicate": (0, 1), "unknown_ssrc": (0, 1), "long_chain": (1, 0)}
+    assert lib.prepass_stats() == want[case], lib.prepass_last_abort()
 
 
 # --------------------------------------------------------------------------
