@@ -775,7 +775,6 @@ def run_gpu(a, world, rank, local, json_out):
     del base_arena
     off = torch.arange(n, dtype=torch.int64, device=dev) * slot
     in_len = torch.full((n,), rtp_len, dtype=torch.int32, device=dev)
-    out_len = torch.empty(n, dtype=torch.int32, device=dev)
     status = torch.empty(n, dtype=torch.int32, device=dev)
     # one status array per batch, preset to a value no status takes, so the
     # check after the timed region sees every step's verdicts (a batch that
@@ -808,18 +807,19 @@ def run_gpu(a, world, rank, local, json_out):
                     torch.from_numpy(rows).to(dev)].reshape(-1)
                 expect_dups.append(ndup)
     sess.set_timing(True)
-    # out_len: capacities in, lengths out.  Filled once: a step leaves the
-    # lengths it produced (<= slot), which are exactly the capacities the
-    # next batch of the same shape needs.
-    out_len.fill_(slot)
+    # out_len: capacities in, lengths out -- one array per batch, each
+    # packet's capacity its whole slot (what a caller with a slotted arena
+    # passes), set before the timed region
+    caps = [torch.full((n,), slot, dtype=torch.int32, device=dev)
+            for _ in range(nb)]
     torch.cuda.synchronize()
     k_step = [0]
     fn = sess.protect_prepared if a.op == "protect" else \
         sess.unprotect_prepared
     # one descriptor per batch, built before the timed region
-    descs = [sess.prepare_device(ar, off, in_len, ar, off, out_len, st,
+    descs = [sess.prepare_device(ar, off, in_len, ar, off, cp, st,
                                  stream=stream)
-             for ar, st in zip(arenas, statuses)]
+             for ar, cp, st in zip(arenas, caps, statuses)]
 
     pipelined = a.pipelined and a.op == "protect"
     warm_ms = []

@@ -78,11 +78,14 @@ struct IcmFused {
     uint32_t *bmap2;
     uint32_t *nfail;
     // k_icm_stg: the largest trailer a protected packet of the batch gets,
-    // and the list of wave groups (64 consecutive packets) it leaves to the
-    // per-lane form: glist[0] = count, group ids from glist[1]
+    // and the wave groups (64 consecutive packets) it leaves to the
+    // per-lane form, per wave w of the grid: glist[0] != 0 when any,
+    // glist[1 + w] = wave w's count, its group ids from
+    // glist[1 + FZ_GL_WAVES + w * cap], cap = ceil(groups / waves)
     uint32_t max_trailer;
     uint32_t *glist;
 };
+constexpr uint32_t FZ_GL_WAVES = 4096;   // waves of a persistent grid, max
 
 // AES-ICM (+ HMAC-SHA1) kernel arguments
 struct IcmArgs {

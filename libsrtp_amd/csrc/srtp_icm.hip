@@ -1013,13 +1013,17 @@ void k_icm_hmac(IcmArgs A)
             // wave groups of 64 consecutive packets: every group in turn,
             // or (glmode) the groups k_icm_stg listed
             const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+            // (glmode: this wave's own list, the groups k_icm_stg's wave of
+            // the same id left, so each lane keeps its stream and key)
             constexpr bool GL = FUSED == 2;
-            const uint32_t cnt = GL ? A.fz.glist[0] : 0u;
-            for (uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);;
-                 w += nw) {
-                if (GL ? w >= cnt : 64ull * w >= A.n)
+            const uint32_t wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+            const uint32_t gcap = (((A.n + 63) >> 6) + nw - 1) / nw;
+            const uint32_t *gl = A.fz.glist + 1 + FZ_GL_WAVES + wid * gcap;
+            const uint32_t cnt = GL ? A.fz.glist[1 + wid] : 0u;
+            for (uint32_t k = 0, w = wid;; k++, w += nw) {
+                if (GL ? k >= cnt : 64ull * w >= A.n)
                     break;
-                const uint32_t i = 64 * (GL ? A.fz.glist[1 + w] : w) + lpos;
+                const uint32_t i = 64 * (GL ? gl[k] : w) + lpos;
                 if (i >= A.n)
                     continue;
                 // fused batches are in place (fused_ok): one offset
@@ -1436,7 +1440,11 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
     u32x4 *img = s_img[wv];
     constexpr uint32_t vid = icm_vid<NR, AUTH>();
     const uint32_t nw = gridDim.x * STG_WAVES;
-    for (uint32_t g = blockIdx.x * STG_WAVES + wv; 64ull * g < A.n; g += nw) {
+    const uint32_t wid = blockIdx.x * STG_WAVES + wv;
+    const uint32_t gcap = (((A.n + 63) >> 6) + nw - 1) / nw;
+    uint32_t *gl = F.glist + 1 + FZ_GL_WAVES + wid * gcap;
+    uint32_t nl = 0;   // groups on this wave's list
+    for (uint32_t g = wid; 64ull * g < A.n; g += nw) {
         const uint32_t i = 64 * g + L;
         const bool live = i < A.n;
         const uint64_t off = live ? A.in_off[i] : 0;
@@ -1456,9 +1464,12 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
                          cap >= D && len + (PROTECT ? F.max_trailer : 0u) <= D;
         if (__builtin_amdgcn_ballot_w64(fit) != ~0ull) {
             // the per-lane form runs this group after the launch (its
-            // registers, inlined here, would spill the staged form's)
+            // registers, inlined here, would spill the staged form's): on
+            // this wave's list, no atomic (one counter for every wave
+            // would serialise them)
             if (L == 0)
-                F.glist[1 + atomicAdd(&F.glist[0], 1u)] = g;
+                gl[nl] = g;
+            nl++;
             continue;
         }
         // fill the image: sweep j, lane L -> image granule 64 j + L, span
@@ -1499,6 +1510,11 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
             if (P < G)
                 *(gptr)(ospan + 16ull * stg_swz(P)) = img[P];
         }
+    }
+    if (L == 0) {
+        F.glist[1 + wid] = nl;
+        if (nl)
+            F.glist[0] = 1;
     }
     fz_flush<PROTECT>(F, z);
 }

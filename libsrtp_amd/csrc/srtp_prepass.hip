@@ -2426,7 +2426,8 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipMalloc((void **)&P->tsave, c * 16));
     if (P->fz_glist)
         PPCHK(hipFree(P->fz_glist));
-    PPCHK(hipMalloc((void **)&P->fz_glist, (c / 64 + 2) * 4));
+    PPCHK(hipMalloc((void **)&P->fz_glist,
+                    (c / 64 + 2 + 2 * FZ_GL_WAVES) * 4));
     // buckets: region A <= 2 x its packets (>= BK_MIN per stream, padded
     // to 64), region B <= its packets
     PPCHK(hipMalloc((void **)&P->rec, 2 * c * sizeof(srtp_dev_rec_t)));
