@@ -1107,6 +1107,7 @@ void k_icm_hmac(IcmArgs A)
 // The swizzle changes only bits 0-1 of k as a function of bits >= 4, so it
 // is its own inverse and each quarter-wave of a sweep still covers one
 // 256-byte block.
+// Slots of 64, 128 or 192 bytes (D a multiple of 64: see StgImg).
 // LDS: the image, 12 KiB per wave (96 KiB for 8 waves), leaves 64 KiB for
 // the AES tables: (T0, T1) with T2 / T3 as rotations (TAB4 = false).
 // A group outside the conditions runs the per-lane form from the arena.
@@ -1116,14 +1117,18 @@ constexpr uint32_t STG_WAVES = 8;    // 512 lanes per workgroup
 DEV uint32_t stg_swz(uint32_t k) { return k ^ ((k / 48u) & 3u); }
 
 // the wave's image, seen from one lane's packet (first granule k0)
+// Slots of D = 64, 128 or 192 bytes put the packet's first granule k0 =
+// L * D / 16 on a multiple of 4 and keep its granules inside one 48-granule
+// block, so its swizzle is one per-lane constant f on bits 0-1: granule q
+// of the packet sits at k0 + (q ^ f)
 struct StgImg {
-    u32x4 *w;
-    uint32_t k0;
+    u32x4 *pk;               // image + k0
+    uint32_t f;              // (k0 / 48) & 3
     uint32_t D;              // slot bytes
     const uint8_t *p;        // the packet in the arena (reads past the slot)
-    DEV u32x4 *gp(uint32_t x) const { return w + stg_swz(k0 + (x >> 4)); }
-    DEV u32x4 ld(uint32_t q) const { return w[stg_swz(k0 + q)]; }
-    DEV void st(uint32_t q, const u32x4 &v) const { w[stg_swz(k0 + q)] = v; }
+    DEV u32x4 *gp(uint32_t x) const { return pk + ((x >> 4) ^ f); }
+    DEV u32x4 ld(uint32_t q) const { return pk[q ^ f]; }
+    DEV void st(uint32_t q, const u32x4 &v) const { pk[q ^ f] = v; }
     // 4-aligned word / byte at byte offset x of the packet
     DEV uint32_t ldw(uint32_t x) const
     {
@@ -1236,7 +1241,7 @@ struct StgImg {
 // icm_chunk over the image: chunk b's quads read from and written back to
 // the lane's granules; the partial last quad keeps the image's bytes past
 // the data (what follows the packet in its slot, or the tag on unprotect)
-template <int NR, bool AUTH, bool PROTECT, class KEY>
+template <int S, int NR, bool AUTH, bool PROTECT, class KEY>
 DEV void stg_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
                    const KEY &rk, const AesLds &T, uint32_t ks_prev[4],
                    uint32_t hst[5], const StgImg &I)
@@ -1285,8 +1290,12 @@ DEV void stg_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
 #pragma unroll
     for (int t = 0; t < 4; t++) {
         const uint32_t q = q0 + t;
+        // the keystream shifted by S = header words mod 4 (register renaming)
         uint32_t kk[4];
-        ks_shift(ks_prev, ks[t], p.s, kk);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+            kk[u] = u >= S ? ks[t][u - S]
+                           : (t ? ks[t - 1][u - S + 4] : ks_prev[u - S + 4]);
         if (b < p.bclean) {
 #pragma unroll
             for (int u = 0; u < 4; u++)
@@ -1312,11 +1321,12 @@ DEV void stg_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
             I.st(q, o);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < 4; u++)
             wv[4 * t + u] = bswap(PROTECT ? o[u] : v[t][u]);
-            ks_prev[u] = ks[t][u];
-        }
     }
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        ks_prev[u] = ks[3][u];
     if (AUTH) {
         if (64 * b + 64 > p.L) {
 #pragma unroll
@@ -1330,6 +1340,15 @@ DEV void stg_chunk(uint32_t b, const IcmPkt &p, const CtrCache &C,
         }
         sha1_compress(hst, wv);
     }
+}
+
+template <int S, int NR, bool AUTH, bool PROTECT, class KEY>
+DEV void stg_chunks(const IcmPkt &p, const CtrCache &C, const KEY &rk,
+                    const AesLds &T, uint32_t hst[5], const StgImg &I)
+{
+    uint32_t ks_prev[4] = { 0, 0, 0, 0 };
+    for (uint32_t b = 0; b < p.nb; b++)
+        stg_chunk<S, NR, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, I);
 }
 
 // one packet out of the image (icm_packet restated over it); returns the
@@ -1368,12 +1387,15 @@ DEV bool stg_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
 #pragma unroll
     for (int k = 0; k < 5; k++)
         hst[k] = AUTH ? key->ipad[k] : 0;
-    uint32_t ks_prev[4] = { 0, 0, 0, 0 };
     CtrCache C{};
     if (p.conf)
         C = ctr_cache<NR, TAB4>(p.cb, rk, T);
-    for (uint32_t b = 0; b < p.nb; b++)
-        stg_chunk<NR, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, I);
+    switch (p.s) {
+    case 0: stg_chunks<0, NR, AUTH, PROTECT>(p, C, rk, T, hst, I); break;
+    case 1: stg_chunks<1, NR, AUTH, PROTECT>(p, C, rk, T, hst, I); break;
+    case 2: stg_chunks<2, NR, AUTH, PROTECT>(p, C, rk, T, hst, I); break;
+    default: stg_chunks<3, NR, AUTH, PROTECT>(p, C, rk, T, hst, I); break;
+    }
 
     const uint32_t tag_len = key->tag_len;
     const uint32_t mki_size = key->mki_size;
@@ -1444,6 +1466,11 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
     const uint32_t gcap = (((A.n + 63) >> 6) + nw - 1) / nw;
     uint32_t *gl = F.glist + 1 + FZ_GL_WAVES + wid * gcap;
     uint32_t nl = 0;   // groups on this wave's list
+    // the swizzle of image granule 64 j + L, j = 0..11, two bits each
+    uint32_t fr = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < STG_GRAN / 64; j++)
+        fr |= (stg_swz(64 * j + L) ^ (64 * j + L)) << (2 * j);
     for (uint32_t g = wid; 64ull * g < A.n; g += nw) {
         const uint32_t i = 64 * g + L;
         const bool live = i < A.n;
@@ -1459,7 +1486,7 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
             (uint32_t)__builtin_amdgcn_readlane((int)olo, 1) - (uint32_t)off0;
         // (protect: with the largest trailer of the batch's streams, so no
         // tag written into the image leaves the packet's slot)
-        const bool fit = live && (off0 & 15) == 0 && (D & 15) == 0 && D >= 16 &&
+        const bool fit = live && (off0 & 15) == 0 && (D & 63) == 0 && D >= 64 &&
                          D <= 16 * STG_GRAN / 64 && off == off0 + (uint64_t)L * D &&
                          cap >= D && len + (PROTECT ? F.max_trailer : 0u) <= D;
         if (__builtin_amdgcn_ballot_w64(fit) != ~0ull) {
@@ -1476,15 +1503,16 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
         // granule stg_swz(64 j + L)
         const uint32_t G = 4 * D;   // granules of the span
         const uint8_t *span = A.in + off0;
-        for (uint32_t j = 0; 64 * j < G; j++) {
-            const uint32_t P = 64 * j + L;
-            if (P < G)
+#pragma unroll
+        for (uint32_t j = 0; j < STG_GRAN / 64; j++) {
+            if (64 * j < G)
                 __builtin_amdgcn_global_load_lds(
-                    (const void __attribute__((address_space(1))) *)(span + 16ull * stg_swz(P)),
+                    (const void __attribute__((address_space(1))) *)(span + 16ull * ((64 * j + L) ^ ((fr >> (2 * j)) & 3))),
                     (void __attribute__((address_space(3))) *)(img + 64 * j), 16, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const StgImg I{ img, (uint32_t)(L * D) >> 4, D, A.in + off };
+        const uint32_t k0 = (L * D) >> 4;
+        const StgImg I{ img + k0, (k0 / 48) & 3, D, A.in + off };
         srtp_dev_meta_t m;
         uint64_t e = 0;
         uint32_t sid = FZ_NOCHAIN;
@@ -1505,10 +1533,11 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
             fzu_verdict(A, i, z, m, e, sid, ok);
         // the image back to the span: the same sweeps
         uint8_t *ospan = A.out + off0;
-        for (uint32_t j = 0; 64 * j < G; j++) {
-            const uint32_t P = 64 * j + L;
-            if (P < G)
-                *(gptr)(ospan + 16ull * stg_swz(P)) = img[P];
+#pragma unroll
+        for (uint32_t j = 0; j < STG_GRAN / 64; j++) {
+            if (64 * j < G)
+                *(gptr)(ospan + 16ull * ((64 * j + L) ^ ((fr >> (2 * j)) & 3))) =
+                    img[64 * j + L];
         }
     }
     if (L == 0) {
