@@ -1438,14 +1438,18 @@ template <int NR, bool AUTH, bool PROTECT>
 __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
 {
     constexpr bool TAB4 = false;
-    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];
-    __shared__ u32x4 s_img[STG_WAVES][STG_GRAN];
+    // one LDS object: the tables at LDS address 0, so a lookup's address is
+    // its v_perm result (the ds_read immediate offset takes the odd table);
+    // the images after them (96 KiB past a second object's base would cost
+    // a v_add per lookup: the immediate offset holds 16 bits)
+    constexpr uint32_t TABQ = AES_TAB2_BYTES / 16;
+    __shared__ u32x4 s_lds[TABQ + STG_WAVES * STG_GRAN];
     if (A.abort && *A.abort)
         return;
     // the S-box row of the table build sits in the image area
-    load_aes_tables<TAB4>(s_tab, (uint32_t *)&s_img[0][0]);
+    load_aes_tables<TAB4>(s_lds, (uint32_t *)(s_lds + TABQ));
     __syncthreads();
-    const AesLds T = make_aes_lds(s_tab);
+    const AesLds T = make_aes_lds(s_lds);
     LaneKey<NR> rk;
     const IcmFused &F = A.fz;
     FzLane z;
@@ -1459,7 +1463,7 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
     z.bw_idx = 0;
     z.bw_bits = 0;
     const uint32_t L = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    u32x4 *img = s_img[wv];
+    u32x4 *img = s_lds + TABQ + wv * STG_GRAN;
     constexpr uint32_t vid = icm_vid<NR, AUTH>();
     const uint32_t nw = gridDim.x * STG_WAVES;
     const uint32_t wid = blockIdx.x * STG_WAVES + wv;
