@@ -1351,11 +1351,37 @@ DEV void stg_chunks(const IcmPkt &p, const CtrCache &C, const KEY &rk,
         stg_chunk<S, NR, AUTH, PROTECT>(b, p, C, rk, T, ks_prev, hst, I);
 }
 
+// The per-packet words of a key record (srtp_dev_key_t): loaded for the
+// lane's last stream before the group's image arrives (one wait for both),
+// again after the classification only when the packet has another key
+struct StgKey {
+    uint32_t slot;
+    uint32_t salt[4], ipad[5], opad[5];
+    uint32_t tag_len, mki_size, conf;
+    DEV void load(const srtp_dev_key_t *keys, uint32_t s)
+    {
+        const srtp_dev_key_t *k = keys + s;
+        slot = s;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            salt[j] = k->salt[j];
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            ipad[j] = k->ipad[j];
+            opad[j] = k->opad[j];
+        }
+        tag_len = k->tag_len;
+        mki_size = k->mki_size;
+        conf = k->conf;
+    }
+};
+
 // one packet out of the image (icm_packet restated over it); returns the
 // tag verdict (unprotect; true on protect)
 template <int NR, bool AUTH, bool PROTECT>
 DEV bool stg_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
-                    const StgImg &I, const AesLds &T, LaneKey<NR> &rk)
+                    const StgKey &K, const StgImg &I, const AesLds &T,
+                    LaneKey<NR> &rk)
 {
     constexpr bool TAB4 = false;
     const uint32_t slot = m.key;
@@ -1372,21 +1398,21 @@ DEV bool stg_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
     p.qoff = p.hw >> 2;
     p.P = p.L - enc_start;
     p.roc = m.roc;
-    p.conf = key->conf != 0;
+    p.conf = K.conf != 0;
     p.nq = (p.L + 15) >> 4;
     p.nb = AUTH ? ((p.L + 12) >> 6) + 1 : ((p.nq + 3) >> 2);
     p.bclean = (p.qoff + 4) >> 2;
     // counter block (aes_icm.c:236-258, srtp.c:2694-2707)
     const uint32_t seq = bswap(I.ldw(0)) & 0xffffu;
-    p.cb[0] = key->salt[0];
-    p.cb[1] = key->salt[1] ^ I.ldw(8);   // SSRC bytes
-    p.cb[2] = key->salt[2] ^ bswap(m.roc);
-    p.cb[3] = key->salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
+    p.cb[0] = K.salt[0];
+    p.cb[1] = K.salt[1] ^ I.ldw(8);   // SSRC bytes
+    p.cb[2] = K.salt[2] ^ bswap(m.roc);
+    p.cb[3] = K.salt[3] ^ (seq >> 8) ^ ((seq & 0xffu) << 8);
 
     uint32_t hst[5];
 #pragma unroll
     for (int k = 0; k < 5; k++)
-        hst[k] = AUTH ? key->ipad[k] : 0;
+        hst[k] = AUTH ? K.ipad[k] : 0;
     CtrCache C{};
     if (p.conf)
         C = ctr_cache<NR, TAB4>(p.cb, rk, T);
@@ -1397,8 +1423,8 @@ DEV bool stg_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
     default: stg_chunks<3, NR, AUTH, PROTECT>(p, C, rk, T, hst, I); break;
     }
 
-    const uint32_t tag_len = key->tag_len;
-    const uint32_t mki_size = key->mki_size;
+    const uint32_t tag_len = K.tag_len;
+    const uint32_t mki_size = K.mki_size;
     if (!AUTH) {
         if (PROTECT && mki_size) {
             for (uint32_t u = 0; u < mki_size; u++)
@@ -1419,7 +1445,7 @@ DEV bool stg_packet(const IcmArgs &A, const srtp_dev_meta_t &m,
     uint32_t oh[5];
 #pragma unroll
     for (int k = 0; k < 5; k++)
-        oh[k] = key->opad[k];
+        oh[k] = K.opad[k];
     sha1_compress(oh, ow);
     uint32_t tw[5];
 #pragma unroll
@@ -1475,12 +1501,27 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
 #pragma unroll
     for (uint32_t j = 0; j < STG_GRAN / 64; j++)
         fr |= (stg_swz(64 * j + L) ^ (64 * j + L)) << (2 * j);
+    // the group's offset, length and capacity, loaded one group ahead
+    uint64_t n_off = 0;
+    uint32_t n_len = 0, n_cap = 0;
+    if (64 * wid + L < A.n) {
+        n_off = A.in_off[64 * wid + L];
+        n_len = F.in_len[64 * wid + L];
+        n_cap = F.cap[64 * wid + L];
+    }
     for (uint32_t g = wid; 64ull * g < A.n; g += nw) {
         const uint32_t i = 64 * g + L;
         const bool live = i < A.n;
-        const uint64_t off = live ? A.in_off[i] : 0;
-        const uint32_t len = live ? F.in_len[i] : 0;
-        const uint32_t cap = live ? F.cap[i] : 0;
+        const uint64_t off = n_off;
+        const uint32_t len = n_len, cap = n_cap;
+        {
+            const uint64_t i2 = 64ull * (g + nw) + L;
+            if (i2 < A.n) {
+                n_off = A.in_off[i2];
+                n_len = F.in_len[i2];
+                n_cap = F.cap[i2];
+            }
+        }
         // the group's slots tile one span: off = off0 + L * D
         const uint32_t olo = (uint32_t)off, ohi = (uint32_t)(off >> 32);
         const uint64_t off0 =
@@ -1514,6 +1555,9 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
                     (const void __attribute__((address_space(1))) *)(span + 16ull * ((64 * j + L) ^ ((fr >> (2 * j)) & 3))),
                     (void __attribute__((address_space(3))) *)(img + 64 * j), 16, 0, 0);
         }
+        // the key words of the lane's last stream, under the same wait
+        StgKey K;
+        K.load(A.keys, z.sid != FZ_NOCHAIN ? z.key : 0u);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t k0 = (L * D) >> 4;
         const StgImg I{ img + k0, (k0 / 48) & 3, D, A.in + off };
@@ -1529,8 +1573,10 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
         const bool run = SRTP_META_STATUS(m.info) == 0 &&
                          SRTP_META_VARIANT(m.info) == vid;
         bool ok = false;
+        if (run && m.key != K.slot)
+            K.load(A.keys, m.key);
         if (run)
-            ok = stg_packet<NR, AUTH, PROTECT>(A, m, I, T, rk);
+            ok = stg_packet<NR, AUTH, PROTECT>(A, m, K, I, T, rk);
         if (!PROTECT && run && A.auth_ok)
             A.auth_ok[i] = ok ? 1 : 0;
         if (!PROTECT && sid != FZ_NOCHAIN)
