@@ -224,14 +224,17 @@ int srtp_gpu_parse(srtp_gpu_t *g, size_t n, const uint8_t *in,
  * the GPU advances it, and the host pulls it back before any host-side use
  * of stream state. */
 enum {
-    SRTP_DS_ELIGIBLE = 1,    /* protect: sender/unknown direction, no
-                                pending ROC (MKI: the devtab's key index) */
+    SRTP_DS_ELIGIBLE = 1,    /* protect: sender/unknown direction (MKI: the
+                                devtab's key index) */
     SRTP_DS_ICM_CONF = 2,    /* AES-ICM encrypting: 2^16 keystream blocks */
-    SRTP_DS_RX_ELIGIBLE = 4, /* unprotect: receiver/unknown direction, no
-                                pending ROC (MKI: packets carrying another
-                                key's MKI abort to the host) */
-    SRTP_DS_AEAD = 8         /* AES-GCM: key usage counted before the tag
+    SRTP_DS_RX_ELIGIBLE = 4, /* unprotect: receiver/unknown direction (MKI:
+                                packets carrying another key's MKI abort to
+                                the host) */
+    SRTP_DS_AEAD = 8,        /* AES-GCM: key usage counted before the tag
                                 check (srtp.c:2390-2406) */
+    SRTP_DS_PENDING = 16     /* a ROC set by srtp_stream_set_roc is pending
+                                (its value in srtp_dev_stream_t.rsv): the host
+                                resolves it per batch (srtp_gpu_pp_pend_*) */
 };
 /* srtp_dev_stream_t.dir: directions the device batches used the stream in */
 enum { SRTP_DIR_TX = 1, SRTP_DIR_RX = 2 };
@@ -250,7 +253,7 @@ typedef struct srtp_dev_stream {
                            srtp.c:1961-2016); 0 without MKI.  `key` is the
                            slot of the key device batches use (the host's
                            devtab mki_j-th master key)                     */
-    uint32_t rsv;
+    uint32_t rsv;       /* SRTP_DS_PENDING: the pending ROC                   */
     uint64_t index;     /* rdbx index (ROC << 16 | SEQ)                      */
     uint64_t uses;      /* packets charged to the key since the upload       */
 } srtp_dev_stream_t;
@@ -293,6 +296,40 @@ typedef struct srtp_gpu_pp_batch {
  * 4 sequence outside the chain domain (bits may combine). */
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback);
+
+/* Pending ROCs (srtp_stream_set_roc, srtp.c:5137-5167): while a stream's
+ * ROC is pending, a packet's index is pending_roc || seq (srtp.c:2038-2081),
+ * and the first packet more than 2^15 past the stored index sets the index
+ * and window to it and clears the pending ROC (2674-2678 protect,
+ * 3161-3167 unprotect, after the tag).  Per batch, for the pending streams
+ * `sids` (device stream ids), srtp_gpu_pp_pend_scan finds in batch order
+ * the first packet that reaches the index estimate (protect: header, length
+ * and capacity checks passed) and the lowest / highest pending_roc || seq
+ * of the stream's packets.  The host decides; for a stream whose first
+ * packet advances, srtp_gpu_pp_pend_apply gives the device the state from
+ * which the normal order-free / chain forms reproduce the reference: index
+ * = that packet's index - 1, an empty window, no pending ROC (the packet
+ * then advances by one and sets its bit, as srtp_rdbx_set_roc_seq +
+ * srtp_rdbx_add_index(0) do).  srtp_gpu_pp_pend_restore takes the applied
+ * records back (a declined batch); srtp_gpu_pp_pend_clear forgets them (a
+ * committed batch).  On unprotect every applied stream's first packet must
+ * authenticate (else the reference would keep the ROC pending): the
+ * pre-pass aborts the batch to the host when one does not. */
+typedef struct srtp_pend_info {
+    uint32_t first;     /* batch position of the first packet, ~0 if none   */
+    uint32_t rsv;
+    uint64_t efirst;    /* its pending_roc || seq                            */
+    uint64_t emin, emax;/* over the stream's packets                         */
+    uint64_t index;     /* the device's stored index of the stream           */
+} srtp_pend_info_t;
+int srtp_gpu_pp_pend_scan(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+                          int unprotect, const uint32_t *sids, uint32_t np,
+                          srtp_pend_info_t *out);
+int srtp_gpu_pp_pend_apply(srtp_gpu_t *g, const uint32_t *sids,
+                           const uint64_t *efirst, const uint32_t *first,
+                           uint32_t nr, void *stream);
+int srtp_gpu_pp_pend_restore(srtp_gpu_t *g, void *stream);
+void srtp_gpu_pp_pend_clear(srtp_gpu_t *g);
 
 /* pre-pass + crypto + commit for unprotect (the order-free form only: per
  * stream every index above the stored one and within one replay window of

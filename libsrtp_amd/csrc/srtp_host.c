@@ -207,6 +207,10 @@ typedef struct {
     int has_mki;
     uint32_t mki_j;
     uint32_t rx_hint;
+    /* streams with a pending ROC (srtp_stream_set_roc) the device may take:
+     * resolved per batch (pend_resolve); the ones the running batch applied */
+    uint32_t *pend, npend;
+    uint32_t *res, nres;
 } devtab_t;
 
 struct srtp_ctx_t_ {
@@ -1475,6 +1479,8 @@ srtp_err_status_t srtp_dealloc(srtp_t ctx)
     free(ctx->dt.sv);
     free(ctx->dt.hs);
     free(ctx->dt.hwin);
+    free(ctx->dt.pend);
+    free(ctx->dt.res);
     free(ctx->kq);
     free(ctx->rel);
     routed_reset(ctx);
@@ -3297,6 +3303,11 @@ static int dev_build(srtp_t ctx)
     free(dt->sv);
     free(dt->hs);
     free(dt->hwin);
+    free(dt->pend);
+    free(dt->res);
+    dt->pend = (uint32_t *)malloc((ns + 1) * sizeof(uint32_t));
+    dt->res = (uint32_t *)malloc((ns + 1) * sizeof(uint32_t));
+    dt->npend = dt->nres = 0;
     dt->sv = (srtp_stream_ctx_t **)calloc(ns + 1, sizeof(void *));
     dt->hs = (srtp_dev_stream_t *)calloc(ns + 1, sizeof(srtp_dev_stream_t));
     dt->hwin = (uint32_t *)calloc(nwords + 1, 4);
@@ -3304,7 +3315,8 @@ static int dev_build(srtp_t ctx)
     uint32_t *hk = (uint32_t *)calloc(hcap, 4);
     uint32_t *hv = (uint32_t *)malloc(hcap * 4);
     int rc = -1;
-    if (!dt->sv || !dt->hs || !dt->hwin || !hk || !hv)
+    if (!dt->sv || !dt->hs || !dt->hwin || !hk || !hv || !dt->pend ||
+        !dt->res)
         goto out;
     dt->num_left_min = UINT64_MAX;
     dt->uniform = dt->rx_uniform = 0xffffffffu;
@@ -3334,10 +3346,15 @@ static int dev_build(srtp_t ctx)
             d->mki = (uint32_t)st->mki_size | (back << 16);
         }
         /* header-extension encryption / cryptex streams and routed keys:
-         * host pre-pass */
+         * host pre-pass.  A pending ROC is resolved per batch
+         * (pend_resolve) */
         const int xs = k->variant >= SRTP_VARIANT_X;
-        if (mki_ok && st->rdbx.pending_roc == 0 && !xs &&
-            st->direction != DIR_RECEIVER) {
+        if (st->rdbx.pending_roc && mki_ok && !xs) {
+            d->flags |= SRTP_DS_PENDING;
+            d->rsv = st->rdbx.pending_roc;
+            dt->pend[dt->npend++] = sid;
+        }
+        if (mki_ok && !xs && st->direction != DIR_RECEIVER) {
             d->flags |= SRTP_DS_ELIGIBLE;
             if (k->num_left < dt->num_left_min)
                 dt->num_left_min = k->num_left;
@@ -3352,8 +3369,7 @@ static int dev_build(srtp_t ctx)
             if (tr > dt->max_trailer)
                 dt->max_trailer = tr;
         }
-        if (mki_ok && st->rdbx.pending_roc == 0 && !xs &&
-            st->direction != DIR_SENDER) {
+        if (mki_ok && !xs && st->direction != DIR_SENDER) {
             d->flags |= SRTP_DS_RX_ELIGIBLE;
             if (k->num_left < dt->num_left_min)
                 dt->num_left_min = k->num_left;
@@ -3508,6 +3524,96 @@ static void dev_pull(srtp_t ctx)
     }
 }
 
+/* Pending ROCs (srtp_stream_set_roc; srtp.c:2038-2081, 5137-5167) of the
+ * streams the device may take, resolved for this batch from the first
+ * packet of each (srtp_dev.h srtp_gpu_pp_pend_*), in the reference's
+ * per-packet terms:
+ *   * the first packet's index pending_roc || seq more than 2^15 past the
+ *     stored index: it sets index and window and clears the pending ROC
+ *     (srtp.c:2674-2678, 3161-3167) -- the device gets the state one packet
+ *     earlier and runs the stream as any other; the host clears the pending
+ *     ROC when the batch commits;
+ *   * every packet's pending_roc || seq within 2^15 of the stored index and
+ *     of each other: each is the index the normal estimate gives, none
+ *     advances past or falls behind the window by 2^15 -- the device runs
+ *     it unchanged and the ROC stays pending;
+ *   * anything else (a first packet 2^15 behind: pkt_idx_old, and the
+ *     ROC stays pending for the next packet): the host path.
+ * Returns 0 (the device may run the batch), 1 (host path), -1 (error). */
+static int pend_resolve(srtp_t ctx, const srtp_gpu_pp_batch_t *pb,
+                        int unprotect)
+{
+    devtab_t *dt = &ctx->dt;
+    dt->nres = 0;
+    if (!dt->npend)
+        return 0;
+    srtp_pend_info_t *inf =
+        (srtp_pend_info_t *)malloc(dt->npend * sizeof *inf);
+    uint64_t *ef = (uint64_t *)malloc(dt->npend * sizeof *ef);
+    uint32_t *fp = (uint32_t *)malloc(dt->npend * sizeof *fp);
+    int rc = -1;
+    if (!inf || !ef || !fp ||
+        srtp_gpu_pp_pend_scan(ctx->gpu, pb, unprotect, dt->pend, dt->npend,
+                              inf))
+        goto out;
+    rc = 0;
+    for (uint32_t k = 0; k < dt->npend && !rc; k++) {
+        const srtp_pend_info_t *r = &inf[k];
+        if (r->first == 0xffffffffu)
+            continue;   /* no packet of the stream: the ROC stays pending */
+        const uint64_t I0 = r->index, e1 = r->efirst;
+        if (e1 > I0 && e1 - I0 > SEQ_MEDIAN) {
+            dt->res[dt->nres] = dt->pend[k];
+            ef[dt->nres] = e1;
+            fp[dt->nres] = r->first;
+            dt->nres++;
+        } else if (!(r->emax - r->emin < SEQ_MEDIAN &&
+                     (r->emax <= I0 || r->emax - I0 < SEQ_MEDIAN) &&
+                     (r->emin >= I0 || I0 - r->emin < SEQ_MEDIAN))) {
+            rc = 1;
+        }
+    }
+    if (!rc && dt->nres &&
+        srtp_gpu_pp_pend_apply(ctx->gpu, dt->res, ef, fp, dt->nres,
+                               pb->stream))
+        rc = -1;
+    if (rc)
+        dt->nres = 0;
+    if (rc == 1)
+        dt->last_abort = 1024;
+out:
+    free(inf);
+    free(ef);
+    free(fp);
+    return rc;
+}
+
+/* after the pre-pass: committed (the applied streams' ROCs are no longer
+ * pending) or declined (their device records back) */
+static int pend_settle(srtp_t ctx, int committed, void *stream)
+{
+    devtab_t *dt = &ctx->dt;
+    if (!dt->nres)
+        return 0;
+    int rc = 0;
+    if (committed) {
+        srtp_gpu_pp_pend_clear(ctx->gpu);
+        for (uint32_t k = 0; k < dt->nres; k++) {
+            const uint32_t sid = dt->res[k];
+            dt->sv[sid]->rdbx.pending_roc = 0;
+            for (uint32_t j = 0; j < dt->npend; j++)
+                if (dt->pend[j] == sid) {
+                    dt->pend[j] = dt->pend[--dt->npend];
+                    break;
+                }
+        }
+    } else {
+        rc = srtp_gpu_pp_pend_restore(ctx->gpu, stream);
+    }
+    dt->nres = 0;
+    return rc;
+}
+
 /* the device pre-pass; returns 1 when the batch was completed on the GPU,
  * 0 when the host path must run it, -1 on a device error */
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
@@ -3552,9 +3658,14 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
                   (dt->mask & 0xfc00u) == dt->mask && dt->max_trailer <= 16 &&
                   !async;
     pb.max_trailer = dt->max_trailer;
+    const int pr = pend_resolve(ctx, &pb, 0);
+    if (pr)
+        return pr < 0 ? -1 : 0;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))
+        return -1;
+    if (pend_settle(ctx, !fallback, b->stream))
         return -1;
     if (fallback) {
         dt->last_abort = fallback;
@@ -3683,9 +3794,14 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
                   dt->rx_uniform == 0xffffffffu && dt->rx_mask &&
                   (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
                   (dt->rx_mask & 0xfc00u) == dt->rx_mask;
+    const int pr = pend_resolve(ctx, &pb, 1);
+    if (pr)
+        return pr < 0 ? -1 : 0;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (srtp_gpu_pp_unprotect(ctx->gpu, &pb, &fallback))
+        return -1;
+    if (pend_settle(ctx, !fallback, b->stream))
         return -1;
     if (fallback) {
         dt->last_abort = fallback;

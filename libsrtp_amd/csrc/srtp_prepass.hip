@@ -68,7 +68,9 @@ constexpr uint32_t NOCHAIN = 0xffffffffu;
 enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4,
        AB_ORDER = 8, /* order-free form does not apply: sorted path */
        AB_STATIC = 16, /* unprotect: a packet with a length/capacity error */
-       AB_MKI = 32 /* unprotect: a packet whose MKI is not the device key's */ };
+       AB_MKI = 32, /* unprotect: a packet whose MKI is not the device key's */
+       AB_PENDING = 512 /* unprotect: the first packet of a stream whose
+                           pending ROC it resolved did not authenticate */ };
 
 struct PpState {
     // stream table
@@ -134,6 +136,23 @@ struct PpState {
     unsigned long long *fz_hicand = nullptr;   // unprotect: highest candidate
     uint32_t *fz_nfail = nullptr;              // unprotect: failed tag checks
     uint32_t *fz_glist = nullptr;              // k_icm_stg's per-lane groups
+    // pending ROCs (srtp_gpu_pp_pend_*): per stream the first packet and the
+    // lowest / highest pending index; the listed streams, their results;
+    // the records and windows an apply replaced, its streams' first packets
+    uint32_t *pd_first = nullptr;
+    unsigned long long *pd_min = nullptr, *pd_max = nullptr;
+    uint32_t pd_cap = 0, pd_cap2 = 0, pd_cap3 = 0;
+    uint32_t *pd_sids = nullptr;
+    srtp_pend_info_t *pd_info = nullptr;
+    uint64_t *pd_efirst = nullptr;
+    uint32_t pd_list_cap = 0, pd_list_cap2 = 0, pd_list_cap3 = 0;
+    srtp_dev_stream_t *pd_bak = nullptr;
+    uint32_t pd_bak_cap = 0;
+    uint32_t *pd_bakwin = nullptr;
+    uint32_t pd_bakwin_cap = 0;
+    uint32_t *pd_pos = nullptr;                // applied: first packets
+    uint32_t pd_pos_cap = 0;
+    uint32_t pd_nres = 0;                      // applied streams (0: none)
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -680,6 +699,128 @@ __global__ void k_pp_tail_restore(uint8_t *arena, const uint64_t *off,
     uint8_t *t = arena + off[i] + len;
     for (uint32_t b = 0; b < tn && b < 16; b++)
         t[b] = (uint8_t)(tsave[i][b >> 2] >> (8 * (b & 3)));
+}
+
+// ---------------------------------------------------------------------------
+// Pending ROCs (srtp_dev.h srtp_gpu_pp_pend_*; srtp.c:2038-2081, 2674-2678,
+// 3161-3167, 5137-5167)
+__global__ void k_pend_reset(const uint32_t *sids, uint32_t np, uint32_t *first,
+                             unsigned long long *emin, unsigned long long *emax)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= np)
+        return;
+    const uint32_t s = sids[k];
+    first[s] = NOCHAIN;
+    emin[s] = ~0ull;
+    emax[s] = 0;
+}
+
+// every packet of a pending stream that reaches the index estimate: its
+// position (the first in batch order wins) and pending_roc || seq.  Protect:
+// the header parses, the capacity holds the trailer and the header the
+// length (srtp_host.c pre_protect, srtp.c:2515-2600; fz_classify's order);
+// unprotect: the header parses (a packet failing a length check sends the
+// batch to the host in every device form)
+__global__ void k_pend_scan(const uint8_t *in, const uint64_t *in_off,
+                            const uint32_t *in_len, const uint32_t *cap,
+                            const srtp_dev_stream_t *st, const uint32_t *hkey,
+                            const uint32_t *hval, uint32_t hmask, uint32_t n,
+                            int unprotect, uint32_t *first,
+                            unsigned long long *emin, unsigned long long *emax)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t off = in_off[i];
+    const uint32_t len = in_len[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, len);
+    if (h.enc_start >> 24)
+        return;
+    const uint32_t sid = srtp_map_lookup(hkey, hval, hmask, h.ssrc);
+    if (sid == NOCHAIN)
+        return;
+    const srtp_dev_stream_t &S = st[sid];
+    if (!(S.flags & SRTP_DS_PENDING))
+        return;
+    if (!unprotect && (cap[i] < len + S.trailer || h.enc_start > len))
+        return;
+    const uint64_t e = ((uint64_t)S.rsv << 16) | (h.seq_len & 0xffffu);
+    atomicMin(&first[sid], i);
+    atomicMin(&emin[sid], (unsigned long long)e);
+    atomicMax(&emax[sid], (unsigned long long)e);
+}
+
+__global__ void k_pend_gather(const uint32_t *sids, uint32_t np,
+                              const uint8_t *in, const uint64_t *in_off,
+                              const srtp_dev_stream_t *st, const uint32_t *first,
+                              const unsigned long long *emin,
+                              const unsigned long long *emax,
+                              srtp_pend_info_t *out)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= np)
+        return;
+    const uint32_t s = sids[k], f = first[s];
+    srtp_pend_info_t r;
+    r.first = f;
+    r.rsv = 0;
+    r.efirst = 0;
+    r.emin = emin[s];
+    r.emax = emax[s];
+    r.index = st[s].index;
+    if (f != NOCHAIN) {
+        const uint32_t w0 = srtp_bswap32(*(const uint32_t *)(in + in_off[f]));
+        r.efirst = ((uint64_t)st[s].rsv << 16) | (w0 & 0xffffu);
+    }
+    out[k] = r;
+}
+
+// the state after the first packet's reset, one packet earlier: index - 1,
+// an empty window, no pending ROC; the replaced record and window kept
+__global__ void k_pend_apply(const uint32_t *sids, const uint64_t *efirst,
+                             uint32_t nr, srtp_dev_stream_t *st, uint32_t *win,
+                             srtp_dev_stream_t *bak, uint32_t *bakwin)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nr)
+        return;
+    const uint32_t s = sids[k];
+    srtp_dev_stream_t S = st[s];
+    bak[k] = S;
+    const uint32_t words = S.win_bits >> 5;
+    for (uint32_t w = 0; w < words; w++) {
+        bakwin[S.win_off + w] = win[S.win_off + w];
+        win[S.win_off + w] = 0;
+    }
+    S.index = efirst[k] - 1;
+    S.flags &= ~(uint32_t)SRTP_DS_PENDING;
+    S.rsv = 0;
+    st[s] = S;
+}
+
+__global__ void k_pend_restore(const uint32_t *sids, uint32_t nr,
+                               srtp_dev_stream_t *st, uint32_t *win,
+                               const srtp_dev_stream_t *bak,
+                               const uint32_t *bakwin)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nr)
+        return;
+    const srtp_dev_stream_t S = bak[k];
+    st[sids[k]] = S;
+    const uint32_t words = S.win_bits >> 5;
+    for (uint32_t w = 0; w < words; w++)
+        win[S.win_off + w] = bakwin[S.win_off + w];
+}
+
+// unprotect: an applied stream's first packet must authenticate
+__global__ void k_pend_authchk(const uint32_t *pos, uint32_t nr,
+                               const uint8_t *auth, uint32_t *abort)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < nr && !auth[pos[k]])
+        atomicOr(abort, (uint32_t)AB_PENDING);
 }
 
 // Fused order-free form (IcmFused): the per-stream aggregates start at
@@ -2470,7 +2611,9 @@ void srtp_gpu_pp_free(void *p)
                      P->ch_ctl, P->ch_abort, P->pu_ctl, P->pu_tile,
                      P->pu_first, P->fzrec, P->tsave, P->fz_cnt,
                      P->fz_emin, P->fz_bmap, P->fz_hicand, P->fz_nfail,
-                     P->fz_glist };
+                     P->fz_glist, P->pd_first, P->pd_min, P->pd_max,
+                     P->pd_sids, P->pd_info, P->pd_efirst, P->pd_bak,
+                     P->pd_bakwin, P->pd_pos };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2559,6 +2702,90 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
     PPCHK(hipStreamSynchronize(stream));
     return 0;
 }
+
+int srtp_gpu_pp_pend_scan(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+                          int unprotect, const uint32_t *sids, uint32_t np,
+                          srtp_pend_info_t *out)
+{
+    PpState *P = pp_of(g);
+    hipStream_t stream = (hipStream_t)b->stream;
+    if (!np || !P->st)
+        return 0;
+    if (regrow(&P->pd_first, &P->pd_cap, P->ns + 1) ||
+        regrow(&P->pd_min, &P->pd_cap2, P->ns + 1) ||
+        regrow(&P->pd_max, &P->pd_cap3, P->ns + 1) ||
+        regrow(&P->pd_sids, &P->pd_list_cap, np) ||
+        regrow(&P->pd_info, &P->pd_list_cap2, np))
+        return -1;
+    PPCHK(hipMemcpyAsync(P->pd_sids, sids, np * 4ull, hipMemcpyHostToDevice,
+                         stream));
+    const dim3 blk(256), gl((np + 255) / 256);
+    hipLaunchKernelGGL(k_pend_reset, gl, blk, 0, stream, P->pd_sids, np,
+                       P->pd_first, P->pd_min, P->pd_max);
+    const uint32_t N = (uint32_t)b->n;
+    if (N)
+        hipLaunchKernelGGL(k_pend_scan, dim3((N + 255) / 256), blk, 0, stream,
+                           b->in, b->in_off, b->in_len, b->out_len, P->st,
+                           P->hkey, P->hval, P->hcap - 1, N, unprotect,
+                           P->pd_first, P->pd_min, P->pd_max);
+    hipLaunchKernelGGL(k_pend_gather, gl, blk, 0, stream, P->pd_sids, np, b->in,
+                       b->in_off, P->st, P->pd_first, P->pd_min, P->pd_max,
+                       P->pd_info);
+    PPCHK(hipGetLastError());
+    PPCHK(hipMemcpyAsync(out, P->pd_info, np * sizeof *out,
+                         hipMemcpyDeviceToHost, stream));
+    PPCHK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+int srtp_gpu_pp_pend_apply(srtp_gpu_t *g, const uint32_t *sids,
+                           const uint64_t *efirst, const uint32_t *first,
+                           uint32_t nr, void *stream_)
+{
+    PpState *P = pp_of(g);
+    hipStream_t stream = (hipStream_t)stream_;
+    P->pd_nres = 0;
+    if (!nr)
+        return 0;
+    if (regrow(&P->pd_sids, &P->pd_list_cap, nr) ||
+        regrow(&P->pd_efirst, &P->pd_list_cap3, nr) ||
+        regrow(&P->pd_pos, &P->pd_pos_cap, nr) ||
+        regrow(&P->pd_bak, &P->pd_bak_cap, nr) ||
+        regrow(&P->pd_bakwin, &P->pd_bakwin_cap, P->nwords + 1))
+        return -1;
+    PPCHK(hipMemcpyAsync(P->pd_sids, sids, nr * 4ull, hipMemcpyHostToDevice,
+                         stream));
+    PPCHK(hipMemcpyAsync(P->pd_efirst, efirst, nr * 8ull,
+                         hipMemcpyHostToDevice, stream));
+    PPCHK(hipMemcpyAsync(P->pd_pos, first, nr * 4ull, hipMemcpyHostToDevice,
+                         stream));
+    hipLaunchKernelGGL(k_pend_apply, dim3((nr + 255) / 256), dim3(256), 0,
+                       stream, P->pd_sids, P->pd_efirst, nr, P->st, P->win,
+                       P->pd_bak, P->pd_bakwin);
+    PPCHK(hipGetLastError());
+    // the host arrays are the caller's stack: the copies complete first
+    PPCHK(hipStreamSynchronize(stream));
+    P->pd_nres = nr;
+    return 0;
+}
+
+int srtp_gpu_pp_pend_restore(srtp_gpu_t *g, void *stream_)
+{
+    PpState *P = pp_of(g);
+    hipStream_t stream = (hipStream_t)stream_;
+    const uint32_t nr = P->pd_nres;
+    P->pd_nres = 0;
+    if (!nr)
+        return 0;
+    hipLaunchKernelGGL(k_pend_restore, dim3((nr + 255) / 256), dim3(256), 0,
+                       stream, P->pd_sids, nr, P->st, P->win, P->pd_bak,
+                       P->pd_bakwin);
+    PPCHK(hipGetLastError());
+    PPCHK(hipStreamSynchronize(stream));
+    return 0;
+}
+
+void srtp_gpu_pp_pend_clear(srtp_gpu_t *g) { pp_of(g)->pd_nres = 0; }
 
 // 48-bit index of every sorted position: the segmented sum of the advances
 // by stream.  One stream: its chain packets come first and every other
@@ -3158,6 +3385,10 @@ static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
     if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "pu_crypto"))
         return pu1_fail(P, stream);
     const dim3 blk(256), gp((N + 255) / 256);
+    if (P->pd_nres)
+        hipLaunchKernelGGL(k_pend_authchk, dim3((P->pd_nres + 255) / 256), blk,
+                           0, stream, P->pd_pos, P->pd_nres, P->auth,
+                           &ctl->abort2);
     hipLaunchKernelGGL(k_pu_first, gp, blk, 0, stream, P->skey, P->est,
                        P->auth, N, ctl, P->pu_first, P->pu_first_cap,
                        P->pu_gen);
@@ -3272,6 +3503,9 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
     };
     if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "fused unprotect crypto"))
         return fail();
+    if (P->pd_nres)
+        hipLaunchKernelGGL(k_pend_authchk, dim3((P->pd_nres + 255) / 256), blk,
+                           0, stream, P->pd_pos, P->pd_nres, P->auth, P->abort);
     hipLaunchKernelGGL(k_fzu_stream, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
                        hi, P->fz_hicand, P->fz_emin, P->fz_bmap, F.bmap2,
                        P->win, P->wnew, P->abort);
@@ -3415,6 +3649,9 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
     if (pp_step(stream, "pu_crypto"))
         return -1;
+    if (P->pd_nres)
+        hipLaunchKernelGGL(k_pend_authchk, dim3((P->pd_nres + 255) / 256), blk,
+                           0, stream, P->pd_pos, P->pd_nres, P->auth, P->abort);
 
     if (!unordered) {
         hipLaunchKernelGGL(k_pu_accepted_est, gp, blk, 0, stream, P->skey2,

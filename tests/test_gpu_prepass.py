@@ -1072,7 +1072,112 @@ def test_fused_paths_ineligible_stream_of_another_variant():
                 rx = [snd.protect(p, len(p) + 32)[1] for p in pk]
                 _receive_check(lib, orc, rx)
         d, h = lib.prepass_stats()
-        assert h >= 1, (op, d, h)
+        # the pending ROC is resolved on the device (srtp_host.c
+        # pend_resolve): the set_roc batch stays there too
+        assert (d, h) == (2, 0), (op, d, h, lib.prepass_last_abort())
+
+
+def _pending_run(lib, orc, snd, op, pk, caps=None):
+    """one device batch in place against the oracle (protect: caps; receive:
+    the sender session `snd` protects pk first) -> statuses"""
+    if op == "protect":
+        caps = caps or [len(p) + 32 for p in pk]
+        st, out = _device_run(lib, pk, caps, "protect")
+        for i, p in enumerate(pk):
+            rc, ref = orc.protect(p, caps[i])
+            assert st[i] == rc, (i, st[i], rc)
+            assert rc or out[i] == ref, i
+        return st
+    rx = [snd.protect(p, len(p) + 32)[1] for p in pk]
+    return _receive_check(lib, orc, rx)
+
+
+@pytest.mark.parametrize("op", ["protect", "unprotect"])
+@pytest.mark.parametrize("shape", ["fused_many", "one_stream", "gcm_many"])
+def test_pending_roc_on_device(op, shape):
+    """srtp_stream_set_roc on running streams (srtp.c:5137-5167; the
+    estimate 2038-2081): a set ROC ahead of the stream's (its first packet
+    then resets index and window, 2674-2678 / 3161-3167) and a set ROC equal
+    to the current one (it stays pending: every estimate is pending_roc ||
+    seq), on the device pre-pass -- the AES-ICM kernel's fused order-free
+    form among 600 streams, the one-stream chain form, and the separate
+    order-free form (AES-GCM) -- bit-exact against the oracle's per-packet
+    srtp_protect / srtp_unprotect, no batch on the host path; a ROC set
+    below the stream's (the first packet 2^15 behind: pkt_idx_old) goes to
+    the host path, whose result the next device batch continues from"""
+    _gpu()
+    rng = random.Random(700 + len(shape) + len(op))
+    name = "gcm256_16" if shape == "gcm_many" else "icm128_hmac80"
+    ns = 1 if shape == "one_stream" else 600
+    ssrcs = [0x28000000 + 5 * k for k in range(ns)]
+    pols = [policy(name, ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    lib, orc, snd = L.Session(pols), O.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(0x9000, 0xf000) for s in ssrcs}
+    per = 200 if ns == 1 else 6
+    ahead, same = ssrcs[0], ssrcs[-1]
+    for b in range(4):
+        pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 20, 160))
+        if b == 1:
+            # ahead: ROC 5 set on a stream at ROC 0: its first packet resets
+            for sess in (lib, orc, snd):
+                assert sess.set_roc(ahead, 5) == 0
+        if b == 0 and ns > 1:
+            # a fresh stream (index 0) given ROC 3 before its first packet
+            for sess in (lib, orc, snd):
+                assert sess.set_roc(same, 3) == 0
+        if b == 2 and ns > 1:
+            # the same ROC again, while its packets stay within 2^15: it
+            # stays pending for the whole batch
+            for sess in (lib, orc, snd):
+                assert sess.set_roc(same, orc.get_roc(same)[1]) == 0
+        _pending_run(lib, orc, snd, op, pk)
+    d, h = lib.prepass_stats()
+    assert (d, h) == (4, 0), (d, h, lib.prepass_last_abort())
+    for s in (ahead, same):
+        assert lib.get_roc(s) == orc.get_roc(s), hex(s)
+    # a ROC below the stream's (the receiver's or the sender's own):
+    # pkt_idx_old from the host path (the sender keeps ROC 5)
+    for sess in (lib, orc):
+        assert sess.set_roc(ahead, 2) == 0
+    pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 20))
+    st = _pending_run(lib, orc, snd, op, pk)
+    assert lib.prepass_stats()[1] == 1
+    pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 20))
+    _pending_run(lib, orc, snd, op, pk)
+    assert lib.get_roc(ahead) == orc.get_roc(ahead)
+
+
+@pytest.mark.parametrize("shape", ["fused_many", "one_stream"])
+def test_pending_roc_forged_first_packet(shape):
+    """receive side: the first packet of a stream with a pending ROC does not
+    authenticate -- the reference keeps the ROC pending (the reset happens
+    only after the tag, srtp.c:3157-3167), so the device batch is declined
+    (AB_PENDING) and the host path decides: statuses and bytes equal to the
+    oracle's"""
+    _gpu()
+    rng = random.Random(720 + len(shape))
+    ns = 1 if shape == "one_stream" else 300
+    ssrcs = [0x29000000 + 3 * k for k in range(ns)]
+    pols = [policy("icm128_hmac80", ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    lib, orc, snd = L.Session(pols), O.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(0x100, 0xf000) for s in ssrcs}
+    per = 100 if ns == 1 else 5
+    pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 40))
+    _pending_run(lib, orc, snd, "unprotect", pk)
+    tgt = ssrcs[ns // 2]
+    for sess in (lib, orc, snd):
+        assert sess.set_roc(tgt, 9) == 0
+    pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 40))
+    rx = [snd.protect(p, len(p) + 32)[1] for p in pk]
+    first = next(i for i, p in enumerate(pk) if p[8:12] == tgt.to_bytes(4, "big"))
+    bad = bytearray(rx[first])
+    bad[-1] ^= 0x5a
+    rx[first] = bytes(bad)
+    d0, h0 = lib.prepass_stats()
+    st = _receive_check(lib, orc, rx)
+    assert st[first] == 7
+    assert lib.prepass_stats()[1] == h0 + 1, lib.prepass_last_abort()
+    assert lib.get_roc(tgt) == orc.get_roc(tgt)
 
 
 @pytest.mark.parametrize("declined", [False, True], ids=["clean", "declined"])
