@@ -259,13 +259,22 @@ typedef struct srtp_dev_stream {
 } srtp_dev_stream_t;
 
 /* the table: streams[ns], window arena (nwords), SSRC hash (hcap a power of
- * two, open addressing with the host's hash, hval ~0 = empty slot) */
+ * two, open addressing with the host's hash, hval ~0 = empty slot).
+ * Template sessions (ssrc_any_*; srtp_stream_clone, srtp.c:762-863, called
+ * from srtp.c:2540 protect and 3141 unprotect): `tmpl` is the template's
+ * record (ssrc unused; win_off the first of `spare` windows of
+ * tmpl->win_bits bits at the end of the arena, which `nwords` includes),
+ * and up to `spare` streams may be created on the device (srtp_gpu_pp_clone)
+ * as records ns, ns + 1, ...; tmpl NULL: none. */
 int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
                        uint32_t ns, const uint32_t *win, uint32_t nwords,
                        const uint32_t *hkey, const uint32_t *hval,
-                       uint32_t hcap);
+                       uint32_t hcap, const srtp_dev_stream_t *tmpl,
+                       uint32_t spare);
+/* the table back: *ns_now records (the uploaded ones, then the streams
+ * created on the device in creation order) and the whole window arena */
 int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
-                         uint32_t *win);
+                         uint32_t *win, uint32_t *ns_now);
 
 typedef struct srtp_gpu_pp_batch {
     size_t n;
@@ -296,6 +305,16 @@ typedef struct srtp_gpu_pp_batch {
  * 4 sequence outside the chain domain (bits may combine). */
 int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
                         int *fallback);
+
+/* Template clones: every packet of the batch whose SSRC has no stream gets
+ * one -- a record copied from the template (fresh index and window, no
+ * direction yet; the pre-pass that then runs sets SRTP_DIR_TX on protect
+ * and SRTP_DIR_RX on unprotect only when a packet of it authenticates,
+ * srtp.c:3117-3155) and an entry in the SSRC hash.  *added: streams created
+ * by this call.  Returns 1 when the spare records ran out (the batch must
+ * take the host path; the host rebuilds the table). */
+int srtp_gpu_pp_clone(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+                      uint32_t *added);
 
 /* Pending ROCs (srtp_stream_set_roc, srtp.c:5137-5167): while a stream's
  * ROC is pending, a packet's index is pending_roc || seq (srtp.c:2038-2081),

@@ -211,6 +211,9 @@ typedef struct {
      * resolved per batch (pend_resolve); the ones the running batch applied */
     uint32_t *pend, npend;
     uint32_t *res, nres;
+    /* template sessions: the device creates streams from the template
+     * (srtp_gpu_pp_clone); dev_pull takes them over */
+    int tmpl_ok;
 } devtab_t;
 
 struct srtp_ctx_t_ {
@@ -3291,6 +3294,71 @@ static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
 /* ------------------------------------------------------------------------
  * device stream table (DESIGN.md "Device pre-pass")
  * ---------------------------------------------------------------------- */
+/* the device record of stream st (or of the template: a clone's record,
+ * fresh, usable in both directions -- srtp.c:2540 makes a protect clone a
+ * sender, 3141 an unprotect clone a receiver), and the table's aggregates */
+static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
+                       srtp_dev_stream_t *d, int *first, int *rx_first)
+{
+    /* MKI streams: master key mki_j, ineligible if they have fewer */
+    const int mki_ok = !st->use_mki || dt->mki_j < st->keys->n;
+    const hkey_t *k = &st->keys->k[st->use_mki && mki_ok ? dt->mki_j : 0];
+    memset(d, 0, sizeof *d);
+    d->ssrc = st->ssrc;
+    d->key = k->slot;
+    d->variant = k->variant;
+    if (st->use_mki) {
+        dt->has_mki = 1;
+        const uint32_t back = (uint32_t)st->mki_size +
+            (k->family == SRTP_DEV_GCM ? 0u : (uint32_t)k->tag_len);
+        d->mki = (uint32_t)st->mki_size | (back << 16);
+    }
+    /* header-extension encryption / cryptex streams and routed keys: host
+     * pre-pass.  A pending ROC is resolved per batch (pend_resolve) */
+    const int xs = k->variant >= SRTP_VARIANT_X;
+    if (!templ && st->rdbx.pending_roc && mki_ok && !xs) {
+        d->flags |= SRTP_DS_PENDING;
+        d->rsv = st->rdbx.pending_roc;
+    }
+    if (mki_ok && !xs && (templ || st->direction != DIR_RECEIVER)) {
+        d->flags |= SRTP_DS_ELIGIBLE;
+        if (k->num_left < dt->num_left_min)
+            dt->num_left_min = k->num_left;
+        if (*first)
+            dt->uniform = k->slot;
+        else if (dt->uniform != k->slot)
+            dt->uniform = 0xffffffffu;
+        *first = 0;
+        dt->mask |= 1u << k->variant;
+        const uint32_t tr =
+            (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
+        if (tr > dt->max_trailer)
+            dt->max_trailer = tr;
+    }
+    if (mki_ok && !xs && (templ || st->direction != DIR_SENDER)) {
+        d->flags |= SRTP_DS_RX_ELIGIBLE;
+        if (k->num_left < dt->num_left_min)
+            dt->num_left_min = k->num_left;
+        if (*rx_first)
+            dt->rx_uniform = k->slot;
+        else if (dt->rx_uniform != k->slot)
+            dt->rx_uniform = 0xffffffffu;
+        *rx_first = 0;
+        dt->rx_mask |= 1u << k->variant;
+    }
+    if (k->family == SRTP_DEV_ICM && (st->rtp_services & sec_serv_conf))
+        d->flags |= SRTP_DS_ICM_CONF;
+    if (k->family == SRTP_DEV_GCM)
+        d->flags |= SRTP_DS_AEAD;
+    d->trailer = (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
+    d->win_bits = (uint32_t)st->rdbx.bits;
+    d->index = templ ? 0 : st->rdbx.index;
+}
+
+/* records of the streams the device may create from the template per
+ * upload (dev_pull takes them over) */
+#define DEV_SPARE_MIN 65536u
+
 static int dev_build(srtp_t ctx)
 {
     if (async_drain(ctx))
@@ -3300,6 +3368,13 @@ static int dev_build(srtp_t ctx)
     size_t nwords = 0;
     for (size_t i = 0; i < ctx->n; i++)
         nwords += ctx->list[i]->rdbx.bits / 32;
+    /* template sessions: spare records for the streams a batch creates */
+    srtp_stream_ctx_t *tp = ctx->templ;
+    const int tmpl_ok = tp && (!tp->use_mki || dt->mki_j < tp->keys->n) &&
+                        tp->keys->k[0].variant < SRTP_VARIANT_X;
+    const uint32_t spare = tmpl_ok ? (ns > DEV_SPARE_MIN ? ns : DEV_SPARE_MIN)
+                                   : 0;
+    const size_t tw = tmpl_ok ? tp->rdbx.bits / 32 : 0;
     free(dt->sv);
     free(dt->hs);
     free(dt->hwin);
@@ -3309,9 +3384,13 @@ static int dev_build(srtp_t ctx)
     dt->res = (uint32_t *)malloc((ns + 1) * sizeof(uint32_t));
     dt->npend = dt->nres = 0;
     dt->sv = (srtp_stream_ctx_t **)calloc(ns + 1, sizeof(void *));
-    dt->hs = (srtp_dev_stream_t *)calloc(ns + 1, sizeof(srtp_dev_stream_t));
-    dt->hwin = (uint32_t *)calloc(nwords + 1, 4);
+    dt->hs = (srtp_dev_stream_t *)calloc(ns + spare + 1,
+                                         sizeof(srtp_dev_stream_t));
+    dt->hwin = (uint32_t *)calloc(nwords + spare * tw + 1, 4);
+    /* the device hash holds the spare streams too: load <= 1/2 */
     size_t hcap = ctx->map.cap ? ctx->map.cap : 1;
+    while (hcap < 2 * ((size_t)ns + spare))
+        hcap *= 2;
     uint32_t *hk = (uint32_t *)calloc(hcap, 4);
     uint32_t *hv = (uint32_t *)malloc(hcap * 4);
     int rc = -1;
@@ -3327,84 +3406,40 @@ static int dev_build(srtp_t ctx)
     dt->has_mki = 0;
     for (uint32_t sid = 0; sid < ns; sid++) {
         srtp_stream_ctx_t *st = ctx->list[sid];
-        /* MKI streams: master key mki_j, ineligible if they have fewer */
-        const int mki_ok = !st->use_mki || dt->mki_j < st->keys->n;
-        const hkey_t *k = &st->keys->k[st->use_mki && mki_ok ? dt->mki_j : 0];
         srtp_dev_stream_t *d = &dt->hs[sid];
         dt->sv[sid] = st;
         st->dev_sid = sid;
-        d->ssrc = st->ssrc;
-        d->key = k->slot;
-        d->variant = k->variant;
-        d->flags = 0;
-        d->mki = 0;
-        d->rsv = 0;
-        if (st->use_mki) {
-            dt->has_mki = 1;
-            const uint32_t back = (uint32_t)st->mki_size +
-                (k->family == SRTP_DEV_GCM ? 0u : (uint32_t)k->tag_len);
-            d->mki = (uint32_t)st->mki_size | (back << 16);
-        }
-        /* header-extension encryption / cryptex streams and routed keys:
-         * host pre-pass.  A pending ROC is resolved per batch
-         * (pend_resolve) */
-        const int xs = k->variant >= SRTP_VARIANT_X;
-        if (st->rdbx.pending_roc && mki_ok && !xs) {
-            d->flags |= SRTP_DS_PENDING;
-            d->rsv = st->rdbx.pending_roc;
+        dev_record(dt, st, 0, d, &first, &rx_first);
+        if (d->flags & SRTP_DS_PENDING)
             dt->pend[dt->npend++] = sid;
-        }
-        if (mki_ok && !xs && st->direction != DIR_RECEIVER) {
-            d->flags |= SRTP_DS_ELIGIBLE;
-            if (k->num_left < dt->num_left_min)
-                dt->num_left_min = k->num_left;
-            if (first)
-                dt->uniform = k->slot;
-            else if (dt->uniform != k->slot)
-                dt->uniform = 0xffffffffu;
-            first = 0;
-            dt->mask |= 1u << k->variant;
-            const uint32_t tr =
-                (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
-            if (tr > dt->max_trailer)
-                dt->max_trailer = tr;
-        }
-        if (mki_ok && !xs && st->direction != DIR_SENDER) {
-            d->flags |= SRTP_DS_RX_ELIGIBLE;
-            if (k->num_left < dt->num_left_min)
-                dt->num_left_min = k->num_left;
-            if (rx_first)
-                dt->rx_uniform = k->slot;
-            else if (dt->rx_uniform != k->slot)
-                dt->rx_uniform = 0xffffffffu;
-            rx_first = 0;
-            dt->rx_mask |= 1u << k->variant;
-        }
-        if (k->family == SRTP_DEV_ICM && (st->rtp_services & sec_serv_conf))
-            d->flags |= SRTP_DS_ICM_CONF;
-        if (k->family == SRTP_DEV_GCM)
-            d->flags |= SRTP_DS_AEAD;
-        d->dir = 0;
-        d->trailer = (uint32_t)(k->tag_len + (st->use_mki ? st->mki_size : 0));
-        d->win_bits = (uint32_t)st->rdbx.bits;
         d->win_off = woff;
-        d->index = st->rdbx.index;
-        d->uses = 0;
         memcpy(dt->hwin + woff, st->rdbx.w, st->rdbx.bits / 8);
         woff += (uint32_t)(st->rdbx.bits / 32);
     }
-    for (size_t h = 0; h < hcap; h++) {
-        hv[h] = 0xffffffffu;
-        if (ctx->map.cap && ctx->map.vals[h]) {
-            hk[h] = ctx->map.keys[h];
-            hv[h] = ctx->map.vals[h]->dev_sid;
-        }
+    srtp_dev_stream_t td;
+    if (tmpl_ok) {
+        dev_record(dt, tp, 1, &td, &first, &rx_first);
+        td.win_off = woff;   /* the spare windows (zero) follow */
     }
-    if (srtp_gpu_pp_upload(ctx->gpu, dt->hs, ns, dt->hwin, woff, hk, hv,
-                           (uint32_t)hcap))
+    for (size_t h = 0; h < hcap; h++)
+        hv[h] = 0xffffffffu;
+    for (size_t h = 0; h < ctx->map.cap; h++) {
+        if (!ctx->map.vals[h])
+            continue;
+        const uint32_t key = ctx->map.keys[h];
+        size_t p = map_hash(key, hcap);
+        while (hv[p] != 0xffffffffu)
+            p = (p + 1) & (hcap - 1);
+        hk[p] = key;
+        hv[p] = ctx->map.vals[h]->dev_sid;
+    }
+    if (srtp_gpu_pp_upload(ctx->gpu, dt->hs, ns, dt->hwin,
+                           woff + (uint32_t)(spare * tw), hk, hv,
+                           (uint32_t)hcap, tmpl_ok ? &td : NULL, spare))
         goto out;
     dt->ns = ns;
     dt->nwords = woff;
+    dt->tmpl_ok = tmpl_ok;
     dt->uses_bound = 0;
     dt->valid = 1;
     dt->dirty = 0;
@@ -3505,7 +3540,8 @@ static void dev_pull(srtp_t ctx)
     if (!dt->dirty)
         return;
     dt->dirty = 0;
-    if (srtp_gpu_pp_download(ctx->gpu, dt->hs, dt->hwin)) {
+    uint32_t ns_now = 0;
+    if (srtp_gpu_pp_download(ctx->gpu, dt->hs, dt->hwin, &ns_now)) {
         log_msg(srtp_log_level_error, "device stream table download failed");
         return;
     }
@@ -3521,6 +3557,30 @@ static void dev_pull(srtp_t ctx)
             st->direction = DIR_SENDER;
         if (st->direction == DIR_UNKNOWN && (d->dir & SRTP_DIR_RX))
             st->direction = DIR_RECEIVER;
+    }
+    /* streams the device created from the template (srtp_gpu_pp_clone), in
+     * creation order: a protect clone is a sender (srtp.c:2540-2559); a
+     * receive clone exists once one of its packets authenticated
+     * (srtp.c:3117-3155) -- before that its packets ran on the template's
+     * keys, whose usage they still count (the clones share its limit,
+     * srtp_key_limit_clone) */
+    srtp_stream_ctx_t *tp = ctx->templ;
+    for (uint32_t sid = dt->ns; tp && sid < ns_now; sid++) {
+        const srtp_dev_stream_t *d = &dt->hs[sid];
+        tp->keys->k[tp->use_mki ? dt->mki_j : 0].num_left -= d->uses;
+        if (!(d->dir & (SRTP_DIR_TX | SRTP_DIR_RX)))
+            continue;
+        srtp_stream_ctx_t *st = stream_clone(tp, d->ssrc);
+        if (!st || list_insert(ctx, st)) {
+            if (st)
+                stream_free(ctx, st);
+            log_msg(srtp_log_level_error,
+                    "device-created stream: allocation failed");
+            continue;
+        }
+        st->direction = (d->dir & SRTP_DIR_TX) ? DIR_SENDER : DIR_RECEIVER;
+        st->rdbx.index = d->index;
+        memcpy(st->rdbx.w, dt->hwin + d->win_off, st->rdbx.bits / 8);
     }
 }
 
@@ -3614,13 +3674,50 @@ static int pend_settle(srtp_t ctx, int committed, void *stream)
     return rc;
 }
 
+/* the device pre-pass of a batch (srtp_gpu_pp_protect / _unprotect) with
+ * the pending ROCs resolved around it, and -- when the first run stopped at
+ * SSRCs without a stream and the session has a template -- those streams
+ * created on the device (srtp_gpu_pp_clone) and the batch run again.
+ * Returns -1 on a device error, else 0 with *fallback the abort reason
+ * (0: committed on the device). */
+static int pp_run(srtp_t ctx, srtp_gpu_pp_batch_t *pb, int unprotect,
+                  int *fallback)
+{
+    devtab_t *dt = &ctx->dt;
+    for (int round = 0;; round++) {
+        const int pr = pend_resolve(ctx, pb, unprotect);
+        if (pr < 0)
+            return -1;
+        if (pr) {
+            *fallback = 1024;
+            return 0;
+        }
+        int fb = 1;
+        if (unprotect ? srtp_gpu_pp_unprotect(ctx->gpu, pb, &fb)
+                      : srtp_gpu_pp_protect(ctx->gpu, pb, &fb))
+            return -1;
+        if (pend_settle(ctx, !fb, pb->stream))
+            return -1;
+        *fallback = fb;
+        if (round == 0 && (fb & 1) && dt->tmpl_ok) {
+            uint32_t added = 0;
+            const int c = srtp_gpu_pp_clone(ctx->gpu, pb, &added);
+            if (c < 0)
+                return -1;
+            if (c == 0 && added)
+                continue;
+        }
+        return 0;
+    }
+}
+
 /* the device pre-pass; returns 1 when the batch was completed on the GPU,
  * 0 when the host path must run it, -1 on a device error */
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
                                int async, const size_t *mki_wide)
 {
     devtab_t *dt = &ctx->dt;
-    if (!ctx->n || b->n > 0x7fffffffu) {
+    if ((!ctx->n && !ctx->templ) || b->n > 0x7fffffffu) {
         dt->last_abort = 64;
         return 0;
     }
@@ -3658,14 +3755,9 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
                   (dt->mask & 0xfc00u) == dt->mask && dt->max_trailer <= 16 &&
                   !async;
     pb.max_trailer = dt->max_trailer;
-    const int pr = pend_resolve(ctx, &pb, 0);
-    if (pr)
-        return pr < 0 ? -1 : 0;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
-    if (srtp_gpu_pp_protect(ctx->gpu, &pb, &fallback))
-        return -1;
-    if (pend_settle(ctx, !fallback, b->stream))
+    if (pp_run(ctx, &pb, 0, &fallback))
         return -1;
     if (fallback) {
         dt->last_abort = fallback;
@@ -3761,7 +3853,7 @@ out:
 static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
 {
     devtab_t *dt = &ctx->dt;
-    if (!ctx->n || b->n > 0x7fffffffu) {
+    if ((!ctx->n && !ctx->templ) || b->n > 0x7fffffffu) {
         dt->last_abort = 64;
         return 0;
     }
@@ -3794,14 +3886,9 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
                   dt->rx_uniform == 0xffffffffu && dt->rx_mask &&
                   (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
                   (dt->rx_mask & 0xfc00u) == dt->rx_mask;
-    const int pr = pend_resolve(ctx, &pb, 1);
-    if (pr)
-        return pr < 0 ? -1 : 0;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
-    if (srtp_gpu_pp_unprotect(ctx->gpu, &pb, &fallback))
-        return -1;
-    if (pend_settle(ctx, !fallback, b->stream))
+    if (pp_run(ctx, &pb, 1, &fallback))
         return -1;
     if (fallback) {
         dt->last_abort = fallback;

@@ -153,6 +153,13 @@ struct PpState {
     uint32_t *pd_pos = nullptr;                // applied: first packets
     uint32_t pd_pos_cap = 0;
     uint32_t pd_nres = 0;                      // applied streams (0: none)
+    // template clones (srtp_gpu_pp_clone): the template's record, spare
+    // records after the uploaded ns0, window words of one, the device's
+    // count of created streams and its overflow / spin-limit flag
+    srtp_dev_stream_t tmpl{};
+    bool has_tmpl = false;
+    uint32_t ns0 = 0, spare = 0, tw = 0;
+    uint32_t *cl_ctl = nullptr;                // [0] created, [1] flags
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -821,6 +828,79 @@ __global__ void k_pend_authchk(const uint32_t *pos, uint32_t nr,
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k < nr && !auth[pos[k]])
         atomicOr(abort, (uint32_t)AB_PENDING);
+}
+
+// ---------------------------------------------------------------------------
+// Template clones (srtp_gpu_pp_clone; srtp_stream_clone, srtp.c:762-863).
+// One thread per packet: a packet whose SSRC is in the hash is done; else
+// the thread claims the empty slot its probe reaches (CAS of the value word
+// to CL_CLAIMED), takes the next spare record, copies the template into it
+// (fresh index and window), then publishes key and record id.  A thread
+// that meets a claimed slot reads it again on its next pass, so threads of
+// one wave never wait inside a branch for each other; every pass is bounded.
+constexpr uint32_t CL_EMPTY = 0xffffffffu, CL_CLAIMED = 0xfffffffeu,
+                   CL_OVERFLOW = 0xfffffffdu;
+
+__global__ void k_clone_insert(const uint8_t *in, const uint64_t *in_off,
+                               const uint32_t *in_len, uint32_t n,
+                               uint32_t *hkey, uint32_t *hval, uint32_t hmask,
+                               srtp_dev_stream_t *st, uint32_t *win,
+                               srtp_dev_stream_t tmpl, uint32_t ns0,
+                               uint32_t spare, uint32_t tw, uint32_t *ctl)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t off = in_off[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
+    if (h.enc_start >> 24)
+        return;
+    const uint32_t ssrc = h.ssrc;
+    uint32_t p = map_hash(ssrc, hmask);
+    for (uint32_t pass = 0, probe = 0; probe <= hmask; pass++) {
+        if (pass > (1u << 22)) {
+            atomicOr(&ctl[1], 2u);   // a claim never published: decline
+            return;
+        }
+        const uint32_t v = __hip_atomic_load(&hval[p], __ATOMIC_ACQUIRE,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+        if (v == CL_CLAIMED)
+            continue;                // published on a later pass
+        if (v != CL_EMPTY) {
+            if (__hip_atomic_load(&hkey[p], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT) == ssrc)
+                return;              // known, or created by another thread
+            p = (p + 1) & hmask;
+            probe++;
+            continue;
+        }
+        uint32_t exp = CL_EMPTY;
+        if (!__hip_atomic_compare_exchange_strong(
+                &hval[p], &exp, CL_CLAIMED, __ATOMIC_ACQ_REL,
+                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            continue;                // another thread took the slot: again
+        const uint32_t k = atomicAdd(&ctl[0], 1u);
+        uint32_t id = CL_OVERFLOW;
+        if (k < spare) {
+            id = ns0 + k;
+            srtp_dev_stream_t S = tmpl;
+            S.ssrc = ssrc;
+            S.win_off = tmpl.win_off + k * tw;
+            S.index = 0;
+            S.uses = 0;
+            S.dir = 0;
+            st[id] = S;
+            for (uint32_t w = 0; w < tw; w++)
+                win[S.win_off + w] = 0;
+        } else {
+            atomicOr(&ctl[1], 1u);   // out of spare records: decline
+        }
+        __hip_atomic_store(&hkey[p], ssrc, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&hval[p], id, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
 }
 
 // Fused order-free form (IcmFused): the per-stream aggregates start at
@@ -2613,7 +2693,7 @@ void srtp_gpu_pp_free(void *p)
                      P->fz_emin, P->fz_bmap, P->fz_hicand, P->fz_nfail,
                      P->fz_glist, P->pd_first, P->pd_min, P->pd_max,
                      P->pd_sids, P->pd_info, P->pd_efirst, P->pd_bak,
-                     P->pd_bakwin, P->pd_pos };
+                     P->pd_bakwin, P->pd_pos, P->cl_ctl };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2623,12 +2703,17 @@ void srtp_gpu_pp_free(void *p)
 }
 
 int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
-                       uint32_t ns, const uint32_t *win, uint32_t nwords,
+                       uint32_t ns_up, const uint32_t *win, uint32_t nwords,
                        const uint32_t *hkey, const uint32_t *hval,
-                       uint32_t hcap)
+                       uint32_t hcap, const srtp_dev_stream_t *tmpl,
+                       uint32_t spare)
 {
     PpState *P = pp_of(g);
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
+    if (!tmpl)
+        spare = 0;
+    // every per-stream array holds the spare records too
+    const uint32_t ns = ns_up + spare;
     uint32_t c1 = P->ns_cap, c2 = P->ns_cap, c5 = P->ns_cap,
              c6 = P->ns_cap, c7 = P->ns_cap, c8 = P->ns_cap, c9 = P->ns_cap,
              c10 = P->ns_cap, c11 = P->ns_cap, c13 = P->ns_cap,
@@ -2669,11 +2754,21 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
         PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
                                       0));
     }
-    P->ns = ns;
+    if (!P->cl_ctl)
+        PPCHK(hipMalloc((void **)&P->cl_ctl, 8));
+    PPCHK(hipMemsetAsync(P->cl_ctl, 0, 8, stream));
+    P->ns = ns_up;
+    P->ns0 = ns_up;
+    P->spare = spare;
+    P->has_tmpl = tmpl != nullptr;
+    if (tmpl) {
+        P->tmpl = *tmpl;
+        P->tw = tmpl->win_bits >> 5;
+    }
     P->nwords = nwords;
     P->hcap = hcap;
     PPCHK(hipMemsetAsync(P->fz_bmap, 0, (4ull * nwords + 4) * 4, stream));
-    PPCHK(hipMemcpyAsync(P->st, streams, ns * sizeof *streams,
+    PPCHK(hipMemcpyAsync(P->st, streams, ns_up * sizeof *streams,
                          hipMemcpyHostToDevice, stream));
     if (nwords) {
         PPCHK(hipMemcpyAsync(P->win, win, nwords * 4ull, hipMemcpyHostToDevice,
@@ -2690,9 +2785,10 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
 }
 
 int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
-                         uint32_t *win)
+                         uint32_t *win, uint32_t *ns_now)
 {
     PpState *P = pp_of(g);
+    *ns_now = P->ns;
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
     PPCHK(hipMemcpyAsync(streams, P->st, P->ns * sizeof *streams,
                          hipMemcpyDeviceToHost, stream));
@@ -2701,6 +2797,33 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
                              hipMemcpyDeviceToHost, stream));
     PPCHK(hipStreamSynchronize(stream));
     return 0;
+}
+
+int srtp_gpu_pp_clone(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
+                      uint32_t *added)
+{
+    PpState *P = pp_of(g);
+    hipStream_t stream = (hipStream_t)b->stream;
+    *added = 0;
+    if (!P->has_tmpl || !b->n)
+        return 0;
+    const uint32_t N = (uint32_t)b->n;
+    hipLaunchKernelGGL(k_clone_insert, dim3((N + 255) / 256), dim3(256), 0,
+                       stream, b->in, b->in_off, b->in_len, N, P->hkey,
+                       P->hval, P->hcap - 1, P->st, P->win, P->tmpl, P->ns0,
+                       P->spare, P->tw, P->cl_ctl);
+    PPCHK(hipGetLastError());
+    uint32_t ctl[2];
+    PPCHK(hipMemcpyAsync(ctl, P->cl_ctl, 8, hipMemcpyDeviceToHost, stream));
+    PPCHK(hipStreamSynchronize(stream));
+    const uint32_t total = ctl[0] < P->spare ? ctl[0] : P->spare;
+    *added = P->ns0 + total - P->ns;
+    P->ns = P->ns0 + total;
+    // a clone's window starts empty in the shifted-window copy too
+    if (*added)
+        PPCHK(hipMemcpyAsync(P->wnew, P->win, P->nwords * 4ull,
+                             hipMemcpyDeviceToDevice, stream));
+    return ctl[1] ? 1 : 0;
 }
 
 int srtp_gpu_pp_pend_scan(srtp_gpu_t *g, const srtp_gpu_pp_batch_t *b,
@@ -3130,8 +3253,14 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         *fallback = 0;
         return 0;
     }
-    if (!P->st || !P->ns || n > 0x7fffffffu)
+    if (!P->st || n > 0x7fffffffu)
         return 0;
+    if (!P->ns) {
+        // a template and no stream yet: every packet's stream is a clone
+        if (P->has_tmpl)
+            *fallback = AB_UNKNOWN_SSRC;
+        return 0;
+    }
     hipStream_t stream = (hipStream_t)b->stream;   // NULL = the null stream
     if (reserve_packets(P, n, stream) || pp_step(stream, "reserve"))
         return -1;
@@ -3548,8 +3677,13 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         *fallback = 0;
         return 0;
     }
-    if (!P->st || !P->ns || n > 0x7fffffffu)
+    if (!P->st || n > 0x7fffffffu)
         return 0;
+    if (!P->ns) {
+        if (P->has_tmpl)
+            *fallback = AB_UNKNOWN_SSRC;
+        return 0;
+    }
     hipStream_t stream = (hipStream_t)b->stream;   // NULL = the null stream
     if (reserve_packets(P, n, stream) || pp_step(stream, "reserve"))
         return -1;

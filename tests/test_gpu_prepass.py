@@ -165,10 +165,118 @@ def test_template_clone_then_device_path():
     ssrcs = [0x3000 + k for k in range(37)]
     pk, nxt = _chains(rng, ssrcs, 500, [rng.randrange(1, 60000)
                                         for _ in ssrcs], big=0)
-    _check(lib, orc, pk, [len(p) + 16 for p in pk])   # clones: host path
+    _check(lib, orc, pk, [len(p) + 16 for p in pk])   # clones on the device
     pk, _ = _chains(rng, ssrcs, 2000, [nxt[s] for s in ssrcs])
     _check(lib, orc, pk, [len(p) + 16 for p in pk])   # all known: device
-    assert lib.prepass_stats() == (1, 1)
+    assert lib.prepass_stats() == (2, 0), lib.prepass_last_abort()
+    for s in ssrcs[::5]:
+        assert lib.get_roc(s) == orc.get_roc(s)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_template_clones_on_device_both_directions(name):
+    """Template sessions (ssrc_any_outbound sender, ssrc_any_inbound
+    receiver; srtp_stream_clone srtp.c:762-863 at 2540 / 3141): the first
+    batch of 300 unseen SSRCs creates every stream on the device, the
+    receiver only for SSRCs whose packet authenticates (a forged first
+    packet leaves none: the next genuine one creates it, 3117-3155); a
+    stream known on the host (specific policy) beside them; three batches,
+    every status and byte against the oracle called per packet, no batch on
+    the host path, and the created streams' state visible through the host
+    API (srtp_stream_get_roc) afterwards"""
+    _gpu()
+    rng = random.Random(808 + len(name))
+    tx = policy(name, ssrc_type=3, seed=31)
+    rx = dict(tx, ssrc_type=2)
+    fixed = policy(name, ssrc=0x0f0f0f0f, seed=32)
+    snd, osnd = L.Session([tx, fixed]), O.Session([tx, fixed])
+    rcv, orcv = L.Session([rx, fixed]), O.Session([rx, fixed])
+    ssrcs = [0x31000000 + 11 * k for k in range(300)] + [0x0f0f0f0f]
+    seq0 = {s: rng.randrange(1, 0xf000) for s in ssrcs}
+    for b in range(3):
+        pk = _interleaved(rng, ssrcs, seq0, 4, payloads=(0, 20, 160))
+        st, out = _device_run(snd, pk, [len(p) + 32 for p in pk], "protect")
+        srtp = []
+        for i, p in enumerate(pk):
+            rc, ref = osnd.protect(p, len(p) + 32)
+            assert st[i] == rc, (b, i, st[i], rc)
+            assert rc or out[i] == ref, (b, i)
+            srtp.append(ref)
+        if b == 0:
+            # forge the first packet of every 7th SSRC
+            seen = set()
+            for i, p in enumerate(srtp):
+                ss = int.from_bytes(p[8:12], "big")
+                if ss not in seen:
+                    seen.add(ss)
+                    if ss % 7 == 0:
+                        bad = bytearray(p)
+                        bad[-1] ^= 0x33
+                        srtp[i] = bytes(bad)
+        _receive_check(rcv, orcv, srtp)
+    assert snd.prepass_stats() == (3, 0), snd.prepass_last_abort()
+    assert rcv.prepass_stats() == (3, 0), rcv.prepass_last_abort()
+    for s in ssrcs[::13]:
+        assert snd.get_roc(s) == osnd.get_roc(s), hex(s)
+        assert rcv.get_roc(s) == orcv.get_roc(s), hex(s)
+
+
+def test_configs3_template_bench_shape():
+    """BASELINE configs[3]'s template variant: 65,536 SSRCs
+    under ONE ssrc_any_outbound key, 128 packets x 160 B each (8M packets,
+    round-robin).  The first batch creates all 65,536 streams on the device
+    (srtp_gpu_pp_clone) and runs there, as does the second; every packet of
+    978 sampled SSRCs (all 64 lane positions) against the C oracle's
+    template session, and every packet back through a receiver template
+    session (its streams created on the device as its packets
+    authenticate)"""
+    _gpu()
+    import numpy as np
+    import torch
+    ns, per, payload, tag = 65536, 128, 160, 10
+    rtp_len = 12 + payload
+    slot = (rtp_len + tag + 15) & ~15
+    n = ns * per
+    base = 0x10000000
+    tx = policy("icm128_hmac80", ssrc_type=3, seed=77)
+    rx = dict(tx, ssrc_type=2)
+    snd, rcv = L.Session([tx]), L.Session([rx])
+    sample = list(range(0, ns, 67))
+    orc = O.Session([tx])
+    rows = torch.tensor([k * ns + s for s in sample for k in range(per)],
+                        dtype=torch.int64, device="cuda")
+    gen = torch.Generator(device="cuda").manual_seed(505)
+    off = torch.arange(n, dtype=torch.int64, device="cuda") * slot
+    seq0 = 0x4000
+    for batch in range(2):
+        a = _rr_arena(ns, per, payload, seq0, base, gen, slot)
+        orig = a.clone()
+        d = a.view(-1)
+        ln = torch.full((n,), rtp_len, dtype=torch.int32, device="cuda")
+        cap = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+        st = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        assert snd.protect_device(d, off, ln, d, off, cap, st) == 0
+        assert int((st != 0).sum()) == 0
+        pin = orig[rows, :rtp_len].cpu().numpy().reshape(-1)
+        m = len(sample) * per
+        offs = np.arange(m, dtype=np.uint64) * rtp_len
+        bad, ref, rlen = orc.protect_many(pin, offs, np.full(m, rtp_len),
+                                          rtp_len + tag)
+        assert bad == 0 and (rlen == rtp_len + tag).all()
+        got = a[rows, :rtp_len + tag].cpu().numpy()
+        diff = np.nonzero((got != ref).any(axis=1))[0]
+        assert len(diff) == 0, ("oracle mismatch", batch, diff[:8])
+        cap2 = torch.full((n,), slot, dtype=torch.int32, device="cuda")
+        st2 = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        assert rcv.unprotect_device(d, off, cap, d, off, cap2, st2) == 0
+        assert int((st2 != 0).sum()) == 0
+        assert torch.equal(a[:, :rtp_len], orig[:, :rtp_len])
+        del a, orig, d
+        seq0 += per
+    assert snd.prepass_stats() == (2, 0), snd.prepass_last_abort()
+    assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
+    for s in sample[::97]:
+        assert snd.get_roc(base + s) == orc.get_roc(base + s)
 
 
 def test_receiver_stream_collision_falls_back():
