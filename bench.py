@@ -84,6 +84,11 @@ WORKLOAD = {
 
 def workload(a):
     """config.workload: the configuration and the operation timed"""
+    if a.template:
+        return ("AES-128-ICM + HMAC-SHA1-80 {op}, 8M packets x 160B, 64k SSRC "
+                "streams under ONE template key (ssrc_any_outbound / "
+                "_inbound; streams created on the device by the warmup's "
+                "first batch)").format(op=a.op)
     return WORKLOAD[a.config].format(op=a.op)
 
 
@@ -139,6 +144,12 @@ def parse():
                     help="--op unprotect: fraction of arrivals that are a "
                     "copy of a packet up to 64 places earlier (duplicates; "
                     "the packet they displace is lost): replay_fail")
+    ap.add_argument("--template", action="store_true",
+                    help="--config g711 only: the 64k SSRCs under one "
+                    "template policy (ssrc_any_outbound sender, "
+                    "ssrc_any_inbound receiver) instead of 64k specific "
+                    "streams with distinct keys (SURVEY 8(d) configs[3] "
+                    "variant); the first warmup batch creates the streams")
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
                     help="auto: measure roofline.traffic and roofline.issue "
                          "with rocprofv3 PMC passes (child processes, N=1 "
@@ -217,6 +228,8 @@ def measure_pmc(a, kname, device=0):
                "--config", a.config, "--op", a.op, "--steps", "2",
                "--warmup", "1",
                "--no-cpu-baseline", "--traffic", "off"]
+        if a.template:
+            cmd.append("--template")
         if a.packets:
             cmd += ["--packets", str(a.packets)]
         # a one-rank child on this rank's device (at N > 1 rank 0 measures
@@ -378,6 +391,55 @@ def _ref_rate_streams(lib_path, payload, nstreams, threads, cycles=1):
     if done <= 0 or secs.value <= 0:
         return None
     return done / secs.value, done
+
+
+def _ref_rate_template(lib_path, payload, nstreams, threads, cycles=2):
+    """the reference with ONE ssrc_any_outbound template per srtp_t and
+    packets round-robin over nstreams SSRCs: the first pass clones every
+    stream (srtp.c:2540-2559), later ones scan the cloned list"""
+    L = C.CDLL(lib_path)
+    fn = L.ref_bench_template
+    fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    secs = C.c_double()
+    done = fn(threads, cycles * nstreams, payload, nstreams, C.byref(secs))
+    if done <= 0 or secs.value <= 0:
+        return None
+    return done / secs.value, done
+
+
+def cpu_baseline_template(payload, nstreams):
+    """--template: the reference's own template path (oracle/bench_ref.c
+    ref_bench_template), both crypto backends, the faster one as value"""
+    ref = os.path.join(ROOT, "oracle", "_ref")
+    affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    th = max(1, min(HOST_SHARE, affinity, quota or affinity))
+    res = {}
+    for k in ("ossl", "int"):
+        path = os.path.join(ref, "bench_ref_%s.so" % k)
+        if not os.path.exists(path):
+            continue
+        note("cpu baseline %s template path, %d SSRCs, %d threads"
+             % (k, nstreams, th))
+        r = _bounded("_ref_rate_template", path, payload, nstreams, th,
+                     limit=240)
+        if r:
+            res[k] = r
+    if not res:
+        return None
+    mk = max(res, key=lambda k: res[k][0])
+    backend = {"ossl": "OpenSSL 3 crypto backend",
+               "int": "built-in crypto kernel"}
+    return {"value": res[mk][0], "unit": "pkt/s", "cores": th,
+            "kind": "reference",
+            "sample": "%d x srtp_protect(), one ssrc_any_outbound template "
+                      "per srtp_t, %d SSRCs round-robin (first pass clones "
+                      "them), %d threads, cisco/libsrtp 3.0.0 with the %s, "
+                      "built from source (oracle/Makefile.ref)"
+                      % (res[mk][1], nstreams, th, backend[mk]),
+            "backends": {"openssl": res["ossl"][0] if "ossl" in res else None,
+                         "internal_kernel": res["int"][0] if "int" in res
+                         else None}}
 
 
 def cpu_baseline(cfg, op, payload, seconds):
@@ -662,6 +724,8 @@ def main():
     if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
         sys.exit(launch_ranks(a, sys.argv[1:]))
     world, rank, local = resolve_world(a)
+    if a.template and a.config != "g711":
+        raise SystemExit("bench: --template applies to --config g711")
     # stdout carries exactly the one JSON line: native libraries' banners
     # (RCCL prints its version block at communicator init) go to stderr
     sys.stdout.flush()
@@ -726,6 +790,16 @@ def run_gpu(a, world, rank, local, json_out):
         for r in range(world):
             if r != rank and sess.remove_stream(rank_ssrc(r)) != 0:
                 raise RuntimeError("bench: removing stream of rank %d" % r)
+    elif a.template:
+        # one template policy per rank (the same key everywhere): every
+        # rank's first batch creates its 64k streams on its own GPU
+        base = (0x10000000 + (rank << 20)) & 0xffffffff
+        policies = [dict(pol, ssrc_type=3, ssrc=0, window_size=128,
+                         allow_repeat_tx=0, keys=[TEST_KEY])]
+        note("session: one template policy, %d SSRCs per batch" % nstreams)
+        sess = L.Session(policies)
+        replication = "template policy per rank" if backend else \
+            "none (one rank)"
     else:
         # 64k streams per rank: the master keys (rank 0's) are broadcast and
         # every rank derives its own streams' session keys
@@ -788,7 +862,11 @@ def run_gpu(a, world, rank, local, json_out):
     if a.op == "unprotect":
         # the sender's side, untimed: protect every batch in place; the
         # receiver (`sess`) then unprotects them in order
-        snd = L.Session([dict(p, ssrc_type=1) for p in policies])
+        snd = L.Session([dict(p, ssrc_type=3 if a.template else 1)
+                         for p in policies])
+        if a.template:
+            sess.close()
+            sess = L.Session([dict(p, ssrc_type=2) for p in policies])
         srtp_len = torch.empty(n, dtype=torch.int32, device=dev)
         for ar in arenas:
             srtp_len.fill_(slot)
@@ -871,7 +949,8 @@ def run_gpu(a, world, rank, local, json_out):
     cpu = None
     if not a.no_cpu_baseline:
         # the host cores beside rank 0's GPU, after the timed region
-        cpu = cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
+        cpu = cpu_baseline_template(payload, nstreams) if a.template else \
+            cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
     roofline = {"bound": "hbm", "achieved": achieved,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,

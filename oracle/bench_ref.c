@@ -239,8 +239,76 @@ static void *run_streams(void *arg)
     return NULL;
 }
 
+/* configs[3]'s template variant: ONE ssrc_any_outbound policy per srtp_t;
+ * packets round-robin over nstreams SSRCs, so the first pass creates every
+ * stream by srtp_stream_clone (srtp.c:2540-2559, 762-863) and every later
+ * srtp_protect() scans the cloned list (srtp.c:5292-5305) */
+static void *run_template(void *arg)
+{
+    sjob_t *j = (sjob_t *)arg;
+    const int ns = j->nstreams;
+    srtp_policy_t p;
+    memset(&p, 0, sizeof p);
+    srtp_crypto_policy_set_rtp_default(&p.rtp);
+    srtp_crypto_policy_set_rtcp_default(&p.rtcp);
+    p.ssrc.type = ssrc_any_outbound;
+    p.key = (uint8_t *)key46;
+    p.window_size = 128;
+    srtp_t s;
+    if (srtp_create(&s, &p))
+        return NULL;
+    const size_t slot = (size_t)(12 + j->payload + 64 + 63) & ~(size_t)63;
+    const int pool = 4096;
+    uint8_t *buf = (uint8_t *)aligned_alloc(64, slot * (size_t)pool);
+    uint64_t x = 0x5352545030303031ULL ^ (uint64_t)(uintptr_t)j;
+    for (size_t i = 0; i < slot * (size_t)pool; i++) {
+        x ^= x << 13;
+        x ^= x >> 7;
+        x ^= x << 17;
+        buf[i] = (uint8_t)x;
+    }
+    const double t0 = now();
+    for (long i = 0; i < j->n; i++) {
+        uint8_t *pk = buf + slot * (size_t)(i % pool);
+        const uint32_t ssrc = 0x10000000u + (uint32_t)(i % ns);
+        const uint16_t seq = (uint16_t)(0x1234 + i / ns);
+        pk[0] = 0x80;
+        pk[1] = 96;
+        pk[2] = (uint8_t)(seq >> 8);
+        pk[3] = (uint8_t)seq;
+        pk[8] = (uint8_t)(ssrc >> 24);
+        pk[9] = (uint8_t)(ssrc >> 16);
+        pk[10] = (uint8_t)(ssrc >> 8);
+        pk[11] = (uint8_t)ssrc;
+        size_t len = slot;
+        if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0)
+            j->done++;
+    }
+    j->secs = now() - t0;
+    free(buf);
+    srtp_dealloc(s);
+    return NULL;
+}
+
+static int bench_sjobs(void *(*fn)(void *), int threads, long pkts_per_thread,
+                       int payload, int nstreams, double *seconds);
+
+int ref_bench_template(int threads, long pkts_per_thread, int payload,
+                       int nstreams, double *seconds)
+{
+    return bench_sjobs(run_template, threads, pkts_per_thread, payload,
+                       nstreams, seconds);
+}
+
 int ref_bench_streams(int threads, long pkts_per_thread, int payload,
                       int nstreams, double *seconds)
+{
+    return bench_sjobs(run_streams, threads, pkts_per_thread, payload,
+                       nstreams, seconds);
+}
+
+static int bench_sjobs(void *(*fn)(void *), int threads, long pkts_per_thread,
+                       int payload, int nstreams, double *seconds)
 {
     *seconds = 0;
     if (ref_init())
@@ -254,7 +322,7 @@ int ref_bench_streams(int threads, long pkts_per_thread, int payload,
         jobs[t].n = pkts_per_thread;
         jobs[t].payload = payload;
         jobs[t].nstreams = nstreams;
-        pthread_create(&th[t], NULL, run_streams, &jobs[t]);
+        pthread_create(&th[t], NULL, fn, &jobs[t]);
     }
     long done = 0;
     double slowest = 0;
