@@ -3746,11 +3746,11 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     pb.mask = dt->mask;
     pb.async = async;
     /* the order-free form may classify inside the AES-ICM kernel: in place
-     * (the declined case restores the input), per-lane keys, one AES-ICM
-     * kernel variant (variant ids 10..15: family ICM, AES-128/192/256), and
-     * trailers the kernel saves whole */
-    pb.fused_ok = b->in == b->out && b->in_off == b->out_off &&
-                  dt->uniform == 0xffffffffu && dt->mask &&
+     * (the declined case restores the input), one AES-ICM kernel variant
+     * (variant ids 10..15: family ICM, AES-128/192/256), and trailers the
+     * kernel saves whole.  One key for every stream (a template session's
+     * clones) takes it too: the per-lane key is then loaded once per lane */
+    pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->mask &&
                   (dt->mask & (dt->mask - 1)) == 0 &&
                   (dt->mask & 0xfc00u) == dt->mask && dt->max_trailer <= 16 &&
                   !async;
@@ -3880,10 +3880,8 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     pb.uniform_key = dt->rx_uniform;
     pb.mask = dt->rx_mask;
     /* the order-free receive form may classify inside the AES-ICM kernel:
-     * in place (a declined batch is restored), per-lane keys, one AES-ICM
-     * kernel variant */
-    pb.fused_ok = b->in == b->out && b->in_off == b->out_off &&
-                  dt->rx_uniform == 0xffffffffu && dt->rx_mask &&
+     * in place (a declined batch is restored), one AES-ICM kernel variant */
+    pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->rx_mask &&
                   (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
                   (dt->rx_mask & 0xfc00u) == dt->rx_mask;
     int fallback = 1;
