@@ -7,6 +7,7 @@
 // Compiled once per AES round count: -DGCM_NR=10 or 14.
 #include "srtp_dev_common.h"
 #include "srtp_gpu_int.h"
+#include "srtp_fused.h"
 
 #ifndef GCM_NR
 #error "GCM_NR (10 or 14) must be defined"
@@ -34,12 +35,19 @@ DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
 // chunks of four CTR blocks whose counters stay in the cached epoch
 // (j + 2 <= 255: the first 4 KiB), data loaded GCM_PF chunks ahead; the
 // rest block by block with full AES.
-template <int NR, bool PROTECT, bool UNIFORM, bool TAB4, class GT, class KEY>
-DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
-                    KEY &rk)
+template <int NR>
+constexpr uint32_t gcm_vid()
 {
-    const srtp_dev_meta_t m = A.meta[i];
-    constexpr uint32_t VID = 16u + 2u * ((NR - 8) / 2);
+    return 16u + 2u * ((NR - 8) / 2);
+}
+
+// m: the packet's descriptor; in_off / out_off its offsets
+template <int NR, bool PROTECT, bool UNIFORM, bool TAB4, class GT, class KEY>
+DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
+                    uint64_t in_off, uint64_t out_off, uint32_t i,
+                    const AesLds &T, GT G, KEY &rk)
+{
+    constexpr uint32_t VID = gcm_vid<NR>();
     if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
         return;
     const uint32_t slot = UNIFORM ? A.uni : m.key;
@@ -49,8 +57,8 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
         G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
     }
 
-    const uint8_t *in = A.in + A.in_off[i];
-    uint8_t *out = A.out + A.out_off[i];
+    const uint8_t *in = A.in + in_off;
+    uint8_t *out = A.out + out_off;
     const uint32_t enc_start = SRTP_META_ENC_START(m.info);
     const uint32_t tag_len = key->tag_len;
     const uint32_t mki_size = key->mki_size;
@@ -194,7 +202,10 @@ DEV void gcm_packet(const GcmArgs &A, uint32_t i, const AesLds &T, GT G,
 #endif
 constexpr int GCM_THREADS = GCM_THREADS_N;
 
-template <int NR, bool PROTECT, bool UNIFORM>
+// FUSED (per-lane keys, in place): the order-free classification in the
+// kernel (srtp_fused.h; srtp_prepass.hip pp_protect_fused /
+// pp_unprotect_fused), as k_icm_hmac does it for AES-ICM
+template <int NR, bool PROTECT, bool UNIFORM, bool FUSED = false>
 __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 {
     constexpr bool TAB4 = UNIFORM;
@@ -236,14 +247,53 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
         G.init(lds, (uint32_t)AES_TAB4_BYTES, threadIdx.x);
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
              i += stride)
-            gcm_packet<NR, PROTECT, UNIFORM, true>(A, i, T, G, rk);
+            gcm_packet<NR, PROTECT, UNIFORM, true>(A, A.meta[i], A.in_off[i],
+                                                   A.out_off[i], i, T, G, rk);
         return;
     }
     GhGlobal G;   // set per packet from its key
     G.g = nullptr;
+    if constexpr (FUSED) {
+        FzLane z;
+        z.ssrc = 0;
+        z.sid = FZ_NOCHAIN;
+        z.run_sid = FZ_NOCHAIN;
+        z.run_cnt = 0;
+        z.run_max = 0;
+        z.run_min = ~0ull;
+        z.run_cmax = 0;
+        z.bw_idx = 0;
+        z.bw_bits = 0;
+        constexpr uint32_t vid = gcm_vid<NR>();
+        for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+             i += stride) {
+            // fused batches are in place: one offset
+            const uint64_t off = A.in_off[i];
+            const GlbSrc S{ A.in + off };
+            const uint32_t len = A.fz.in_len[i], cap = A.fz.cap[i];
+            if constexpr (PROTECT) {
+                const srtp_dev_meta_t m =
+                    fz_classify(A, i, z, vid, off, len, cap, S);
+                gcm_packet<NR, PROTECT, UNIFORM, false>(A, m, off, off, i, T,
+                                                        G, rk);
+            } else {
+                uint64_t e;
+                uint32_t sid;
+                const srtp_dev_meta_t m =
+                    fzu_classify(A, i, z, vid, off, len, cap, S, e, sid);
+                gcm_packet<NR, PROTECT, UNIFORM, false>(A, m, off, off, i, T,
+                                                        G, rk);
+                if (sid != FZ_NOCHAIN)
+                    fzu_verdict(A, i, z, m, e, sid, A.auth_ok[i] != 0);
+            }
+        }
+        fz_flush<PROTECT>(A.fz, z);
+        return;
+    }
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
          i += stride)
-        gcm_packet<NR, PROTECT, UNIFORM, false>(A, i, T, G, rk);
+        gcm_packet<NR, PROTECT, UNIFORM, false>(A, A.meta[i], A.in_off[i],
+                                                A.out_off[i], i, T, G, rk);
 }
 
 }   // namespace
@@ -253,11 +303,17 @@ int launch_gcm_nr(const GcmArgs &A, bool prot, int ncu, hipStream_t st)
 {
     // persistent grid: one workgroup per CU (128 KiB of tables) for uniform
     // keys, two otherwise (64 KiB)
-    const bool uni = A.uni != 0xffffffffu;
+    const bool uni = A.uni != 0xffffffffu && !A.fused;
     const size_t wgs = (A.n + GCM_THREADS - 1) / GCM_THREADS;
     const size_t cap = (size_t)ncu * (uni ? 1 : 2);
     const dim3 grid((unsigned)(wgs < cap ? wgs : cap)), block(GCM_THREADS);
-    if (uni && prot)
+    if (A.fused && prot)
+        hipLaunchKernelGGL((k_gcm<NR, true, false, true>), grid, block, 0, st,
+                           A);
+    else if (A.fused)
+        hipLaunchKernelGGL((k_gcm<NR, false, false, true>), grid, block, 0, st,
+                           A);
+    else if (uni && prot)
         hipLaunchKernelGGL((k_gcm<NR, true, true>), grid, block, 0, st, A);
     else if (uni)
         hipLaunchKernelGGL((k_gcm<NR, false, true>), grid, block, 0, st, A);

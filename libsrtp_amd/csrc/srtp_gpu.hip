@@ -1274,6 +1274,9 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
+    A.fused = b->fused != nullptr;
+    if (A.fused)
+        A.fz = *(const IcmFused *)b->fused;
     return launch_gcm_nr<NR>(A, PROT, g->ncu, st);
 }
 

@@ -126,6 +126,10 @@ struct GcmArgs {
     const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;
+    // order-free form classified in the kernel (per-lane keys; in place):
+    // fz valid when fused, meta then neither read nor written
+    bool fused;
+    IcmFused fz;
 };
 
 // records a HIP error in the FFI's error string, returns -1

@@ -3711,6 +3711,16 @@ static int pp_run(srtp_t ctx, srtp_gpu_pp_batch_t *pb, int unprotect,
     }
 }
 
+/* the kernel variant (one bit of a variant mask) whose kernel classifies
+ * order-free batches itself: AES-ICM (variant ids 10..15, any key mode) and,
+ * with a key per stream, AES-GCM (ids 18, 22: k_gcm's per-lane form) */
+static int fused_variant(uint32_t mask, uint32_t uniform)
+{
+    if ((mask & 0xfc00u) == mask)
+        return 1;
+    return (mask & 0x440000u) == mask && uniform == 0xffffffffu;
+}
+
 /* the device pre-pass; returns 1 when the batch was completed on the GPU,
  * 0 when the host path must run it, -1 on a device error */
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
@@ -3752,8 +3762,8 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
      * clones) takes it too: the per-lane key is then loaded once per lane */
     pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->mask &&
                   (dt->mask & (dt->mask - 1)) == 0 &&
-                  (dt->mask & 0xfc00u) == dt->mask && dt->max_trailer <= 16 &&
-                  !async;
+                  fused_variant(dt->mask, dt->uniform) &&
+                  dt->max_trailer <= 16 && !async;
     pb.max_trailer = dt->max_trailer;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
@@ -3883,7 +3893,7 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
      * in place (a declined batch is restored), one AES-ICM kernel variant */
     pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->rx_mask &&
                   (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
-                  (dt->rx_mask & 0xfc00u) == dt->rx_mask;
+                  fused_variant(dt->rx_mask, dt->rx_uniform);
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (pp_run(ctx, &pb, 1, &fallback))

@@ -451,6 +451,31 @@ def test_configs3_shape_64k_distinct_key_streams():
     assert lib.prepass_sorted_batches() == 0
 
 
+@pytest.mark.parametrize("op", ["protect", "unprotect"])
+def test_configs3_shape_64k_gcm256_streams_fused(op):
+    """65,536 AES-256-GCM streams with distinct keys, packets round-robin,
+    in place: the order-free form classified inside k_gcm (srtp_fused.h,
+    per-lane keys), two batches; every status and byte against the oracle
+    called once per packet (protect, or the receive side of what the
+    oracle's sender protected)"""
+    _gpu()
+    rng = random.Random(909)
+    ns = 65536
+    ssrcs = [0x11000000 + k for k in range(ns)]
+    pols = [policy("gcm256_16", ssrc=s, seed=k) for k, s in enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    snd = O.Session(pols)
+    seq0 = 0x9000
+    for per in (2, 3):
+        pk = [rtp_packet(rng, ssrcs[i % ns], (seq0 + i // ns) & 0xffff,
+                         rng.choice([0, 20, 160]))
+              for i in range(ns * per)]
+        _pending_run(lib, orc, snd, op, pk)
+        seq0 += per
+    assert lib.prepass_stats() == (2, 0), lib.prepass_last_abort()
+    assert lib.prepass_sorted_batches() == 0
+
+
 def _rr_arena(ns, per, payload, seq0, base_ssrc, gen, slot):
     """configs[3]-shaped arena on the GPU: ns streams round-robin, per
     packets each (packet i: stream i % ns, its packet i // ns)"""
@@ -726,7 +751,7 @@ def _device_protect_raw(sess, pkts, caps, fill=0xa5):
 
 
 @pytest.mark.parametrize("name", ["icm128_hmac80", "icm128_nullauth",
-                                  "icm256_hmac32"])
+                                  "icm256_hmac32", "gcm256_16", "gcm256_8"])
 @pytest.mark.parametrize("caps_mode", ["roomy", "tight"])
 @pytest.mark.parametrize("case", ["duplicate", "unknown_ssrc", "long_chain"])
 def test_fused_order_free_declined_batch_is_restored(case, caps_mode, name):
@@ -935,7 +960,7 @@ def _receive_check(lib, orc, pkts):
 
 
 @pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
-                                  "icm128_nullauth"])
+                                  "icm128_nullauth", "gcm256_16", "gcm256_8"])
 def test_fused_unprotect_clean_forged_and_declined(name):
     """clean batches, reordered inside the window, with forgeries (auth_fail,
     undone in place), then a duplicate (-> host), an unknown SSRC (-> host),
