@@ -775,7 +775,7 @@ def test_fused_order_free_declined_batch_is_restored(case, caps_mode, name):
         caps = [len(p) + 16 for p in pk]
     else:
         tag = {"icm128_hmac80": 10, "icm128_nullauth": 0,
-               "icm256_hmac32": 4}[name]
+               "icm256_hmac32": 4, "gcm256_16": 16, "gcm256_8": 8}[name]
         caps = [len(p) + tag + rng.randrange(0, 3) for p in pk]
     st, got, orig, offs, olen = _device_protect_raw(lib, pk, caps)
     for i, p in enumerate(pk):
