@@ -452,6 +452,10 @@ void srtp_mi355x_set_key_buckets(int on);
 
 #define SRTP_MI355X_FAIL_VERDICT_WAIT 1
 #define SRTP_MI355X_FAIL_ASYNC_DRAIN 2
+/* ... or that the next `count` srtp_mi355x_session_broadcast calls of this
+ * process fail to allocate their blob buffers (every rank then returns
+ * srtp_err_status_alloc_fail) */
+#define SRTP_MI355X_FAIL_BCAST_ALLOC 3
 void srtp_mi355x_debug_inject_failure(int what, int count);
 
 /* ========================================================================

@@ -3456,6 +3456,7 @@ out:
  * reads or changes the device stream table, the keys or the staging arenas
  * from another stream */
 static int g_fail_drains;   /* test hook: srtp_mi355x_debug_inject_failure */
+static int g_fail_bcast_alloc;   /* ... and for srtp_mi355x_session_broadcast */
 
 /* returns -1 (and poisons the session) when the queued batch failed */
 static int async_drain(srtp_t ctx)
@@ -4694,7 +4695,9 @@ void srtp_mi355x_set_key_buckets(int on) { srtp_gpu_pp_set_buckets(on); }
 
 void srtp_mi355x_debug_inject_failure(int what, int count)
 {
-    if (what == SRTP_MI355X_FAIL_VERDICT_WAIT)
+    if (what == SRTP_MI355X_FAIL_BCAST_ALLOC)
+        g_fail_bcast_alloc = count;
+    else if (what == SRTP_MI355X_FAIL_VERDICT_WAIT)
         srtp_gpu_pp_debug_fail_waits(count);
     else if (what == SRTP_MI355X_FAIL_ASYNC_DRAIN)
         g_fail_drains = count;
@@ -5242,6 +5245,10 @@ srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
         blen = blob ? hlen : 0;
     }
     flag = (!dblob || !blob) ? 1 : 0;
+    if (g_fail_bcast_alloc > 0) {
+        g_fail_bcast_alloc--;
+        flag = 1;
+    }
     if (srtp_gpu_h2d(NULL, dlen, &flag, sizeof flag, stream) ||
         (nr = allred(dlen, dlen, 1, NCCL_UINT64, NCCL_MAX, nccl_comm,
                      stream)) ||
