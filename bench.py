@@ -363,17 +363,24 @@ def cgroup_cpus(root="/sys/fs/cgroup"):
 
 
 def _ref_rate(lib_path, op, payload, gcm, threads, seconds):
-    """packets/s of the reference build at lib_path: calibrate on one thread,
-    then ~`seconds` of work on `threads` threads (sized for HOST_SHARE
-    CPUs, so a thread count above the share does not stretch the sample)"""
+    """packets/s of the reference build at lib_path: calibrate with all
+    `threads` threads on a short run, timing the whole call (unprotect's
+    untimed protect pass and any lock contention between the threads
+    included: a one-thread calibration sent OpenSSL unprotect at 16 threads
+    past the child's time limit), then a run of ~`seconds` wall time"""
     L = C.CDLL(lib_path)
     fn = L.ref_bench if op == "protect" else L.ref_bench_unprotect
     fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
     secs = C.c_double()
-    n = fn(1, 8192, payload, int(gcm), C.byref(secs))
-    busy = min(threads, HOST_SHARE)
-    per_thread = max(2048, int(n / max(secs.value, 1e-6) * seconds * busy /
-                               threads))
+    cal = 1024
+    while True:   # grow the calibration until its fixed costs are small
+        t0 = time.perf_counter()
+        fn(threads, cal, payload, int(gcm), C.byref(secs))
+        wall = time.perf_counter() - t0
+        if wall >= seconds / 8 or cal >= 1 << 22:
+            break
+        cal *= 4
+    per_thread = max(cal, int(cal * seconds / max(wall, 1e-6)))
     done = fn(threads, per_thread, payload, int(gcm), C.byref(secs))
     return done / secs.value, done
 
