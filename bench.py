@@ -163,18 +163,26 @@ def note(msg):
     print("bench: " + msg, file=sys.stderr, flush=True)
 
 
-def pmc_counter(path, kernel_substr, counter):
-    """mean per-dispatch value of one rocprofv3 --pmc counter of the
-    kernels whose name contains kernel_substr, from counter_collection.csv"""
+def pmc_counter(path, kernels, counter):
+    """one rocprofv3 --pmc counter per step of the crypto launches: for each
+    name in `kernels` (substrings; each kernel launches once per step) the
+    mean per dispatch of the kernels whose name contains it, summed over the
+    names present in counter_collection.csv"""
     import csv
-    tot, disp = 0.0, set()
+    tot, disp = {}, {}
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel_substr in row.get("Kernel_Name", "") and \
-                    row.get("Counter_Name", "") == counter:
-                tot += float(row.get("Counter_Value", 0) or 0)
-                disp.add(row.get("Dispatch_Id"))
-    return tot / len(disp) if disp else None
+            if row.get("Counter_Name", "") != counter:
+                continue
+            for k in kernels:
+                if k in row.get("Kernel_Name", ""):
+                    tot[k] = tot.get(k, 0.0) + float(row.get("Counter_Value", 0)
+                                                     or 0)
+                    disp.setdefault(k, set()).add(row.get("Dispatch_Id"))
+                    break
+    if not disp:
+        return None
+    return sum(tot[k] / len(disp[k]) for k in disp)
 
 
 # PMC passes (MI355X_MICROARCH.md: one pass holds at most 4 TCC counters,
@@ -204,7 +212,7 @@ def traffic_split(a, n, rtp_len, tag, pmc):
             "write_over_written_bytes": w / wr}
 
 
-def measure_pmc(a, kname, device=0):
+def measure_pmc(a, kernels, device=0):
     """per-launch PMC counters of the dominant kernel over a short run of
     this same workload, one rocprofv3 --pmc pass per entry of PMC_PASSES,
     each a child process started before this process touches the GPU.
@@ -247,7 +255,7 @@ def measure_pmc(a, kname, device=0):
         if not csvs:
             break
         for c in ctrs:
-            v = pmc_counter(csvs[0], kname, c)
+            v = pmc_counter(csvs[0], kernels, c)
             if v is not None:
                 got[c] = v
     shutil.rmtree(base, ignore_errors=True)
@@ -400,12 +408,16 @@ def _ref_rate_streams(lib_path, payload, nstreams, threads, cycles=1):
     return done / secs.value, done
 
 
-def _ref_rate_template(lib_path, payload, nstreams, threads, cycles=2):
+def _ref_rate_template(lib_path, payload, nstreams, threads, cycles=2,
+                       op="protect"):
     """the reference with ONE ssrc_any_outbound template per srtp_t and
     packets round-robin over nstreams SSRCs: the first pass clones every
-    stream (srtp.c:2540-2559), later ones scan the cloned list"""
+    stream (srtp.c:2540-2559), later ones scan the cloned list; unprotect:
+    one ssrc_any_inbound srtp_t per thread receiving a template sender's
+    packets (clones on first authentication, srtp.c:3117-3155)"""
     L = C.CDLL(lib_path)
-    fn = L.ref_bench_template
+    fn = L.ref_bench_template if op == "protect" else \
+        L.ref_bench_template_unprotect
     fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
     secs = C.c_double()
     done = fn(threads, cycles * nstreams, payload, nstreams, C.byref(secs))
@@ -414,9 +426,10 @@ def _ref_rate_template(lib_path, payload, nstreams, threads, cycles=2):
     return done / secs.value, done
 
 
-def cpu_baseline_template(payload, nstreams):
+def cpu_baseline_template(payload, nstreams, op="protect"):
     """--template: the reference's own template path (oracle/bench_ref.c
-    ref_bench_template), both crypto backends, the faster one as value"""
+    ref_bench_template / ref_bench_template_unprotect), both crypto
+    backends, the faster one as value"""
     ref = os.path.join(ROOT, "oracle", "_ref")
     affinity = len(os.sched_getaffinity(0))
     quota = cgroup_cpus()
@@ -428,7 +441,7 @@ def cpu_baseline_template(payload, nstreams):
             continue
         note("cpu baseline %s template path, %d SSRCs, %d threads"
              % (k, nstreams, th))
-        r = _bounded("_ref_rate_template", path, payload, nstreams, th,
+        r = _bounded("_ref_rate_template", path, payload, nstreams, th, 2, op,
                      limit=240)
         if r:
             res[k] = r
@@ -439,11 +452,13 @@ def cpu_baseline_template(payload, nstreams):
                "int": "built-in crypto kernel"}
     return {"value": res[mk][0], "unit": "pkt/s", "cores": th,
             "kind": "reference",
-            "sample": "%d x srtp_protect(), one ssrc_any_outbound template "
+            "sample": "%d x srtp_%s(), one ssrc_any_%s template "
                       "per srtp_t, %d SSRCs round-robin (first pass clones "
                       "them), %d threads, cisco/libsrtp 3.0.0 with the %s, "
                       "built from source (oracle/Makefile.ref)"
-                      % (res[mk][1], nstreams, th, backend[mk]),
+                      % (res[mk][1], op,
+                         "outbound" if op == "protect" else "inbound",
+                         nstreams, th, backend[mk]),
             "backends": {"openssl": res["ossl"][0] if "ossl" in res else None,
                          "internal_kernel": res["int"][0] if "int" in res
                          else None}}
@@ -752,6 +767,13 @@ def main():
 def run_gpu(a, world, rank, local, json_out):
     pol, payload, npk, tag = CONFIGS[a.config]
     kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
+    kernels = (kname,)
+    if a.config == "g711" and os.environ.get("SRTP_ICM_STG", "1") != "0":
+        # configs[3]'s fused batches: the LDS-staged kernel, then the
+        # per-lane form over the groups it listed (one launch per step each;
+        # DESIGN.md §4 k_icm_stg); the HIP events bracket both
+        kname = "k_icm_stg + k_icm_hmac (list pass)"
+        kernels = ("k_icm_stg", "k_icm_hmac")
     # PMC passes first: child processes, before this one touches the GPU
     # SRTP_BENCH_DEVICE: every rank of this process on that device (the
     # N > 1 path exercised on a one-GPU box, with gloo: RCCL refuses two
@@ -759,7 +781,7 @@ def run_gpu(a, world, rank, local, json_out):
     devno = int(os.environ.get("SRTP_BENCH_DEVICE", local))
     pmc = {}
     if rank == 0 and a.traffic == "auto":
-        pmc = measure_pmc(a, kname, devno)
+        pmc = measure_pmc(a, kernels, devno)
     traffic = None
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         traffic = (pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
@@ -956,7 +978,7 @@ def run_gpu(a, world, rank, local, json_out):
     cpu = None
     if not a.no_cpu_baseline:
         # the host cores beside rank 0's GPU, after the timed region
-        cpu = cpu_baseline_template(payload, nstreams) if a.template else \
+        cpu = cpu_baseline_template(payload, nstreams, a.op) if a.template else \
             cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
     roofline = {"bound": "hbm", "achieved": achieved,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",

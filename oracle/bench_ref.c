@@ -173,8 +173,9 @@ static int bench(int threads, long pkts_per_thread, int payload, int gcm,
 typedef struct {
     long n;
     int payload, nstreams;
+    int rx;      /* run_template: time a receiver's template path instead */
     long done;
-    double secs; /* protect time, setup excluded */
+    double secs; /* protect (or unprotect) time, setup excluded */
 } sjob_t;
 
 static void *run_streams(void *arg)
@@ -242,7 +243,11 @@ static void *run_streams(void *arg)
 /* configs[3]'s template variant: ONE ssrc_any_outbound policy per srtp_t;
  * packets round-robin over nstreams SSRCs, so the first pass creates every
  * stream by srtp_stream_clone (srtp.c:2540-2559, 762-863) and every later
- * srtp_protect() scans the cloned list (srtp.c:5292-5305) */
+ * srtp_protect() scans the cloned list (srtp.c:5292-5305).  With j->rx the
+ * receiver's side is timed instead: a sender (untimed, its own template)
+ * protects each pool of packets, then ONE ssrc_any_inbound srtp_t
+ * unprotects them (timed): its first pass clones a stream per SSRC once the
+ * packet authenticates (srtp.c:3117-3155) */
 static void *run_template(void *arg)
 {
     sjob_t *j = (sjob_t *)arg;
@@ -254,12 +259,20 @@ static void *run_template(void *arg)
     p.ssrc.type = ssrc_any_outbound;
     p.key = (uint8_t *)key46;
     p.window_size = 128;
-    srtp_t s;
+    srtp_t s, r = NULL;
     if (srtp_create(&s, &p))
         return NULL;
+    if (j->rx) {
+        p.ssrc.type = ssrc_any_inbound;
+        if (srtp_create(&r, &p)) {
+            srtp_dealloc(s);
+            return NULL;
+        }
+    }
     const size_t slot = (size_t)(12 + j->payload + 64 + 63) & ~(size_t)63;
     const int pool = 4096;
     uint8_t *buf = (uint8_t *)aligned_alloc(64, slot * (size_t)pool);
+    size_t *plen = (size_t *)malloc(sizeof(size_t) * (size_t)pool);
     uint64_t x = 0x5352545030303031ULL ^ (uint64_t)(uintptr_t)j;
     for (size_t i = 0; i < slot * (size_t)pool; i++) {
         x ^= x << 13;
@@ -267,48 +280,77 @@ static void *run_template(void *arg)
         x ^= x << 17;
         buf[i] = (uint8_t)x;
     }
-    const double t0 = now();
-    for (long i = 0; i < j->n; i++) {
-        uint8_t *pk = buf + slot * (size_t)(i % pool);
-        const uint32_t ssrc = 0x10000000u + (uint32_t)(i % ns);
-        const uint16_t seq = (uint16_t)(0x1234 + i / ns);
-        pk[0] = 0x80;
-        pk[1] = 96;
-        pk[2] = (uint8_t)(seq >> 8);
-        pk[3] = (uint8_t)seq;
-        pk[8] = (uint8_t)(ssrc >> 24);
-        pk[9] = (uint8_t)(ssrc >> 16);
-        pk[10] = (uint8_t)(ssrc >> 8);
-        pk[11] = (uint8_t)ssrc;
-        size_t len = slot;
-        if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0)
-            j->done++;
+    for (long i0 = 0; i0 < j->n; i0 += pool) {
+        const long m = j->n - i0 < pool ? j->n - i0 : pool;
+        const double t0 = now();
+        for (long q = 0; q < m; q++) {
+            const long i = i0 + q;
+            uint8_t *pk = buf + slot * (size_t)q;
+            const uint32_t ssrc = 0x10000000u + (uint32_t)(i % ns);
+            const uint16_t seq = (uint16_t)(0x1234 + i / ns);
+            pk[0] = 0x80;
+            pk[1] = 96;
+            pk[2] = (uint8_t)(seq >> 8);
+            pk[3] = (uint8_t)seq;
+            pk[8] = (uint8_t)(ssrc >> 24);
+            pk[9] = (uint8_t)(ssrc >> 16);
+            pk[10] = (uint8_t)(ssrc >> 8);
+            pk[11] = (uint8_t)ssrc;
+            size_t len = slot;
+            plen[q] = 0;
+            if (srtp_protect(s, pk, 12 + (size_t)j->payload, pk, &len, 0) == 0) {
+                plen[q] = len;
+                if (!r)
+                    j->done++;
+            }
+        }
+        if (!r) {
+            j->secs += now() - t0;
+            continue;
+        }
+        const double t1 = now();
+        for (long q = 0; q < m; q++) {
+            uint8_t *pk = buf + slot * (size_t)q;
+            size_t len = slot;
+            if (plen[q] && srtp_unprotect(r, pk, plen[q], pk, &len) == 0)
+                j->done++;
+        }
+        j->secs += now() - t1;
     }
-    j->secs = now() - t0;
+    free(plen);
     free(buf);
     srtp_dealloc(s);
+    if (r)
+        srtp_dealloc(r);
     return NULL;
 }
 
 static int bench_sjobs(void *(*fn)(void *), int threads, long pkts_per_thread,
-                       int payload, int nstreams, double *seconds);
+                       int payload, int nstreams, int rx, double *seconds);
 
 int ref_bench_template(int threads, long pkts_per_thread, int payload,
                        int nstreams, double *seconds)
 {
     return bench_sjobs(run_template, threads, pkts_per_thread, payload,
-                       nstreams, seconds);
+                       nstreams, 0, seconds);
+}
+
+int ref_bench_template_unprotect(int threads, long pkts_per_thread,
+                                 int payload, int nstreams, double *seconds)
+{
+    return bench_sjobs(run_template, threads, pkts_per_thread, payload,
+                       nstreams, 1, seconds);
 }
 
 int ref_bench_streams(int threads, long pkts_per_thread, int payload,
                       int nstreams, double *seconds)
 {
     return bench_sjobs(run_streams, threads, pkts_per_thread, payload,
-                       nstreams, seconds);
+                       nstreams, 0, seconds);
 }
 
 static int bench_sjobs(void *(*fn)(void *), int threads, long pkts_per_thread,
-                       int payload, int nstreams, double *seconds)
+                       int payload, int nstreams, int rx, double *seconds)
 {
     *seconds = 0;
     if (ref_init())
@@ -322,6 +364,7 @@ static int bench_sjobs(void *(*fn)(void *), int threads, long pkts_per_thread,
         jobs[t].n = pkts_per_thread;
         jobs[t].payload = payload;
         jobs[t].nstreams = nstreams;
+        jobs[t].rx = rx;
         pthread_create(&th[t], NULL, fn, &jobs[t]);
     }
     long done = 0;

@@ -31,6 +31,14 @@
                  : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), \
                    "+v"(a6), "+v"(a7)                                          \
                  : "v"(x))
+#define R8_2S(OP, SFX)                                                         \
+    asm volatile(OP " %0, %0, %8 " SFX "\n\t" OP " %1, %1, %8 " SFX "\n\t"     \
+                 OP " %2, %2, %8 " SFX "\n\t" OP " %3, %3, %8 " SFX "\n\t"     \
+                 OP " %4, %4, %8 " SFX "\n\t" OP " %5, %5, %8 " SFX "\n\t"     \
+                 OP " %6, %6, %8 " SFX "\n\t" OP " %7, %7, %8 " SFX            \
+                 : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), \
+                   "+v"(a6), "+v"(a7)                                          \
+                 : "v"(x))
 #define R8_1(OP, S)                                                            \
     asm volatile(OP " %0, %0 " S "\n\t" OP " %1, %1 " S "\n\t"                 \
                  OP " %2, %2 " S "\n\t" OP " %3, %3 " S "\n\t"                 \
@@ -75,6 +83,16 @@ __global__ __launch_bounds__(1024) void k_rate(uint32_t *out, int iters,
             if (K == 23) R8("v_bfe_u32");
             if (K == 24) R8_1("v_mov_b32_dpp", "row_shr:1 row_mask:0xf bank_mask:0xf");
             if (K == 25) R8_2("v_xor_b32_dpp");
+            // packed 16-bit and 24-bit forms (round 5: byte moves at full rate?)
+            if (K == 26) R8("v_pk_mad_u16");
+            if (K == 27) R8_2S("v_pk_add_u16", "op_sel:[1,0] op_sel_hi:[0,1]");
+            if (K == 28) R8_2("v_pk_lshlrev_b16");
+            if (K == 29) R8_2("v_lshrrev_b32");
+            if (K == 30) R8("v_mad_u32_u24");
+            if (K == 31) R8("v_dot4_u32_u8");
+            if (K == 32) R8("v_alignbyte_b32");
+            if (K == 33) R8_2("v_pk_mul_lo_u16");
+            if (K == 34) R8S("v_pk_mad_u16", "op_sel:[1,0,0] op_sel_hi:[0,1,1]");
         }
     }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -92,7 +110,11 @@ static const char *NAMES[] = { "v_xor_b32", "v_add_u32", "v_perm_b32",
                                "v_bfi_b32", "v_xor_b32_e64", "unused",
                                "v_sub_u32", "sdwa mov b2->b1", "sdwa mov b0->b1",
                                "permlane32_swap", "permlane16_swap", "v_bfe_u32",
-                               "dpp row_shr", "v_xor_b32_dpp" };
+                               "dpp row_shr", "v_xor_b32_dpp", "v_pk_mad_u16",
+                               "pk_add_u16 swap", "v_pk_lshlrev_b16",
+                               "v_lshrrev_b32", "v_mad_u32_u24",
+                               "v_dot4_u32_u8", "v_alignbyte_b32",
+                               "v_pk_mul_lo_u16", "pk_mad_u16 opsel" };
 
 template <int K>
 static void one(uint32_t *out, uint64_t *clk)
@@ -154,5 +176,14 @@ int main()
     one<22>(out, clk);
     one<23>(out, clk);
     one<24>(out, clk);
+    one<26>(out, clk);
+    one<27>(out, clk);
+    one<28>(out, clk);
+    one<29>(out, clk);
+    one<30>(out, clk);
+    one<31>(out, clk);
+    one<32>(out, clk);
+    one<33>(out, clk);
+    one<34>(out, clk);
     return 0;
 }
