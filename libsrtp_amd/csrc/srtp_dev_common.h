@@ -120,17 +120,11 @@ struct AesLds {
     uint32_t L[2];   // lane templates of tables (0,1) and (2,3): bytes 0, 2
 };
 
-// timing experiment: lanes read AES_LDS_COPIES of the 32 table
-// copies, i.e. 32 / AES_LDS_COPIES lanes of a 32-lane group per bank
-#ifndef AES_LDS_COPIES
-#define AES_LDS_COPIES 32
-#endif
-
 DEV AesLds make_aes_lds(const void *lds)
 {
     AesLds T;
     T.lds = (const char *)lds;
-    const uint32_t c = (threadIdx.x & (AES_LDS_COPIES - 1)) * 4;
+    const uint32_t c = (threadIdx.x & 31) * 4;   // the lane's table copy
     T.L[0] = c;
     T.L[1] = 0x10000u | c;
     return T;

@@ -1128,6 +1128,8 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
 #pragma unroll
     for (uint32_t j = 0; j < STG_GRAN / 64; j++)
         fr |= (stg_swz(64 * j + L) ^ (64 * j + L)) << (2 * j);
+    StgKey K;   // the per-packet words of the lane's last key
+    K.slot = FZ_NOCHAIN;
     // the group's offset, length and capacity, loaded one group ahead
     uint64_t n_off = 0;
     uint32_t n_len = 0, n_cap = 0;
@@ -1182,9 +1184,13 @@ __global__ __launch_bounds__(512) void k_icm_stg(IcmArgs A)
                     (const void __attribute__((address_space(1))) *)(span + 16ull * ((64 * j + L) ^ ((fr >> (2 * j)) & 3))),
                     (void __attribute__((address_space(3))) *)(img + 64 * j), 16, 0, 0);
         }
-        // the key words of the lane's last stream, under the same wait
-        StgKey K;
-        K.load(A.keys, z.sid != FZ_NOCHAIN ? z.key : 0u);
+        // the key words of the lane's last stream, under the same wait,
+        // when the lane's previous group left another key's words
+        {
+            const uint32_t want = z.sid != FZ_NOCHAIN ? z.key : 0u;
+            if (want != K.slot)
+                K.load(A.keys, want);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const uint32_t k0 = (L * D) >> 4;
         const StgImg I{ img + k0, (k0 / 48) & 3, D, A.in + off };
