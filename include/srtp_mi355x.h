@@ -439,6 +439,10 @@ int srtp_mi355x_gpu_available(void);
  * order), to reach the key-usage soft / hard limits in tests */
 srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
                                                   uint64_t num_left);
+/* test hook: uses left on master key j of stream `ssrc` (key.c:74-90's
+ * counter, after the device state came back) */
+srtp_err_status_t srtp_mi355x_debug_key_left(srtp_t ctx, uint32_t ssrc,
+                                             size_t j, uint64_t *num_left);
 
 /* test hook: make the next `count` waits for the device pre-pass verdict
  * (srtp_protect_device_async) or drains of a queued async batch report a

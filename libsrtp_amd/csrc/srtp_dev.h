@@ -254,6 +254,11 @@ typedef struct srtp_dev_stream {
                            slot of the key device batches use (the host's
                            devtab mki_j-th master key)                     */
     uint32_t rsv;       /* SRTP_DS_PENDING: the pending ROC                   */
+    uint32_t kbase;     /* MKI streams: the slots of master keys 0..nkeys-1
+                           are mkslot[kbase ..] (srtp_gpu_pp_upload); protect
+                           batches pick one per packet (srtp_gpu_pp_batch_t
+                           mki)                                              */
+    uint32_t nkeys;     /* MKI streams: number of master keys; 0 without MKI */
     uint64_t index;     /* rdbx index (ROC << 16 | SEQ)                      */
     uint64_t uses;      /* packets charged to the key since the upload       */
 } srtp_dev_stream_t;
@@ -270,11 +275,13 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
                        uint32_t ns, const uint32_t *win, uint32_t nwords,
                        const uint32_t *hkey, const uint32_t *hval,
                        uint32_t hcap, const srtp_dev_stream_t *tmpl,
-                       uint32_t spare);
+                       uint32_t spare, const uint32_t *mkslot, uint32_t nmk);
 /* the table back: *ns_now records (the uploaded ones, then the streams
- * created on the device in creation order) and the whole window arena */
+ * created on the device in creation order), the whole window arena and
+ * (kuses, nmk entries; may be NULL) the protect packets charged to each
+ * master key of the MKI streams, mkslot's order */
 int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
-                         uint32_t *win, uint32_t *ns_now);
+                         uint32_t *win, uint32_t *ns_now, uint64_t *kuses);
 
 typedef struct srtp_gpu_pp_batch {
     size_t n;
@@ -297,6 +304,12 @@ typedef struct srtp_gpu_pp_batch {
                                classify inside the crypto kernel */
     uint32_t max_trailer;   /* protect: the largest tag + MKI of the streams
                                the device may encrypt */
+    const uint8_t *mki;     /* protect, HOST array: each packet's master key
+                               index for the MKI streams (srtp.c:2536-2545;
+                               below every MKI stream's key count: the host
+                               checks), NULL without MKI streams.  The
+                               packets of an MKI stream run on key
+                               mkslot[kbase + mki[i]] and are charged to it */
 } srtp_gpu_pp_batch_t;
 
 /* pre-pass + crypto for protect.  *fallback != 0: nothing was written (no

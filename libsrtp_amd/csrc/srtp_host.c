@@ -201,12 +201,19 @@ typedef struct {
     void *async_stream;     /* ... on this stream                          */
     int async_err;          /* a queued batch failed on the GPU: sticky,
                                every later packet call returns _fail      */
-    /* MKI streams (srtp.c:1961-2036): device batches use master key mki_j
-     * of each; protect batches select it by a uniform mki_index, receive
-     * batches follow the key the host path last matched (rx_hint) */
+    /* MKI streams (srtp.c:1961-2036): protect batches run each packet on
+     * the master key its mki_index selects (the slots of every stream's
+     * keys in mkslot, the packets charged to each counted in kuses);
+     * receive batches use master key mki_j, the key the host path last
+     * matched (rx_hint) */
     int has_mki;
     uint32_t mki_j;
     uint32_t rx_hint;
+    uint32_t *mkslot, nmk;  /* key slots of the MKI streams' keys          */
+    uint64_t *kuses;        /* downloaded per-key protect charges          */
+    uint32_t mki_nmin;      /* fewest master keys of a protect-eligible
+                               MKI stream                                  */
+    uint32_t tmpl_kbase;    /* the template's keys in mkslot               */
     /* streams with a pending ROC (srtp_stream_set_roc) the device may take:
      * resolved per batch (pend_resolve); the ones the running batch applied */
     uint32_t *pend, npend;
@@ -2861,8 +2868,8 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
     if (!n)
         return srtp_err_status_ok;
     {
-        /* MKI: one mki_index for the whole batch runs on the device
-         * (protect_device_fast, dev_mki_select) */
+        /* MKI: each packet's mki_index picks its key on the device
+         * (protect_device_fast, dev_mki_index) */
         size_t done = 0;
         int fast = batch_device_run(ctx, 0, n, rtp, rtp_len, srtp, srtp_len,
                                     mki_index, status, &done);
@@ -3300,18 +3307,28 @@ static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
 static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
                        srtp_dev_stream_t *d, int *first, int *rx_first)
 {
-    /* MKI streams: master key mki_j, ineligible if they have fewer */
+    /* MKI streams: receive batches use master key mki_j (ineligible if the
+     * stream has fewer); protect batches pick a key per packet from the
+     * stream's list in mkslot */
     const int mki_ok = !st->use_mki || dt->mki_j < st->keys->n;
     const hkey_t *k = &st->keys->k[st->use_mki && mki_ok ? dt->mki_j : 0];
     memset(d, 0, sizeof *d);
     d->ssrc = st->ssrc;
     d->key = k->slot;
     d->variant = k->variant;
+    uint64_t left = k->num_left;   /* protect: the least of the stream's keys */
     if (st->use_mki) {
         dt->has_mki = 1;
         const uint32_t back = (uint32_t)st->mki_size +
             (k->family == SRTP_DEV_GCM ? 0u : (uint32_t)k->tag_len);
         d->mki = (uint32_t)st->mki_size | (back << 16);
+        d->kbase = dt->nmk;
+        d->nkeys = (uint32_t)st->keys->n;
+        for (size_t j = 0; j < st->keys->n; j++) {
+            dt->mkslot[dt->nmk++] = st->keys->k[j].slot;
+            if (st->keys->k[j].num_left < left)
+                left = st->keys->k[j].num_left;
+        }
     }
     /* header-extension encryption / cryptex streams and routed keys: host
      * pre-pass.  A pending ROC is resolved per batch (pend_resolve) */
@@ -3320,10 +3337,12 @@ static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
         d->flags |= SRTP_DS_PENDING;
         d->rsv = st->rdbx.pending_roc;
     }
-    if (mki_ok && !xs && (templ || st->direction != DIR_RECEIVER)) {
+    if (!xs && (templ || st->direction != DIR_RECEIVER)) {
         d->flags |= SRTP_DS_ELIGIBLE;
-        if (k->num_left < dt->num_left_min)
-            dt->num_left_min = k->num_left;
+        if (st->use_mki && st->keys->n < dt->mki_nmin)
+            dt->mki_nmin = (uint32_t)st->keys->n;
+        if (left < dt->num_left_min)
+            dt->num_left_min = left;
         if (*first)
             dt->uniform = k->slot;
         else if (dt->uniform != k->slot)
@@ -3380,6 +3399,18 @@ static int dev_build(srtp_t ctx)
     free(dt->hwin);
     free(dt->pend);
     free(dt->res);
+    free(dt->mkslot);
+    free(dt->kuses);
+    size_t nmk = 1;   /* the MKI streams' keys (and the template's) */
+    for (size_t i = 0; i < ctx->n; i++)
+        if (ctx->list[i]->use_mki)
+            nmk += ctx->list[i]->keys->n;
+    if (tp && tp->use_mki)
+        nmk += tp->keys->n;
+    dt->mkslot = (uint32_t *)malloc(nmk * sizeof(uint32_t));
+    dt->kuses = (uint64_t *)calloc(nmk, sizeof(uint64_t));
+    dt->nmk = 0;
+    dt->mki_nmin = UINT32_MAX;
     dt->pend = (uint32_t *)malloc((ns + 1) * sizeof(uint32_t));
     dt->res = (uint32_t *)malloc((ns + 1) * sizeof(uint32_t));
     dt->npend = dt->nres = 0;
@@ -3395,7 +3426,7 @@ static int dev_build(srtp_t ctx)
     uint32_t *hv = (uint32_t *)malloc(hcap * 4);
     int rc = -1;
     if (!dt->sv || !dt->hs || !dt->hwin || !hk || !hv || !dt->pend ||
-        !dt->res)
+        !dt->res || !dt->mkslot || !dt->kuses)
         goto out;
     dt->num_left_min = UINT64_MAX;
     dt->uniform = dt->rx_uniform = 0xffffffffu;
@@ -3420,6 +3451,7 @@ static int dev_build(srtp_t ctx)
     if (tmpl_ok) {
         dev_record(dt, tp, 1, &td, &first, &rx_first);
         td.win_off = woff;   /* the spare windows (zero) follow */
+        dt->tmpl_kbase = td.kbase;
     }
     for (size_t h = 0; h < hcap; h++)
         hv[h] = 0xffffffffu;
@@ -3435,7 +3467,8 @@ static int dev_build(srtp_t ctx)
     }
     if (srtp_gpu_pp_upload(ctx->gpu, dt->hs, ns, dt->hwin,
                            woff + (uint32_t)(spare * tw), hk, hv,
-                           (uint32_t)hcap, tmpl_ok ? &td : NULL, spare))
+                           (uint32_t)hcap, tmpl_ok ? &td : NULL, spare,
+                           dt->mkslot, dt->nmk))
         goto out;
     dt->ns = ns;
     dt->nwords = woff;
@@ -3483,31 +3516,29 @@ static int async_drain(srtp_t ctx)
 
 static void dev_pull(srtp_t ctx);
 
-/* MKI sessions: the master key a protect batch selects (mki_index, one per
- * packet, srtp.c:2536-2545) must be one for the whole batch to run on the
- * device; a change of key rebuilds the device table (the device-advanced
- * state comes back first, its key uses charged to the previous key).
- * Returns 1 when the batch must take the host path. */
-static int dev_mki_select(srtp_t ctx, const uint8_t *m8, const size_t *m64,
-                          size_t n)
+/* MKI sessions: the master key each protect packet selects (mki_index,
+ * srtp.c:2536-2545) runs on the device when it is below every MKI stream's
+ * key count; otherwise (srtp_err_status_bad_mki for some packet) the batch
+ * takes the host path.  *out: the indices as bytes for the device (NULL:
+ * the caller passed none, every packet uses key 0).  Returns 1 for the
+ * host path, -1 on allocation failure. */
+static int dev_mki_index(srtp_t ctx, const uint8_t *m8, const size_t *m64,
+                         size_t n, uint8_t **out)
 {
     devtab_t *dt = &ctx->dt;
-    const size_t j = m64 ? m64[0] : m8 ? m8[0] : 0;
-    for (size_t i = 1; (m8 || m64) && i < n; i++)
-        if ((m64 ? m64[i] : m8[i]) != j) {
+    uint8_t *o = (uint8_t *)calloc(n ? n : 1, 1);
+    if (!o)
+        return -1;
+    for (size_t i = 0; (m8 || m64) && i < n; i++) {
+        const size_t j = m64 ? m64[i] : m8[i];
+        if (j >= dt->mki_nmin) {
+            free(o);
             dt->last_abort = 256;
             return 1;
         }
-    if (j > 0xffffffffu) {
-        dt->last_abort = 256;
-        return 1;
+        o[i] = (uint8_t)j;
     }
-    if ((uint32_t)j != dt->mki_j) {
-        dev_pull(ctx);
-        dt->mki_j = (uint32_t)j;
-        if (dev_build(ctx))
-            return 1;
-    }
+    *out = o;
     return 0;
 }
 
@@ -3542,7 +3573,8 @@ static void dev_pull(srtp_t ctx)
         return;
     dt->dirty = 0;
     uint32_t ns_now = 0;
-    if (srtp_gpu_pp_download(ctx->gpu, dt->hs, dt->hwin, &ns_now)) {
+    if (srtp_gpu_pp_download(ctx->gpu, dt->hs, dt->hwin, &ns_now,
+                             dt->kuses)) {
         log_msg(srtp_log_level_error, "device stream table download failed");
         return;
     }
@@ -3551,7 +3583,14 @@ static void dev_pull(srtp_t ctx)
         const srtp_dev_stream_t *d = &dt->hs[sid];
         st->rdbx.index = d->index;
         memcpy(st->rdbx.w, dt->hwin + d->win_off, st->rdbx.bits / 8);
-        st->keys->k[st->use_mki ? dt->mki_j : 0].num_left -= d->uses;
+        /* uses: the packets charged to the stream's device key (receive
+         * batches of MKI streams: key mki_j); kuses: protect packets of
+         * MKI streams, per master key */
+        const size_t kj = st->use_mki ? dt->mki_j : 0;
+        if (kj < st->keys->n)
+            st->keys->k[kj].num_left -= d->uses;
+        for (uint32_t j = 0; j < d->nkeys; j++)
+            st->keys->k[j].num_left -= dt->kuses[d->kbase + j];
         /* a device batch never used a stream against its direction (the
          * eligibility flags), so no ssrc_collision event is due here */
         if (st->direction == DIR_UNKNOWN && (d->dir & SRTP_DIR_TX))
@@ -3566,9 +3605,14 @@ static void dev_pull(srtp_t ctx)
      * keys, whose usage they still count (the clones share its limit,
      * srtp_key_limit_clone) */
     srtp_stream_ctx_t *tp = ctx->templ;
+    if (tp && dt->tmpl_ok && tp->use_mki)
+        for (size_t j = 0; j < tp->keys->n; j++)
+            tp->keys->k[j].num_left -= dt->kuses[dt->tmpl_kbase + j];
     for (uint32_t sid = dt->ns; tp && sid < ns_now; sid++) {
         const srtp_dev_stream_t *d = &dt->hs[sid];
-        tp->keys->k[tp->use_mki ? dt->mki_j : 0].num_left -= d->uses;
+        const size_t kj = tp->use_mki ? dt->mki_j : 0;
+        if (kj < tp->keys->n)
+            tp->keys->k[kj].num_left -= d->uses;
         if (!(d->dir & (SRTP_DIR_TX | SRTP_DIR_RX)))
             continue;
         srtp_stream_ctx_t *st = stream_clone(tp, d->ssrc);
@@ -3734,16 +3778,21 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     }
     if (!dt->valid && dev_build(ctx))
         return -1;
-    if (dt->has_mki && dev_mki_select(ctx, b->mki_index, mki_wide, b->n))
-        return 0;
     /* no key can reach its soft limit inside this batch (key.c:74-90) */
     if (dt->num_left_min == UINT64_MAX ||
         dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT) {
         dt->last_abort = 128;
         return 0;
     }
+    uint8_t *mki8 = NULL;
+    if (dt->has_mki) {
+        const int r = dev_mki_index(ctx, b->mki_index, mki_wide, b->n, &mki8);
+        if (r)
+            return r < 0 ? -1 : 0;
+    }
     srtp_gpu_pp_batch_t pb;
     memset(&pb, 0, sizeof pb);
+    pb.mki = mki8;
     pb.n = b->n;
     pb.in = b->in;
     pb.in_off = b->in_off;
@@ -3753,7 +3802,8 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     pb.out_len = b->out_len;
     pb.status = b->status;
     pb.stream = b->stream;
-    pb.uniform_key = dt->uniform;
+    /* MKI streams: a key per packet */
+    pb.uniform_key = mki8 ? 0xffffffffu : dt->uniform;
     pb.mask = dt->mask;
     pb.async = async;
     /* the order-free form may classify inside the AES-ICM kernel: in place
@@ -3764,11 +3814,13 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->mask &&
                   (dt->mask & (dt->mask - 1)) == 0 &&
                   fused_variant(dt->mask, dt->uniform) &&
-                  dt->max_trailer <= 16 && !async;
+                  dt->max_trailer <= 16 && !async && !mki8;
     pb.max_trailer = dt->max_trailer;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
-    if (pp_run(ctx, &pb, 0, &fallback))
+    const int rr = pp_run(ctx, &pb, 0, &fallback);
+    free(mki8);
+    if (rr)
         return -1;
     if (fallback) {
         dt->last_abort = fallback;
@@ -4714,6 +4766,21 @@ srtp_err_status_t srtp_mi355x_debug_set_key_limit(srtp_t ctx, uint32_t ssrc,
         return srtp_err_status_no_ctx;
     st->keys->k[0].num_left = num_left;
     ctx->dt.valid = 0;   /* the device table's key bound is stale */
+    return srtp_err_status_ok;
+}
+
+srtp_err_status_t srtp_mi355x_debug_key_left(srtp_t ctx, uint32_t ssrc,
+                                             size_t j, uint64_t *num_left)
+{
+    if (!ctx || !num_left)
+        return srtp_err_status_bad_param;
+    dev_pull(ctx);
+    srtp_stream_ctx_t *st = map_get(ctx, ssrc);
+    if (!st)
+        return srtp_err_status_no_ctx;
+    if (j >= st->keys->n)
+        return srtp_err_status_bad_param;
+    *num_left = st->keys->k[j].num_left;
     return srtp_err_status_ok;
 }
 

@@ -160,6 +160,14 @@ struct PpState {
     bool has_tmpl = false;
     uint32_t ns0 = 0, spare = 0, tw = 0;
     uint32_t *cl_ctl = nullptr;                // [0] created, [1] flags
+    // MKI streams: the key slots of their master keys (srtp_dev_stream_t
+    // kbase / nkeys), the protect packets charged to each, and the batch's
+    // per-packet key indices (srtp_gpu_pp_batch_t mki)
+    uint32_t *mkslot = nullptr;
+    unsigned long long *kuses = nullptr;
+    uint32_t nmk = 0, nmk_cap = 0;
+    uint8_t *mki8 = nullptr;
+    size_t mki8_cap = 0;
 };
 
 // the host reads the published abort word after the stream synchronises
@@ -687,6 +695,49 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
     const uint32_t off = st[s].win_off, words = st[s].win_bits >> 5;
     for (uint32_t w = 0; w < words; w++)
         win[off + w] = wnew[off + w];
+}
+
+// MKI streams on protect (srtp.c:2536-2545, srtp_get_session_keys): every
+// packet of an MKI stream runs on the master key its mki_index selects and
+// is charged to that key (key.c:74-90).  After the pre-pass committed (the
+// sorted / order-free / one-stream forms; not the fused ones), each packet
+// whose stream the classification found -- the packets it charged to the
+// stream -- moves its charge from `uses` to kuses[kbase + j], and a packet
+// with a crypto descriptor takes key mkslot[kbase + j].  j is below every
+// MKI stream's key count (the host checked).
+__global__ void k_mki_keys(const uint8_t *in, const uint64_t *in_off,
+                           const uint32_t *in_len, srtp_dev_stream_t *st,
+                           const uint32_t *hkey, const uint32_t *hval,
+                           uint32_t hmask, uint32_t n, const uint8_t *mki,
+                           const uint32_t *mkslot, unsigned long long *kuses,
+                           srtp_dev_meta_t *meta, const uint32_t *abort)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || *abort)
+        return;
+    const uint64_t off = in_off[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
+    if (h.enc_start >> 24)
+        return;   // no stream touched
+    uint32_t sid = NOCHAIN;
+    uint32_t p = map_hash(h.ssrc, hmask);
+    for (uint32_t probe = 0; probe <= hmask; probe++) {
+        const uint32_t v = hval[p];
+        if (v == NOCHAIN)
+            break;
+        if (hkey[p] == h.ssrc) {
+            sid = v;
+            break;
+        }
+        p = (p + 1) & hmask;
+    }
+    if (sid == NOCHAIN || st[sid].nkeys == 0)
+        return;
+    const uint32_t k = st[sid].kbase + mki[i];
+    atomicAdd(&kuses[k], 1ull);
+    atomicAdd((unsigned long long *)&st[sid].uses, ~0ull);   // - 1
+    if (SRTP_META_STATUS(meta[i].info) == 0)
+        meta[i].key = mkslot[k];
 }
 
 // An in-place batch classified inside the crypto kernel that the pre-pass
@@ -2693,7 +2744,8 @@ void srtp_gpu_pp_free(void *p)
                      P->fz_emin, P->fz_bmap, P->fz_hicand, P->fz_nfail,
                      P->fz_glist, P->pd_first, P->pd_min, P->pd_max,
                      P->pd_sids, P->pd_info, P->pd_efirst, P->pd_bak,
-                     P->pd_bakwin, P->pd_pos, P->cl_ctl };
+                     P->pd_bakwin, P->pd_pos, P->cl_ctl, P->mkslot,
+                     P->kuses, P->mki8 };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -2706,7 +2758,7 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
                        uint32_t ns_up, const uint32_t *win, uint32_t nwords,
                        const uint32_t *hkey, const uint32_t *hval,
                        uint32_t hcap, const srtp_dev_stream_t *tmpl,
-                       uint32_t spare)
+                       uint32_t spare, const uint32_t *mkslot, uint32_t nmk)
 {
     PpState *P = pp_of(g);
     hipStream_t stream = (hipStream_t)srtp_gpu_stream_of(g);
@@ -2754,6 +2806,15 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
         PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
                                       0));
     }
+    if (nmk) {
+        uint32_t c14 = P->nmk_cap;
+        if (regrow(&P->mkslot, &P->nmk_cap, nmk) || regrow(&P->kuses, &c14, nmk))
+            return -1;
+        PPCHK(hipMemcpyAsync(P->mkslot, mkslot, nmk * 4ull,
+                             hipMemcpyHostToDevice, stream));
+        PPCHK(hipMemsetAsync(P->kuses, 0, nmk * 8ull, stream));
+    }
+    P->nmk = nmk;
     if (!P->cl_ctl)
         PPCHK(hipMalloc((void **)&P->cl_ctl, 8));
     PPCHK(hipMemsetAsync(P->cl_ctl, 0, 8, stream));
@@ -2785,7 +2846,7 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
 }
 
 int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
-                         uint32_t *win, uint32_t *ns_now)
+                         uint32_t *win, uint32_t *ns_now, uint64_t *kuses)
 {
     PpState *P = pp_of(g);
     *ns_now = P->ns;
@@ -2794,6 +2855,9 @@ int srtp_gpu_pp_download(srtp_gpu_t *g, srtp_dev_stream_t *streams,
                          hipMemcpyDeviceToHost, stream));
     if (P->nwords)
         PPCHK(hipMemcpyAsync(win, P->win, P->nwords * 4ull,
+                             hipMemcpyDeviceToHost, stream));
+    if (kuses && P->nmk)
+        PPCHK(hipMemcpyAsync(kuses, P->kuses, P->nmk * 8ull,
                              hipMemcpyDeviceToHost, stream));
     PPCHK(hipStreamSynchronize(stream));
     return 0;
@@ -3058,6 +3122,38 @@ static int chain1_fail(PpState *P, hipStream_t stream)
 
 // the one-stream chain form in two launches (k_pp_chain1 + commit), then
 // the crypto kernels; see k_pp_chain1
+// MKI streams: the batch's per-packet key indices to the device (before
+// any kernel of the batch; synchronous: the host array is the caller's)
+static int mki_stage(PpState *P, const srtp_gpu_pp_batch_t *b,
+                     hipStream_t stream)
+{
+    if (!b->mki)
+        return 0;
+    if (b->n > P->mki8_cap) {
+        if (P->mki8)
+            PPCHK(hipFree(P->mki8));
+        P->mki8 = nullptr;
+        PPCHK(hipMalloc((void **)&P->mki8, b->n));
+        P->mki8_cap = b->n;
+    }
+    PPCHK(hipStreamSynchronize(stream));
+    PPCHK(hipMemcpy(P->mki8, b->mki, b->n, hipMemcpyHostToDevice));
+    return 0;
+}
+
+// ... and, after the commit, every MKI stream packet's key (k_mki_keys)
+static void mki_keys(PpState *P, const srtp_gpu_pp_batch_t *b,
+                     const uint32_t *abort, hipStream_t stream)
+{
+    if (!b->mki)
+        return;
+    const uint32_t N = (uint32_t)b->n;
+    hipLaunchKernelGGL(k_mki_keys, dim3((N + 255) / 256), dim3(256), 0, stream,
+                       b->in, b->in_off, b->in_len, P->st, P->hkey, P->hval,
+                       P->hcap - 1, N, P->mki8, P->mkslot, P->kuses, P->meta,
+                       abort);
+}
+
 static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
                              hipStream_t stream, int *fallback)
 {
@@ -3122,6 +3218,7 @@ static int pp_protect_chain1(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     }
     if (pp_step(stream, "chain1_commit"))
         return chain1_fail(P, stream);
+    mki_keys(P, b, ab, stream);
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
     cb.in = b->in;
@@ -3262,7 +3359,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return 0;
     }
     hipStream_t stream = (hipStream_t)b->stream;   // NULL = the null stream
-    if (reserve_packets(P, n, stream) || pp_step(stream, "reserve"))
+    if (reserve_packets(P, n, stream) || pp_step(stream, "reserve") ||
+        mki_stage(P, b, stream))
         return -1;
     const uint32_t N = (uint32_t)n, ns = P->ns;
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
@@ -3276,7 +3374,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return e && *e == '1';
     }();
     bool unordered = ns > 1 && !force_sorted;
-    if (unordered && b->fused_ok && fused_of_on() &&
+    if (unordered && b->fused_ok && !b->mki && fused_of_on() &&
         !(b->uniform_key == 0xffffffffu && buckets_on())) {
         bool sorted = false;
         if (pp_protect_fused(g, P, b, stream, fallback, &sorted))
@@ -3377,6 +3475,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     PPCHK(hipGetLastError());
     if (pp_step(stream, "commit_stream"))
         return -1;
+    mki_keys(P, b, P->abort, stream);
 
     srtp_gpu_batch_t cb = {};
     if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&

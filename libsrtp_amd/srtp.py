@@ -149,6 +149,8 @@ def lib():
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
         "srtp_mi355x_prepass_sorted_batches": ([P], C.c_uint64),
+        "srtp_mi355x_debug_key_left": ([P, C.c_uint32, C.c_size_t,
+                                        C.POINTER(C.c_uint64)], C.c_int),
         "srtp_mi355x_debug_set_key_limit": ([P, C.c_uint32, C.c_uint64],
                                             C.c_int),
         "srtp_mi355x_debug_inject_failure": ([C.c_int, C.c_int], None),
@@ -546,6 +548,12 @@ class Session:
         d, h = C.c_uint64(), C.c_uint64()
         self.L.srtp_mi355x_prepass_stats(self.h, C.byref(d), C.byref(h))
         return d.value, h.value
+
+    def debug_key_left(self, ssrc, j=0):
+        """uses left of master key j of the stream (key limit counter)"""
+        v = C.c_uint64()
+        rc = self.L.srtp_mi355x_debug_key_left(self.h, ssrc, j, C.byref(v))
+        return Status(rc), v.value
 
     def debug_set_key_limit(self, ssrc, num_left):
         return Status(self.L.srtp_mi355x_debug_set_key_limit(self.h, ssrc,

@@ -57,6 +57,8 @@ def lib():
                                   C.POINTER(C.c_size_t), C.c_size_t]
         L.orc_unprotect.argtypes = [C.c_void_p, P, C.c_size_t, P,
                                     C.POINTER(C.c_size_t)]
+        L.orc_key_left.argtypes = [C.c_void_p, C.c_uint32, C.c_size_t,
+                                   C.POINTER(C.c_uint64)]
         L.orc_get_roc.argtypes = [C.c_void_p, C.c_uint32,
                                   C.POINTER(C.c_uint32)]
         L.orc_set_roc.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
@@ -208,6 +210,12 @@ class Session:
 
     def set_roc(self, ssrc, roc):
         return lib().orc_set_roc(self.h, ssrc, roc)
+
+    def key_left(self, ssrc, j=0):
+        """uses left of master key j of the stream (key limit counter)"""
+        v = C.c_uint64()
+        rc = lib().orc_key_left(self.h, ssrc, j, C.byref(v))
+        return rc, v.value
 
     def __del__(self):
         try:

@@ -1299,6 +1299,16 @@ int orc_get_roc(orc_session_t *s, uint32_t ssrc, uint32_t *roc)
     return ST_OK;
 }
 
+/* the uses left of master key j of stream ssrc (key.c:74-90's counter) */
+int orc_key_left(orc_session_t *s, uint32_t ssrc, size_t j, uint64_t *left)
+{
+    stream_t *st = list_get(s, ssrc);
+    if (!st || j >= st->num_keys)
+        return ST_BAD_PARAM;
+    *left = st->keys[j].limit->num_left;
+    return ST_OK;
+}
+
 int orc_set_roc(orc_session_t *s, uint32_t ssrc, uint32_t roc)
 {
     stream_t *st = list_get(s, ssrc);

@@ -98,6 +98,7 @@ int orc_unprotect(orc_session_t *s, const uint8_t *srtp, size_t srtp_len,
                   uint8_t *rtp, size_t *rtp_len);
 int orc_get_roc(orc_session_t *s, uint32_t ssrc, uint32_t *roc);
 int orc_set_roc(orc_session_t *s, uint32_t ssrc, uint32_t roc);
+int orc_key_left(orc_session_t *s, uint32_t ssrc, size_t j, uint64_t *left);
 
 /* Derived session keys for a master key (KDF, srtp/srtp.c:1070-1142,
  * 1233-1607): enc key, salt (14 or 12 bytes), auth key (20). */

@@ -882,15 +882,26 @@ def _device_run(sess, pkts, caps, op, mki=None):
                 for o, c, s in zip(offs, cap, st)]
 
 
+def _key_left_equal(lib, orc, ssrcs, nkeys):
+    for s in ssrcs:
+        for j in range(nkeys):
+            rc, got = lib.debug_key_left(s, j)
+            orc_rc, want = orc.key_left(s, j)
+            assert rc == 0 and orc_rc == 0, (s, j, rc, orc_rc)
+            assert got == want, (hex(s), j, got, want)
+
+
 @pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
 def test_mki_streams_on_device_prepass(name):
-    """MKI streams (srtp.c:1961-2036) on the device pre-pass: protect
-    batches with one mki_index for the batch run on the device with that
-    master key (a change of key rebuilds the device table); a batch mixing
-    keys takes the host path.  Receive batches run on the device with the
-    key the host path matched last; a batch carrying another key's MKI
-    goes back to the host (AB_MKI), the next one is on the device again.
-    Every status and byte against the oracle, one packet at a time."""
+    """MKI streams (srtp.c:1961-2036, 2536-2545) on the device pre-pass:
+    protect batches run every packet on the master key its mki_index
+    selects -- one index for the batch or a different one per packet -- and
+    charge the use to that key (key.c:74-90); a batch with an index past a
+    stream's keys (bad_mki) takes the host path.  Receive batches run on the
+    device with the key the host path matched last; a batch carrying another
+    key's MKI goes back to the host (AB_MKI), the next one is on the device
+    again.  Every status and byte against the oracle, one packet at a time,
+    and every key's remaining uses."""
     _gpu()
     rng = random.Random(613)
     ssrcs = [0x22000000 + 3 * k for k in range(24)]
@@ -900,37 +911,81 @@ def test_mki_streams_on_device_prepass(name):
     rcv, orc_r = L.Session(pols), O.Session(pols)
     seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
     plan = [("uniform", 0, 1), ("uniform", 2, 1), ("uniform", 2, 1),
-            ("mixed", None, 0), ("uniform", 1, 1)]
+            ("mixed", None, 1), ("mixed", None, 1), ("bad", None, 0),
+            ("uniform", 1, 1), ("uniform", 1, 1), ("mixed", None, 1)]
     d0, h0 = 0, 0
     for kind, j, dev in plan:
         pk = _interleaved(rng, ssrcs, seq0, 12, payloads=(0, 7, 160))
         mki = [j] * len(pk) if kind == "uniform" else \
             [rng.randrange(3) for _ in pk]
+        if kind == "bad":
+            mki[rng.randrange(len(pk))] = 3   # srtp_err_status_bad_mki
         caps = [len(p) + 32 for p in pk]
+        for i in rng.sample(range(len(pk)), 5):
+            caps[i] = len(pk[i]) + 2           # buffer_small: charged too
         st, out = _device_run(snd, pk, caps, "protect", mki)
         sent = []
         for i, p in enumerate(pk):
             rc, ref = orc.protect(p, caps[i], mki[i])
             assert st[i] == rc, (kind, i, st[i], rc)
             assert rc or out[i] == ref, (kind, i)
-            sent.append(ref)
+            if rc == 0:
+                sent.append(ref)
         d, h = snd.prepass_stats()
         assert (d - d0, h - h0) == ((1, 0) if dev else (0, 1)), (kind, j)
         d0, h0 = d, h
+        _key_left_equal(snd, orc, ssrcs[::4], 3)
         # the receiver: first batch of a new key on the host, then device
-        rd0, rh0 = rcv.prepass_stats()
         st, out = _device_run(rcv, sent, [len(p) for p in sent], "unprotect")
         for i, p in enumerate(sent):
             rc, ref = orc_r.unprotect(p, len(p))
             assert st[i] == rc, ("rx", kind, i, st[i], rc)
             assert rc or out[i] == ref, ("rx", kind, i)
     rd, rh = rcv.prepass_stats()
-    # keys 0, 2, 2, mixed, 1: the batches after a key change and the mixed
-    # one are host batches, the rest device
-    assert rd >= 2 and rh >= 2, (rd, rh)
+    # keys 0, 2, 2, mixed, mixed, mixed, 1, 1, mixed: the receiver takes the
+    # host path after a key change and for mixed batches, else the device
+    # (the first 1 may follow a mixed batch whose last match was key 1)
+    assert rd >= 3 and rh >= 5 and rd + rh == len(plan), (rd, rh)
+    _key_left_equal(rcv, orc_r, ssrcs[::4], 3)
     for s in ssrcs[::5]:
         assert snd.get_roc(s)[1] == orc.get_roc(s)[1]
         assert rcv.get_roc(s)[1] == orc_r.get_roc(s)[1]
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_mki_one_stream_mixed_keys_on_device(name):
+    """one MKI stream (the one-stream chain form, k_pp_chain1): 4k-packet
+    protect batches whose packets pick master keys 0-3 at random run on the
+    device, every packet on its key, bytes / statuses / per-key uses equal
+    to the oracle; a second session with a template (ssrc_any_outbound, 4
+    keys) does the same through device-created streams"""
+    _gpu()
+    rng = random.Random(615)
+    ssrc = 0x22400000
+    pols = [policy(name, ssrc=ssrc, seed=3, mki=4, nkeys=4)]
+    for variant in ("stream", "template"):
+        if variant == "template":
+            pols = [dict(policy(name, ssrc=0, seed=5, mki=4, nkeys=4),
+                         ssrc_type=3)]
+            ssrcs = [0x22500000 + k for k in range(37)]
+        else:
+            ssrcs = [ssrc]
+        lib, orc = L.Session(pols), O.Session(pols)
+        seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
+        d0, h0 = lib.prepass_stats()
+        for b in range(3):
+            pk = _interleaved(rng, ssrcs, seq0, 4096 // len(ssrcs),
+                              payloads=(0, 20, 172))
+            mki = [rng.randrange(4) for _ in pk]
+            caps = [len(p) + 32 for p in pk]
+            st, out = _device_run(lib, pk, caps, "protect", mki)
+            for i, p in enumerate(pk):
+                rc, ref = orc.protect(p, caps[i], mki[i])
+                assert st[i] == rc, (variant, b, i, st[i], rc)
+                assert rc or out[i] == ref, (variant, b, i)
+        d, h = lib.prepass_stats()
+        assert (d - d0, h - h0) == (3, 0), (variant, d - d0, h - h0)
+        _key_left_equal(lib, orc, ssrcs[:5], 4)
 
 
 # --------------------------------------------------------------------------
