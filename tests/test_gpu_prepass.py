@@ -1335,6 +1335,39 @@ def test_pending_roc_on_device(op, shape):
     assert lib.get_roc(ahead) == orc.get_roc(ahead)
 
 
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+@pytest.mark.parametrize("ns", [1, 50])
+def test_mki_mixed_keys_with_pending_roc(name, ns):
+    """MKI streams with per-packet keys (k_mki_keys) meeting a pending ROC
+    (k_pend_apply) in the same batch -- the one-stream chain form and the
+    order-free form: every status and byte, every key's remaining uses and
+    the ROCs against the oracle, no batch on the host path"""
+    _gpu()
+    rng = random.Random(720 + ns)
+    ssrcs = [0x28800000 + 9 * k for k in range(ns)]
+    pols = [policy(name, ssrc=s, seed=k, mki=4, nkeys=3)
+            for k, s in enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(0x9000, 0xf000) for s in ssrcs}
+    per = 300 if ns == 1 else 8
+    for b in range(3):
+        if b == 1:
+            for sess in (lib, orc):
+                assert sess.set_roc(ssrcs[0], 4) == 0
+        pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 20, 160))
+        mki = [rng.randrange(3) for _ in pk]
+        caps = [len(p) + 32 for p in pk]
+        st, out = _device_run(lib, pk, caps, "protect", mki)
+        for i, p in enumerate(pk):
+            rc, ref = orc.protect(p, caps[i], mki[i])
+            assert st[i] == rc, (b, i, st[i], rc)
+            assert rc or out[i] == ref, (b, i)
+    d, h = lib.prepass_stats()
+    assert (d, h) == (3, 0), (d, h, lib.prepass_last_abort())
+    _key_left_equal(lib, orc, ssrcs[:4], 3)
+    assert lib.get_roc(ssrcs[0]) == orc.get_roc(ssrcs[0])
+
+
 @pytest.mark.parametrize("shape", ["fused_many", "one_stream"])
 def test_pending_roc_forged_first_packet(shape):
     """receive side: the first packet of a stream with a pending ROC does not
