@@ -192,6 +192,11 @@ typedef struct srtp_gpu_batch {
      * kernel (IcmFused, srtp_gpu_int.h; srtp_prepass.hip pp_protect_fused):
      * meta is written there, not read */
     const void *fused;
+    /* or NULL: one stream's in-order batch, the index of every packet
+     * computed inside the AES-ICM kernel (IcmChain, srtp_gpu_int.h;
+     * srtp_prepass.hip pp_protect_inorder): meta is neither read nor
+     * written */
+    const void *inorder;
 } srtp_gpu_batch_t;
 
 int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b);
@@ -304,6 +309,10 @@ typedef struct srtp_gpu_pp_batch {
                                classify inside the crypto kernel */
     uint32_t max_trailer;   /* protect: the largest tag + MKI of the streams
                                the device may encrypt */
+    int inorder_ok;         /* protect: in place, one uniform-key AES-ICM / GCM
+                               variant, trailers <= 16 bytes, synchronous: a
+                               one-stream batch may try the in-order form
+                               (indices computed in the crypto kernel) */
     const uint8_t *mki;     /* protect, HOST array: each packet's master key
                                index for the MKI streams (srtp.c:2536-2545;
                                below every MKI stream's key count: the host

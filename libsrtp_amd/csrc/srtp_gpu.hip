@@ -1241,6 +1241,9 @@ static int launch_icm(srtp_gpu_t *g, const srtp_gpu_batch_t *b,
     A.fused = b->fused != nullptr;
     if (A.fused)
         A.fz = *(const IcmFused *)b->fused;
+    A.ch = IcmChain{};
+    if (b->inorder)
+        A.ch = *(const IcmChain *)b->inorder;
     static const bool stg = [] {
         const char *e = getenv("SRTP_ICM_STG");
         return !(e && e[0] == '0');
@@ -1277,6 +1280,9 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.fused = b->fused != nullptr;
     if (A.fused)
         A.fz = *(const IcmFused *)b->fused;
+    A.ch = IcmChain{};
+    if (b->inorder)
+        A.ch = *(const IcmChain *)b->inorder;
     return launch_gcm_nr<NR>(A, PROT, g->ncu, st);
 }
 

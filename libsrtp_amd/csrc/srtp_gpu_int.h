@@ -87,6 +87,21 @@ struct IcmFused {
 };
 constexpr uint32_t FZ_GL_WAVES = 4096;   // waves of a persistent grid, max
 
+// One stream's in-order protect batch, classified inside the uniform-key
+// AES-ICM kernel (srtp_prepass.hip pp_protect_inorder): packet i has
+// sequence number seq_0 + i and index e_0 + i, e_0 the stored index's
+// guess for packet 0 -- what the reference's walk gives a sender's
+// consecutive packets (rdbx.c:112-145: every advance is 1).  A packet
+// outside that (or with a length / parse error) is not encrypted and sets
+// *abort; the pre-pass then restores the batch and runs the chain form.
+struct IcmChain {
+    const uint32_t *in_len;
+    const uint32_t *cap;
+    const srtp_dev_stream_t *st;   // the batch's one stream
+    uint32_t *abort;
+    uint32_t (*tsave)[4];          // the trailer bytes the tag overwrites
+};
+
 // AES-ICM (+ HMAC-SHA1) kernel arguments
 struct IcmArgs {
     const uint8_t *in;
@@ -111,6 +126,8 @@ struct IcmArgs {
     // fused batches through the LDS-staged kernel (k_icm_stg; default on,
     // SRTP_ICM_STG=0 selects the per-lane form for A/B runs)
     bool stg;
+    // one stream's in-order batch (ch.st != null), classified here
+    IcmChain ch;
 };
 
 // AES-GCM kernel arguments
@@ -130,6 +147,8 @@ struct GcmArgs {
     // fz valid when fused, meta then neither read nor written
     bool fused;
     IcmFused fz;
+    // one stream's in-order batch (ch.st != null), classified here
+    IcmChain ch;
 };
 
 // records a HIP error in the FFI's error string, returns -1

@@ -3816,6 +3816,15 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
                   fused_variant(dt->mask, dt->uniform) &&
                   dt->max_trailer <= 16 && !async && !mki8;
     pb.max_trailer = dt->max_trailer;
+    /* one stream in order: indices in the crypto kernel (uniform key, one
+     * AES-ICM or AES-GCM variant, in place, synchronous; srtp_prepass.hip
+     * pp_protect_inorder) */
+    pb.inorder_ok = b->in == b->out && b->in_off == b->out_off &&
+                    dt->mask && (dt->mask & (dt->mask - 1)) == 0 &&
+                    ((dt->mask & 0xfc00u) == dt->mask ||
+                     (dt->mask & 0x440000u) == dt->mask) &&
+                    dt->uniform != 0xffffffffu && dt->max_trailer <= 16 &&
+                    !async && !mki8;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     const int rr = pp_run(ctx, &pb, 0, &fallback);

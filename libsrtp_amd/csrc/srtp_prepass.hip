@@ -697,6 +697,124 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
         win[off + w] = wnew[off + w];
 }
 
+// One stream's in-order batch (pp_protect_inorder; the crypto kernel
+// classified every packet, srtp_icm.hip inorder_meta): unless declined,
+// every packet's status 0 and protected length, and the stream moved by n
+// indices -- index e_0 + n - 1, the window shifted by the advance with the
+// bits of the last min(n, window) indices set (rdbx.c:253-270), n key uses
+// (key.c:74-90) -- and the verdict published to the host.
+__global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
+                            const uint32_t *in_len, uint32_t n,
+                            srtp_dev_stream_t *st, uint32_t *win,
+                            const uint32_t *abort, uint32_t *pub,
+                            int32_t *status, uint32_t *out_len)
+{
+    const uint32_t ab = *abort;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    srtp_dev_stream_t &S = st[0];
+    if (i < n && !ab) {
+        status[i] = 0;
+        out_len[i] = in_len[i] + S.trailer;
+    }
+    if (blockIdx.x != 0)
+        return;
+    __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
+    const uint32_t words = S.win_bits >> 5;
+    const uint64_t old = S.index;
+    uint64_t e0 = 0;
+    srtp_guess_index(old, srtp_bswap32(*(const uint32_t *)(in + in_off[0])) & 0xffffu,
+                     &e0);
+    const uint64_t hi = e0 + n - 1;
+    if (!ab) {
+        const uint64_t adv = hi - old;
+        const uint32_t *w = win + S.win_off;
+        const uint32_t setb = n < S.win_bits ? n : S.win_bits;
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x) {
+            uint32_t v = 0;
+            if (adv < S.win_bits) {
+                const uint32_t b0 = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+                const uint32_t a = x + b0 < words ? w[x + b0] : 0u;
+                const uint32_t b = x + b0 + 1 < words ? w[x + b0 + 1] : 0u;
+                v = bi ? (a >> bi) | (b << (32 - bi)) : a;
+            }
+            // bits [win_bits - setb, win_bits): the batch's last indices
+            const uint32_t lo = S.win_bits - setb, base = 32 * x;
+            for (uint32_t k = 0; k < 32; k++)
+                if (base + k >= lo)
+                    v |= 1u << k;
+            s_win[x] = v;
+        }
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x)
+            win[S.win_off + x] = s_win[x];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!ab) {
+            S.uses += n;
+            S.dir |= SRTP_DIR_TX;
+            S.index = hi;
+        }
+        if (pub)
+            __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// ... declined: the descriptors of the packets the kernel encrypted (the
+// same test as inorder_meta) for the keystream undo, and their trailer
+// bytes back
+__global__ void k_io_restore_meta(const uint8_t *in, const uint64_t *in_off,
+                                  const uint32_t *in_len, const uint32_t *cap,
+                                  uint32_t n, const srtp_dev_stream_t *st,
+                                  srtp_dev_meta_t *meta)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const srtp_dev_stream_t S = st[0];
+    const uint32_t seq0 = srtp_bswap32(*(const uint32_t *)(in + in_off[0])) & 0xffffu;
+    uint64_t e0 = 0;
+    const bool e0ok = (S.flags & SRTP_DS_ELIGIBLE) && !(S.dir & SRTP_DIR_RX) &&
+                      srtp_guess_index(S.index, seq0, &e0) >= 1;
+    const uint64_t off = in_off[i];
+    const uint32_t len = in_len[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, len);
+    srtp_dev_meta_t m;
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;
+    const bool ok = e0ok && (h.enc_start >> 24) == 0 && h.ssrc == S.ssrc &&
+                    (h.seq_len & 0xffffu) == ((seq0 + i) & 0xffffu) &&
+                    h.enc_start <= len && cap[i] >= len + S.trailer &&
+                    !((S.flags & SRTP_DS_ICM_CONF) &&
+                      (len - h.enc_start + 15) / 16 > 0xffffu);
+    if (ok) {
+        const uint64_t e = e0 + i;
+        m.key = S.key;
+        m.roc = (uint32_t)(e >> 16);
+        m.info = h.enc_start | (S.variant << 24);
+        m.len = len;
+    }
+    meta[i] = m;
+}
+
+__global__ void k_io_restore_tail(uint8_t *arena, const uint64_t *off,
+                                  const uint32_t *in_len,
+                                  const srtp_dev_stream_t *st,
+                                  const srtp_dev_meta_t *meta,
+                                  const uint32_t (*tsave)[4], uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || SRTP_META_STATUS(meta[i].info))
+        return;
+    const uint32_t tn = st[0].trailer < 16 ? st[0].trailer : 16;
+    uint8_t *p = arena + off[i] + in_len[i];
+    for (uint32_t b = 0; b < tn; b++)
+        p[b] = (uint8_t)(tsave[i][b >> 2] >> (8 * (b & 3)));
+}
+
 // MKI streams on protect (srtp.c:2536-2545, srtp_get_session_keys): every
 // packet of an MKI stream runs on the master key its mki_index selects and
 // is charged to that key (key.c:74-90).  After the pre-pass committed (the
@@ -3107,6 +3225,16 @@ static bool fused_on()
     return on;
 }
 
+// SRTP_PP_INORDER=0: one-stream batches skip the in-order form (A/B runs)
+static bool inorder_on()
+{
+    static const bool on = [] {
+        const char *e = getenv("SRTP_PP_INORDER");
+        return !(e && *e == '0');
+    }();
+    return on;
+}
+
 // An error after k_pp_chain1 was queued: only k_pp_chain1_commit zeroes the
 // look-back words, the tile ticket / key-use counters and the next batch's
 // abort word, so they are zeroed here (else the next one-stream batch would
@@ -3122,6 +3250,69 @@ static int chain1_fail(PpState *P, hipStream_t stream)
 
 // the one-stream chain form in two launches (k_pp_chain1 + commit), then
 // the crypto kernels; see k_pp_chain1
+// One stream, in place, one uniform-key AES-ICM / GCM variant: the in-order form
+// first -- no separate pre-pass kernel, the crypto kernel takes every
+// packet's index from packet 0's (IcmChain) -- then k_io_commit.  A batch
+// that is not a run of consecutive sequence numbers (or has a packet with
+// a length / parse error) is restored and *declined: the chain form runs.
+static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
+                              srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                              int *fallback, bool *declined)
+{
+    const uint32_t N = (uint32_t)b->n;
+    const dim3 blk(256), gp((N + 255) / 256);
+    *declined = false;
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
+    IcmChain Q;
+    Q.in_len = b->in_len;
+    Q.cap = b->out_len;
+    Q.st = P->st;
+    Q.abort = P->abort;
+    Q.tsave = P->tsave;
+    srtp_gpu_batch_t cb = {};
+    cb.n = b->n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;   // not read
+    cb.auth_ok = nullptr;
+    cb.uniform_key = b->uniform_key;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = nullptr;   // the kernel itself classifies: it always runs
+    cb.inorder = &Q;
+    if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "in-order crypto"))
+        return -1;
+    hipLaunchKernelGGL(k_io_commit, gp, blk, 0, stream, b->in, b->in_off,
+                       b->in_len, N, P->st, P->win, P->abort, P->h_abort_dev,
+                       b->status, b->out_len);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "in-order commit"))
+        return -1;
+    PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    if (*(volatile uint32_t *)P->h_abort == 0) {
+        b->sorted = 1;
+        *fallback = 0;
+        return 0;
+    }
+    // declined: the input comes back exactly
+    hipLaunchKernelGGL(k_io_restore_meta, gp, blk, 0, stream, b->in,
+                       b->in_off, b->in_len, b->out_len, N, P->st, P->meta);
+    PPCHK(hipGetLastError());
+    if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
+        return -1;
+    hipLaunchKernelGGL(k_io_restore_tail, gp, blk, 0, stream, b->out,
+                       b->out_off, b->in_len, P->st, P->meta, P->tsave, N);
+    PPCHK(hipGetLastError());
+    PPCHK(hipStreamSynchronize(stream));
+    *declined = true;
+    return 0;
+}
+
 // MKI streams: the batch's per-packet key indices to the device (before
 // any kernel of the batch; synchronous: the host array is the caller's)
 static int mki_stage(PpState *P, const srtp_gpu_pp_batch_t *b,
@@ -3364,8 +3555,16 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         return -1;
     const uint32_t N = (uint32_t)n, ns = P->ns;
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
-    if (ns == 1 && fused_on())
+    if (ns == 1 && fused_on()) {
+        if (b->inorder_ok && inorder_on()) {
+            bool declined = false;
+            if (pp_protect_inorder(g, P, b, stream, fallback, &declined))
+                return -1;
+            if (!declined)
+                return 0;
+        }
         return pp_protect_chain1(g, P, b, stream, fallback);
+    }
 
     // many streams: the order-free form first (no sort); AB_ORDER -> again
     // through the sorted chain path.  SRTP_PP_SORTED=1 forces the latter.

@@ -1442,3 +1442,121 @@ def test_large_host_batch_pipelined_chunks(declined):
         assert st[i] == rc, ("rx", i, st[i], rc)
         assert rc or out[i] == ref, ("rx", i)
     assert rlib.prepass_stats() == (8, 0)
+
+
+# --------------------------------------------------------------------------
+# one stream in order: the indices computed inside the AES-ICM kernel
+# (srtp_prepass.hip pp_protect_inorder, srtp_icm.hip inorder_meta)
+
+def _arena_run(sess, pkts, caps, slot_extra, rng):
+    """srtp_protect_device in place over an arena whose bytes around the
+    packets are random -> (statuses, the arena before, the arena after,
+    offsets)"""
+    import torch
+    offs, pos = [], 0
+    for p, c in zip(pkts, caps):
+        offs.append(pos)
+        pos += (max(len(p), c) + slot_extra + 15) & ~15
+    before = bytearray(rng.randbytes(pos + 16))
+    for o, p in zip(offs, pkts):
+        before[o:o + len(p)] = p
+    arena = torch.frombuffer(bytearray(before), dtype=torch.uint8).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor([len(p) for p in pkts], dtype=torch.int32).cuda()
+    cap = torch.tensor(caps, dtype=torch.int32).cuda()
+    st = torch.full((len(pkts),), -1, dtype=torch.int32).cuda()
+    assert sess.protect_device(arena, off, ln, arena, off, cap, st) == 0
+    return st.cpu().tolist(), bytes(before), arena.cpu().numpy().tobytes(), offs
+
+
+def _check_arena(orc, pkts, caps, st, before, after, offs):
+    """every status and every arena byte against the oracle's per-packet
+    srtp_protect: a protected packet's bytes, the rest untouched"""
+    expect = bytearray(before)
+    for i, p in enumerate(pkts):
+        rc, ref = orc.protect(p, caps[i])
+        assert st[i] == rc, (i, st[i], rc)
+        if rc == 0:
+            expect[offs[i]:offs[i] + len(ref)] = ref
+    if bytes(expect) != after:
+        bad = next(k for k in range(len(after)) if after[k] != expect[k])
+        raise AssertionError("arena byte %d differs" % bad)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
+                                  "icm128_nullauth", "icm128_authonly",
+                                  "gcm256_16", "gcm256_8"])
+def test_one_stream_in_order_form(name):
+    """a sender's batches of consecutive sequence numbers (across a ROC
+    wrap, headers with CSRCs and extensions) take the in-order form; a
+    duplicate, a gap, a too-small buffer or a replayed packet in the batch
+    declines it -- the input comes back exactly and the chain form runs;
+    every status and every arena byte (the slot bytes after each packet
+    included) against the oracle, then the stream's window through a
+    replayed packet"""
+    _gpu()
+    rng = random.Random(731)
+    ssrc = 0x29000000
+    pols = [policy(name, ssrc=ssrc, seed=2)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq = 0xffff - 1500
+
+    def batch(n, tweak=None):
+        nonlocal seq
+        seqs = [(seq + k) & 0xffff for k in range(n)]
+        seq += n
+        pk = []
+        for k, q in enumerate(seqs):
+            cc = rng.choice((0, 0, 0, 2))
+            xw = rng.choice((-1, -1, 1, 3))
+            pk.append(rtp_packet(rng, ssrc, q, rng.choice((0, 7, 160, 1000)),
+                                 cc=cc, xwords=xw))
+        caps = [len(p) + 32 for p in pk]
+        if tweak:
+            tweak(pk, caps)
+        return pk, caps
+
+    def dup(pk, caps):
+        pk[700] = pk[699]
+
+    def gap(pk, caps):
+        nonlocal seq
+        seq += 1                        # the next batch continues after it
+        for k in range(900, len(pk)):   # one advance of 2 from packet 900 on
+            p = bytearray(pk[k])
+            q = ((p[2] << 8) | p[3]) + 1
+            p[2], p[3] = (q >> 8) & 0xff, q & 0xff
+            pk[k] = bytes(p)
+
+    def small(pk, caps):
+        caps[1234] = len(pk[1234]) + 3
+
+    # a fresh stream's first packet 1500 below the sequence wrap: the
+    # reference's first estimate (rdbx.c:112-145 from index 0) is the host
+    # path's; the batches after it run on the device
+    pk, caps = batch(16)
+    st, before, after, offs = _arena_run(lib, pk, caps, 24, rng)
+    _check_arena(orc, pk, caps, st, before, after, offs)
+    plan = [(3000, None), (2000, dup), (2000, gap), (2000, small), (3000, None)]
+    d0, h0 = lib.prepass_stats()
+    sent, where = [], []
+    for n, tw in plan:
+        pk, caps = batch(n, tw)
+        hb = lib.prepass_stats()[1]
+        st, before, after, offs = _arena_run(lib, pk, caps, 24, rng)
+        where.append((lib.prepass_stats()[1] - hb, lib.prepass_last_abort()))
+        _check_arena(orc, pk, caps, st, before, after, offs)
+        sent.append(pk)
+    d, h = lib.prepass_stats()
+    # the duplicate sends its batch to the host (the chain form takes
+    # advances in [1, 2^15) only); the gap and the small buffer stay on the
+    # device through the chain form
+    assert (d - d0, h - h0) == (len(plan) - 1, 1), (d - d0, h - h0, where)
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    # the window the batches left: the last packets again (replay_fail /
+    # replay_old on the sender's side) next to a new one
+    pk = sent[-1][-40:] + sent[0][:3]
+    pk.append(rtp_packet(rng, ssrc, seq & 0xffff, 50))
+    caps = [len(p) + 32 for p in pk]
+    st, before, after, offs = _arena_run(lib, pk, caps, 24, rng)
+    _check_arena(orc, pk, caps, st, before, after, offs)
