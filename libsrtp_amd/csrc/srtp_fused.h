@@ -376,11 +376,10 @@ DEV void fzu_verdict(const ARGS &A, uint32_t i, FzLane &z,
 }
 
 // One stream's in-order batch (IcmChain): the descriptor of packet i from
-// its header -- index e_0 + i when its sequence number is seq_0 + i and it
-// passes pre_protect's checks (srtp_host.c; srtp.c:2515-2600), else no
-// crypto and the batch is declined (*abort).  The trailer bytes the tag
-// will overwrite are saved for the decline's restore.
-template <class ARGS>
+// its header (srtp_rtp_hdr.h srtp_inorder_desc), else no crypto and the
+// batch is declined (*abort).  Protect saves the trailer bytes the tag will
+// overwrite, for the decline's restore.
+template <bool RX, class ARGS>
 DEV srtp_dev_meta_t inorder_meta(const ARGS &A, uint32_t i, uint64_t off,
                                  const srtp_dev_stream_t &S, uint32_t seq0,
                                  uint64_t e0, bool e0ok)
@@ -389,27 +388,15 @@ DEV srtp_dev_meta_t inorder_meta(const ARGS &A, uint32_t i, uint64_t off,
     const uint32_t len = Q.in_len[i], cap = Q.cap[i];
     const srtp_dev_hdr_t h = srtp_parse_rtp(A.in + off, off, len);
     srtp_dev_meta_t m;
-    m.key = 0;
-    m.roc = 0;
-    m.len = 0;
-    m.info = 0xff0000u;   // no crypto
-    const bool ok = e0ok && (h.enc_start >> 24) == 0 && h.ssrc == S.ssrc &&
-                    (h.seq_len & 0xffffu) == ((seq0 + i) & 0xffffu) &&
-                    h.enc_start <= len && cap >= len + S.trailer &&
-                    !((S.flags & SRTP_DS_ICM_CONF) &&
-                      (len - h.enc_start + 15) / 16 > 0xffffu);
-    if (!ok) {
+    if (!srtp_inorder_desc(S, h, i, len, cap, seq0, e0, e0ok, RX, m)) {
         atomicOr(Q.abort, 1u);
         return m;
     }
-    const uint64_t e = e0 + i;
-    m.key = S.key;
-    m.roc = (uint32_t)(e >> 16);
-    m.info = h.enc_start | (S.variant << 24);
-    m.len = len;
-    u32x4 w;
-    fz_tail_save(A.out + off + len, S.trailer < 16 ? S.trailer : 16, w);
-    *(u32x4 *)Q.tsave[i] = w;
+    if constexpr (!RX) {
+        u32x4 w;
+        fz_tail_save(A.out + off + len, S.trailer < 16 ? S.trailer : 16, w);
+        *(u32x4 *)Q.tsave[i] = w;
+    }
     return m;
 }
 

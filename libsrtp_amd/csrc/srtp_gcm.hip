@@ -245,26 +245,21 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
     if constexpr (TAB4) {
         GhPos8 G;
         G.init(lds, (uint32_t)AES_TAB4_BYTES, threadIdx.x);
-        if constexpr (PROTECT) {
-            if (A.ch.st) {
-                // one stream in order (IcmChain, srtp_fused.h inorder_meta)
-                const srtp_dev_stream_t S = *A.ch.st;
-                const uint64_t o0 = A.in_off[0];
-                const uint32_t seq0 =
-                    bswap(*(const uint32_t *)(A.in + o0)) & 0xffffu;
-                uint64_t e0 = 0;
-                const bool e0ok =
-                    (S.flags & SRTP_DS_ELIGIBLE) && !(S.dir & SRTP_DIR_RX) &&
-                    srtp_guess_index(S.index, seq0, &e0) >= 1;
-                for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-                     i < A.n; i += stride) {
-                    const uint64_t off = A.in_off[i];
-                    gcm_packet<NR, PROTECT, UNIFORM, true>(
-                        A, inorder_meta(A, i, off, S, seq0, e0, e0ok), off,
-                        off, i, T, G, rk);
-                }
-                return;
+        if (A.ch.st) {
+            // one stream in order (IcmChain, srtp_fused.h inorder_meta)
+            const srtp_dev_stream_t S = *A.ch.st;
+            uint32_t seq0;
+            uint64_t e0;
+            const bool e0ok = srtp_inorder_head(S, A.in + A.in_off[0],
+                                                !PROTECT, seq0, e0);
+            for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+                 i += stride) {
+                const uint64_t off = A.in_off[i];
+                gcm_packet<NR, PROTECT, UNIFORM, true>(
+                    A, inorder_meta<!PROTECT>(A, i, off, S, seq0, e0, e0ok),
+                    off, off, i, T, G, rk);
             }
+            return;
         }
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
              i += stride)

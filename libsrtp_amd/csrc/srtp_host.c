@@ -3956,6 +3956,12 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->rx_mask &&
                   (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
                   fused_variant(dt->rx_mask, dt->rx_uniform);
+    /* one stream in order (srtp_prepass.hip pp_unprotect_inorder) */
+    pb.inorder_ok = b->in == b->out && b->in_off == b->out_off &&
+                    dt->rx_mask && (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
+                    ((dt->rx_mask & 0xfc00u) == dt->rx_mask ||
+                     (dt->rx_mask & 0x440000u) == dt->rx_mask) &&
+                    dt->rx_uniform != 0xffffffffu && !dt->has_mki;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (pp_run(ctx, &pb, 1, &fallback))

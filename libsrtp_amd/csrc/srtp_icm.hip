@@ -662,21 +662,18 @@ void k_icm_hmac(IcmArgs A)
             fz_flush<PROTECT>(A.fz, z);
             return;
         }
-        if constexpr (KM == KM_UNI && PROTECT && FUSED == 0) {
+        if constexpr (KM == KM_UNI && FUSED == 0) {
             if (A.ch.st) {
                 // one stream in order: packet 0 fixes seq_0 and e_0
                 const srtp_dev_stream_t S = *A.ch.st;
-                const uint64_t o0 = A.in_off[0];
-                const uint32_t seq0 =
-                    bswap(*(const uint32_t *)(A.in + o0)) & 0xffffu;
-                uint64_t e0 = 0;
-                const bool e0ok =
-                    (S.flags & SRTP_DS_ELIGIBLE) && !(S.dir & SRTP_DIR_RX) &&
-                    srtp_guess_index(S.index, seq0, &e0) >= 1;
+                uint32_t seq0;
+                uint64_t e0;
+                const bool e0ok = srtp_inorder_head(S, A.in + A.in_off[0],
+                                                    !PROTECT, seq0, e0);
                 for (uint32_t i = first; i < A.n; i += stride) {
                     const uint64_t off = A.in_off[i];
                     icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
-                        A, inorder_meta(A, i, off, S, seq0, e0, e0ok),
+                        A, inorder_meta<!PROTECT>(A, i, off, S, seq0, e0, e0ok),
                         off, off, i, A.uni, T, rk);
                 }
                 return;

@@ -163,6 +163,7 @@ struct PpState {
     // MKI streams: the key slots of their master keys (srtp_dev_stream_t
     // kbase / nkeys), the protect packets charged to each, and the batch's
     // per-packet key indices (srtp_gpu_pp_batch_t mki)
+    uint64_t *io_e0 = nullptr;   // pp_unprotect_inorder: the run's e_0
     uint32_t *mkslot = nullptr;
     unsigned long long *kuses = nullptr;
     uint32_t nmk = 0, nmk_cap = 0;
@@ -721,9 +722,9 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
     __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
     const uint32_t words = S.win_bits >> 5;
     const uint64_t old = S.index;
-    uint64_t e0 = 0;
-    srtp_guess_index(old, srtp_bswap32(*(const uint32_t *)(in + in_off[0])) & 0xffffu,
-                     &e0);
+    uint32_t seq0;
+    uint64_t e0;
+    srtp_inorder_head(S, in + in_off[0], false, seq0, e0);
     const uint64_t hi = e0 + n - 1;
     if (!ab) {
         const uint64_t adv = hi - old;
@@ -761,42 +762,151 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
     }
 }
 
+// The receive side of it (pp_unprotect_inorder): the crypto kernel
+// verified and decrypted every packet of the run (auth[]); a rejected
+// packet (auth_fail) changes no other packet's index -- every estimate is
+// the same from the highest ACCEPTED index before it, each advance being
+// 1 or more (rdbx.c:112-145) -- so, unless declined: the verdicts, the
+// stream at the last accepted index with the window shifted to it and the
+// accepted packets' bits set (rdbx.c:253-270, after the tag: srtp.c:
+// 3157-3167), key uses (AES-ICM / HMAC the accepted packets, AES-GCM every
+// packet: srtp_unprotect_aead counts before the tag), the failures counted
+// for the host (their decryption is undone), the verdict published.
+constexpr uint32_t IO_RX_BLOCKS = 256;
+
+__global__ __launch_bounds__(1024) void k_io_rx_commit(const uint8_t *in, const uint64_t *in_off,
+                               const uint32_t *in_len, const uint8_t *auth,
+                               uint32_t n, srtp_dev_stream_t *st,
+                               uint32_t *win, const uint32_t *abort,
+                               uint32_t *nfail, uint32_t *pub,
+                               int32_t *status, uint32_t *out_len,
+                               uint64_t *e0_run)
+{
+    const uint32_t ab = *abort;
+    srtp_dev_stream_t &S = st[0];
+    __shared__ uint32_t s_acc, s_fail;
+    if (threadIdx.x == 0)
+        s_acc = s_fail = 0;
+    __syncthreads();
+    // a grid of at most IO_RX_BLOCKS blocks: one atomic per block on the
+    // stream's counters (same-address atomics serialise in L2)
+    uint32_t acc = 0, fail = 0;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n && !ab;
+         i += gridDim.x * blockDim.x) {
+        if (auth[i]) {
+            status[i] = 0;
+            out_len[i] = in_len[i] - S.trailer;
+            acc++;
+        } else {
+            status[i] = 7;   // srtp_err_status_auth_fail
+            fail++;
+        }
+    }
+    if (acc)
+        atomicAdd(&s_acc, acc);
+    if (fail)
+        atomicAdd(&s_fail, fail);
+    __syncthreads();
+    if (threadIdx.x == 0 && !ab) {
+        const uint32_t used = (S.flags & SRTP_DS_AEAD) ? s_acc + s_fail : s_acc;
+        if (used)
+            atomicAdd((unsigned long long *)&S.uses, (unsigned long long)used);
+        if (s_acc)
+            atomicOr(&S.dir, (uint32_t)SRTP_DIR_RX);
+        if (s_fail)
+            atomicAdd(nfail, s_fail);
+    }
+    if (blockIdx.x != 0)
+        return;
+    __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
+    __shared__ int64_t s_last;
+    const uint32_t words = S.win_bits >> 5;
+    const uint64_t old = S.index;
+    uint32_t seq0;
+    uint64_t e0;
+    srtp_inorder_head(S, in + in_off[0], true, seq0, e0);
+    if (threadIdx.x == 0) {
+        s_last = -1;
+        *e0_run = e0;   // for the undo of the rejected packets
+    }
+    __syncthreads();
+    // the last accepted packet (usually the batch's last)
+    for (int64_t c = (int64_t)n - 1; c >= 0 && !ab; c -= blockDim.x) {
+        const int64_t j = c - (int64_t)threadIdx.x;
+        if (j >= 0 && auth[j])
+            atomicMax((long long *)&s_last, (long long)j);
+        __syncthreads();
+        if (s_last >= 0)
+            break;
+    }
+    const int64_t last = s_last;
+    if (!ab && last >= 0) {
+        const uint64_t hi = e0 + (uint64_t)last;
+        const uint64_t adv = hi - old;
+        const uint32_t *w = win + S.win_off;
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x) {
+            uint32_t v = 0;
+            if (adv < S.win_bits) {
+                const uint32_t b0 = (uint32_t)adv >> 5, bi = (uint32_t)adv & 31;
+                const uint32_t a = x + b0 < words ? w[x + b0] : 0u;
+                const uint32_t b = x + b0 + 1 < words ? w[x + b0 + 1] : 0u;
+                v = bi ? (a >> bi) | (b << (32 - bi)) : a;
+            }
+            s_win[x] = v;
+        }
+        __syncthreads();
+        // the accepted packets among the window's indices below hi
+        const uint32_t span = (uint64_t)last + 1 < S.win_bits
+                                  ? (uint32_t)last + 1 : S.win_bits;
+        for (uint32_t k = threadIdx.x; k < span; k += blockDim.x) {
+            const uint64_t j = (uint64_t)last - k;
+            if (auth[j]) {
+                const uint32_t bit = S.win_bits - 1 - k;
+                atomicOr(&s_win[bit >> 5], 1u << (bit & 31));
+            }
+        }
+        __syncthreads();
+        for (uint32_t x = threadIdx.x; x < words; x += blockDim.x)
+            win[S.win_off + x] = s_win[x];
+        __syncthreads();
+        if (threadIdx.x == 0)
+            S.index = hi;
+    }
+    if (threadIdx.x == 0 && pub)
+        __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ... declined: the descriptors of the packets the kernel encrypted (the
 // same test as inorder_meta) for the keystream undo, and their trailer
 // bytes back
 __global__ void k_io_restore_meta(const uint8_t *in, const uint64_t *in_off,
                                   const uint32_t *in_len, const uint32_t *cap,
                                   uint32_t n, const srtp_dev_stream_t *st,
-                                  srtp_dev_meta_t *meta)
+                                  const uint8_t *auth, srtp_dev_meta_t *meta,
+                                  int rx, const uint64_t *e0_run)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
     const srtp_dev_stream_t S = st[0];
-    const uint32_t seq0 = srtp_bswap32(*(const uint32_t *)(in + in_off[0])) & 0xffffu;
-    uint64_t e0 = 0;
-    const bool e0ok = (S.flags & SRTP_DS_ELIGIBLE) && !(S.dir & SRTP_DIR_RX) &&
-                      srtp_guess_index(S.index, seq0, &e0) >= 1;
+    uint32_t seq0;
+    uint64_t e0;
+    bool e0ok = srtp_inorder_head(S, in + in_off[0], rx != 0, seq0, e0);
+    if (e0_run) {
+        // a committed batch: the stream has moved on; e_0 as the kernel
+        // had it
+        e0 = *e0_run;
+        e0ok = true;
+    }
     const uint64_t off = in_off[i];
     const uint32_t len = in_len[i];
     const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, len);
     srtp_dev_meta_t m;
-    m.key = 0;
-    m.roc = 0;
-    m.len = 0;
-    m.info = 0xff0000u;
-    const bool ok = e0ok && (h.enc_start >> 24) == 0 && h.ssrc == S.ssrc &&
-                    (h.seq_len & 0xffffu) == ((seq0 + i) & 0xffffu) &&
-                    h.enc_start <= len && cap[i] >= len + S.trailer &&
-                    !((S.flags & SRTP_DS_ICM_CONF) &&
-                      (len - h.enc_start + 15) / 16 > 0xffffu);
-    if (ok) {
-        const uint64_t e = e0 + i;
-        m.key = S.key;
-        m.roc = (uint32_t)(e >> 16);
-        m.info = h.enc_start | (S.variant << 24);
-        m.len = len;
-    }
+    // (receive, accepted batch: only the packets whose tag failed)
+    if (!srtp_inorder_desc(S, h, i, len, cap[i], seq0, e0, e0ok, rx != 0, m) ||
+        (auth && auth[i]))
+        m.info = 0xff0000u;
     meta[i] = m;
 }
 
@@ -2863,7 +2973,7 @@ void srtp_gpu_pp_free(void *p)
                      P->fz_glist, P->pd_first, P->pd_min, P->pd_max,
                      P->pd_sids, P->pd_info, P->pd_efirst, P->pd_bak,
                      P->pd_bakwin, P->pd_pos, P->cl_ctl, P->mkslot,
-                     P->kuses, P->mki8 };
+                     P->kuses, P->mki8, P->io_e0 };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -3301,7 +3411,9 @@ static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
     }
     // declined: the input comes back exactly
     hipLaunchKernelGGL(k_io_restore_meta, gp, blk, 0, stream, b->in,
-                       b->in_off, b->in_len, b->out_len, N, P->st, P->meta);
+                       b->in_off, b->in_len, b->out_len, N, P->st,
+                       (const uint8_t *)nullptr, P->meta, 0,
+                       (const uint64_t *)nullptr);
     PPCHK(hipGetLastError());
     if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
         return -1;
@@ -3310,6 +3422,87 @@ static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
     PPCHK(hipGetLastError());
     PPCHK(hipStreamSynchronize(stream));
     *declined = true;
+    return 0;
+}
+
+// The receive side: one stream, in place, one uniform-key AES-ICM / GCM
+// variant, no MKI.  The crypto kernel verifies and decrypts every packet of
+// the run (its index e_0 + i, srtp_fused.h inorder_meta), k_io_rx_commit
+// takes the verdicts; the packets whose tag failed have their decryption
+// undone.  A batch that is not one run (a reordered, repeated or missing-
+// header packet, a length error) comes back exactly and *declined: the
+// chain form (k_pu_chain1) runs it.
+static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
+                                srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                                int *fallback, bool *declined)
+{
+    const uint32_t N = (uint32_t)b->n;
+    const dim3 blk(256), gp((N + 255) / 256);
+    *declined = false;
+    *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
+    PPCHK(hipMemsetAsync(P->fz_nfail, 0, 4, stream));
+    if (!P->io_e0)
+        PPCHK(hipMalloc((void **)&P->io_e0, 8));
+    IcmChain Q;
+    Q.in_len = b->in_len;
+    Q.cap = b->out_len;
+    Q.st = P->st;
+    Q.abort = P->abort;
+    Q.tsave = nullptr;
+    srtp_gpu_batch_t cb = {};
+    cb.n = b->n;
+    cb.in = b->in;
+    cb.in_off = b->in_off;
+    cb.out = b->out;
+    cb.out_off = b->out_off;
+    cb.meta = P->meta;   // not read
+    cb.auth_ok = P->auth;
+    cb.uniform_key = b->uniform_key;
+    cb.mask = b->mask;
+    cb.stream = stream;
+    cb.abort = nullptr;
+    cb.inorder = &Q;
+    if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "in-order rx crypto"))
+        return -1;
+    const uint32_t rxb = (N + 1023) / 1024 < IO_RX_BLOCKS ? (N + 1023) / 1024
+                                                         : IO_RX_BLOCKS;
+    hipLaunchKernelGGL(k_io_rx_commit, dim3(rxb), dim3(1024), 0, stream, b->in,
+                       b->in_off,
+                       b->in_len, P->auth, N, P->st, P->win, P->abort,
+                       P->fz_nfail, P->h_abort_dev, b->status, b->out_len,
+                       P->io_e0);
+    PPCHK(hipGetLastError());
+    if (pp_step(stream, "in-order rx commit"))
+        return -1;
+    uint32_t nfail = 0;
+    PPCHK(hipMemcpyAsync(&nfail, P->fz_nfail, 4, hipMemcpyDeviceToHost,
+                         stream));
+    PPCHK(hipStreamSynchronize(stream));
+    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    const bool ab = *(volatile uint32_t *)P->h_abort != 0;
+    if (!ab && !nfail) {
+        b->sorted = 1;
+        *fallback = 0;
+        return 0;
+    }
+    // the decryption of every packet that ran (declined) or of the ones
+    // whose tag failed (accepted batch) is undone
+    hipLaunchKernelGGL(k_io_restore_meta, gp, blk, 0, stream, b->in,
+                       b->in_off, b->in_len, b->out_len, N, P->st,
+                       ab ? (const uint8_t *)nullptr : (const uint8_t *)P->auth,
+                       P->meta, 1, ab ? (const uint64_t *)nullptr : P->io_e0);
+    PPCHK(hipGetLastError());
+    if (srtp_gpu_undo(g, b->n, b->out, b->out_off, P->meta, stream))
+        return -1;
+    PPCHK(hipStreamSynchronize(stream));
+    if (ab) {
+        *declined = true;
+        return 0;
+    }
+    b->sorted = 1;
+    *fallback = 0;
     return 0;
 }
 
@@ -3993,8 +4186,18 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     }();
     // one stream: the fused chain form, in order or not (k_pu_chain1);
     // several: order-free first, then the sorted chain form
-    if (ns == 1 && fused_on())
+    if (ns == 1 && fused_on()) {
+        // (a pending ROC applied to this batch needs k_pend_authchk: the
+        // chain form)
+        if (b->inorder_ok && inorder_on() && !P->pd_nres) {
+            bool declined = false;
+            if (pp_unprotect_inorder(g, P, b, stream, fallback, &declined))
+                return -1;
+            if (!declined)
+                return 0;
+        }
         return pp_unprotect_chain1(g, P, b, stream, fallback);
+    }
     bool unordered = ns > 1 && !force_sorted;
     if (unordered && b->fused_ok && fused_of_on() &&
         !(b->uniform_key == 0xffffffffu && buckets_on())) {

@@ -121,4 +121,58 @@ __device__ __forceinline__ int64_t srtp_guess_index(uint64_t idx, uint32_t seq,
     return (int64_t)seq - (int64_t)idx;
 }
 
+// One stream's in-order batch (srtp_prepass.hip pp_protect_inorder /
+// pp_unprotect_inorder): packet i belongs to the run when its header parses
+// with the stream's SSRC, its sequence number is seq_0 + i and the checks
+// of the host pre-pass pass (protect: srtp_host.c pre_protect, srtp.c:
+// 2515-2600; unprotect: un_static, srtp.c:2905-2990); its index is then
+// e_0 + i.  Returns false (no descriptor) otherwise: the batch is declined.
+__device__ __forceinline__ bool srtp_inorder_desc(
+    const srtp_dev_stream_t &S, const srtp_dev_hdr_t &h, uint32_t i,
+    uint32_t len, uint32_t cap, uint32_t seq0, uint64_t e0, bool e0ok,
+    bool rx, srtp_dev_meta_t &m)
+{
+    m.key = 0;
+    m.roc = 0;
+    m.len = 0;
+    m.info = 0xff0000u;   // no crypto
+    if (!e0ok || (h.enc_start >> 24) != 0 || h.ssrc != S.ssrc ||
+        (h.seq_len & 0xffffu) != ((seq0 + i) & 0xffffu))
+        return false;
+    const uint32_t es = h.enc_start, tag = S.trailer;
+    uint32_t plen = len;   // the authenticated / encrypted region's end
+    if (rx) {
+        if (S.mki || len < tag || es > len - tag ||
+            ((S.flags & SRTP_DS_AEAD) && len - es < tag) || cap < len - tag)
+            return false;
+        plen = len - tag;
+    } else if (es > len || cap < len + tag) {
+        return false;
+    }
+    if ((S.flags & SRTP_DS_ICM_CONF) && (plen - es + 15) / 16 > 0xffffu)
+        return false;
+    const uint64_t e = e0 + i;
+    m.key = S.key;
+    m.roc = (uint32_t)(e >> 16);
+    m.info = es | (S.variant << 24);
+    m.len = plen;
+    return true;
+}
+
+// ... and its packet 0: seq_0, e_0 (the stored index's guess; the run must
+// lie above it) and whether the stream may run this direction
+__device__ __forceinline__ bool srtp_inorder_head(const srtp_dev_stream_t &S,
+                                                  const uint8_t *pkt0, bool rx,
+                                                  uint32_t &seq0,
+                                                  uint64_t &e0)
+{
+    seq0 = srtp_bswap32(*(const uint32_t *)pkt0) & 0xffffu;
+    e0 = 0;
+    const bool dir = rx ? ((S.flags & SRTP_DS_RX_ELIGIBLE) &&
+                           !(S.dir & SRTP_DIR_TX))
+                        : ((S.flags & SRTP_DS_ELIGIBLE) &&
+                           !(S.dir & SRTP_DIR_RX));
+    return srtp_guess_index(S.index, seq0, &e0) >= 1 && dir;
+}
+
 #endif

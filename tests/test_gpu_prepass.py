@@ -14,7 +14,7 @@ import pytest
 
 import libsrtp_amd as L
 from oracle import pyoracle as O
-from tests.test_gpu_parity import _gpu, policy, rtp_packet
+from tests.test_gpu_parity import POLICIES, _gpu, policy, rtp_packet
 
 pytestmark = pytest.mark.gpu
 
@@ -1560,3 +1560,113 @@ def test_one_stream_in_order_form(name):
     caps = [len(p) + 32 for p in pk]
     st, before, after, offs = _arena_run(lib, pk, caps, 24, rng)
     _check_arena(orc, pk, caps, st, before, after, offs)
+
+
+def _arena_run_rx(sess, pkts, caps, slot_extra, rng):
+    """srtp_unprotect_device in place over an arena with random bytes
+    around the packets"""
+    import torch
+    offs, pos = [], 0
+    for p, c in zip(pkts, caps):
+        offs.append(pos)
+        pos += (max(len(p), c) + slot_extra + 15) & ~15
+    before = bytearray(rng.randbytes(pos + 16))
+    for o, p in zip(offs, pkts):
+        before[o:o + len(p)] = p
+    arena = torch.frombuffer(bytearray(before), dtype=torch.uint8).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor([len(p) for p in pkts], dtype=torch.int32).cuda()
+    cap = torch.tensor(caps, dtype=torch.int32).cuda()
+    st = torch.full((len(pkts),), -1, dtype=torch.int32).cuda()
+    assert sess.unprotect_device(arena, off, ln, arena, off, cap, st) == 0
+    return st.cpu().tolist(), bytes(before), arena.cpu().numpy().tobytes(), offs
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
+                                  "icm128_nullauth", "gcm256_16", "gcm256_8"])
+def test_one_stream_in_order_receive(name):
+    """the receive side of the in-order form: runs of consecutive packets
+    (across a ROC wrap) with forged tags among them -- rejected, their
+    decryption undone, the others accepted at the same indices -- and runs
+    with a swapped pair, a repeated packet or a too-short packet (declined,
+    restored, the chain form decides); every status and every arena byte
+    against the oracle's srtp_unprotect per packet, then the window through
+    replayed packets"""
+    _gpu()
+    rng = random.Random(733)
+    ssrc = 0x29100000
+    pols = [policy(name, ssrc=ssrc, seed=3)]
+    snd = O.Session(pols)
+    lib, orc = L.Session(pols), O.Session(pols)
+    tag = POLICIES[name][4]
+    seq = 0xffff - 2500
+    sent_all = []
+
+    def run(n):
+        nonlocal seq
+        out = []
+        for k in range(n):
+            p = rtp_packet(rng, ssrc, seq & 0xffff,
+                           rng.choice((0, 7, 160, 1000)),
+                           cc=rng.choice((0, 0, 2)),
+                           xwords=rng.choice((-1, -1, 2)))
+            seq += 1
+            rc, ref = snd.protect(p, len(p) + 64)
+            assert rc == 0
+            out.append(ref)
+        sent_all.extend(out)
+        return out
+
+    def forge(pk):
+        if tag == 0:
+            return
+        for k in rng.sample(range(len(pk)), 25) + [len(pk) - 1]:
+            b = bytearray(pk[k])
+            b[-1] ^= 0x40
+            pk[k] = bytes(b)
+
+    def swap(pk):
+        pk[500], pk[501] = pk[501], pk[500]
+
+    def repeat(pk):
+        pk[800] = pk[799]
+
+    def short(pk):
+        pk[321] = pk[321][:8]
+
+    warm = run(8)   # the stream's first packets (host path: fresh index)
+    st, before, after, offs = _arena_run_rx(lib, warm, [len(p) for p in warm],
+                                            24, rng)
+    _check_rx_arena(orc, warm, st, before, after, offs)
+    plan = [None, forge, swap, repeat, short, forge, None]
+    for b, tw in enumerate(plan):
+        pk = run(2000)
+        if tw:
+            tw(pk)
+        caps = [len(p) for p in pk]
+        st, before, after, offs = _arena_run_rx(lib, pk, caps, 24, rng)
+        _check_rx_arena(orc, pk, st, before, after, offs,
+                        "batch %d %s" % (b, tw.__name__ if tw else "clean"))
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    # the window: recent packets again (replay_fail) and older ones
+    # (replay_old), then a new one
+    pk = sent_all[-30:] + sent_all[-3000:-2990]
+    pk += run(1)
+    st, before, after, offs = _arena_run_rx(lib, pk, [len(p) for p in pk], 24,
+                                            rng)
+    _check_rx_arena(orc, pk, st, before, after, offs)
+
+
+def _check_rx_arena(orc, pkts, st, before, after, offs, what=""):
+    expect = bytearray(before)
+    for i, p in enumerate(pkts):
+        rc, ref = orc.unprotect(p, len(p))
+        assert st[i] == rc, (what, i, st[i], rc)
+        if rc == 0:
+            expect[offs[i]:offs[i] + len(ref)] = ref
+    if bytes(expect) != after:
+        bad = next(k for k in range(len(after)) if after[k] != expect[k])
+        i = max(k for k in range(len(offs)) if offs[k] <= bad)
+        raise AssertionError("%s: arena byte %d differs: packet %d (len %d, "
+                             "status %d) byte %d" % (what, bad, i, len(pkts[i]),
+                                                     st[i], bad - offs[i]))
