@@ -202,6 +202,15 @@ __device__ __forceinline__ void publish_abort(uint32_t *pub,
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ... and, for a receive batch, the count of failed tags beside it (pub[1]):
+// the host reads both from pinned memory after its one synchronize, no copy
+__device__ __forceinline__ void publish_nfail(uint32_t *pub, uint32_t nfail)
+{
+    if (pub)
+        __hip_atomic_store(pub + 1, nfail, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ uint32_t map_hash(uint32_t k, uint32_t mask)
 {
     // srtp_host.c map_hash
@@ -780,7 +789,7 @@ __global__ __launch_bounds__(1024) void k_io_rx_commit(const uint8_t *in, const 
                                uint32_t *win, const uint32_t *abort,
                                uint32_t *nfail, uint32_t *pub,
                                int32_t *status, uint32_t *out_len,
-                               uint64_t *e0_run)
+                               uint64_t *e0_run, uint32_t *ticket)
 {
     const uint32_t ab = *abort;
     srtp_dev_stream_t &S = st[0];
@@ -816,8 +825,26 @@ __global__ __launch_bounds__(1024) void k_io_rx_commit(const uint8_t *in, const 
         if (s_fail)
             atomicAdd(nfail, s_fail);
     }
-    if (blockIdx.x != 0)
+    // the last block to finish publishes the abort word and the failed-tag
+    // count to pinned host memory (the host needs no copy after its sync)
+    auto finish = [&]() {
+        if (threadIdx.x != 0)
+            return;
+        __threadfence();
+        if (atomicAdd(ticket, 1u) != gridDim.x - 1)
+            return;
+        __threadfence();
+        *ticket = 0;
+        publish_nfail(pub, __hip_atomic_load(nfail, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+        if (pub)
+            __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    };
+    if (blockIdx.x != 0) {
+        finish();
         return;
+    }
     __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
     __shared__ int64_t s_last;
     const uint32_t words = S.win_bits >> 5;
@@ -872,9 +899,8 @@ __global__ __launch_bounds__(1024) void k_io_rx_commit(const uint8_t *in, const 
         if (threadIdx.x == 0)
             S.index = hi;
     }
-    if (threadIdx.x == 0 && pub)
-        __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    finish();
 }
 
 // ... declined: the descriptors of the packets the kernel encrypted (the
@@ -1358,9 +1384,12 @@ __global__ void k_fzu_commit(srtp_dev_stream_t *st, uint32_t ns,
                              const unsigned long long *cnt,
                              const unsigned long long *new_index,
                              const uint32_t *wnew, uint32_t *win,
-                             const uint32_t *abort, uint32_t *pub)
+                             const uint32_t *abort, uint32_t *pub,
+                             const uint32_t *nfail)
 {
     publish_abort(pub, abort);
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        publish_nfail(pub, *nfail);   // final: the crypto kernel has ended
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (*abort || s >= ns)
         return;
@@ -3029,7 +3058,7 @@ int srtp_gpu_pp_upload(srtp_gpu_t *g, const srtp_dev_stream_t *streams,
         memset(h, 0, sizeof h);
         h[0].umin = h[1].umin = ~0ull;
         PPCHK(hipMemcpy(P->pu_ctl, h, sizeof h, hipMemcpyHostToDevice));
-        PPCHK(hipHostMalloc((void **)&P->h_abort, 4,
+        PPCHK(hipHostMalloc((void **)&P->h_abort, 8,
                             hipHostMallocMapped | hipHostMallocCoherent));
         PPCHK(hipHostGetDevicePointer((void **)&P->h_abort_dev, P->h_abort,
                                       0));
@@ -3345,6 +3374,21 @@ static bool inorder_on()
     return on;
 }
 
+// After the synchronize that ends a receive batch's commit: the abort word
+// and the failed-tag count its last kernel published to pinned memory, each
+// copied from device memory instead if the mapped store was not seen.
+static int pp_published(PpState *P, uint32_t *nfail)
+{
+    volatile uint32_t *h = (volatile uint32_t *)P->h_abort;
+    if (h[0] == ABORT_UNSET)
+        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    if (h[1] == ABORT_UNSET)
+        PPCHK(hipMemcpy(nfail, P->fz_nfail, 4, hipMemcpyDeviceToHost));
+    else
+        *nfail = h[1];
+    return 0;
+}
+
 // An error after k_pp_chain1 was queued: only k_pp_chain1_commit zeroes the
 // look-back words, the tile ticket / key-use counters and the next batch's
 // abort word, so they are zeroed here (else the next one-stream batch would
@@ -3440,10 +3484,16 @@ static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
     const dim3 blk(256), gp((N + 255) / 256);
     *declined = false;
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    ((volatile uint32_t *)P->h_abort)[1] = ABORT_UNSET;
     PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
     PPCHK(hipMemsetAsync(P->fz_nfail, 0, 4, stream));
     if (!P->io_e0)
-        PPCHK(hipMalloc((void **)&P->io_e0, 8));
+    {
+        // [0] the run's e_0, [1] k_io_rx_commit's block ticket (zero
+        // between launches: its last block resets it)
+        PPCHK(hipMalloc((void **)&P->io_e0, 16));
+        PPCHK(hipMemsetAsync(P->io_e0, 0, 16, stream));
+    }
     IcmChain Q;
     Q.in_len = b->in_len;
     Q.cap = b->out_len;
@@ -3471,16 +3521,14 @@ static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
                        b->in_off,
                        b->in_len, P->auth, N, P->st, P->win, P->abort,
                        P->fz_nfail, P->h_abort_dev, b->status, b->out_len,
-                       P->io_e0);
+                       P->io_e0, (uint32_t *)(P->io_e0 + 1));
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order rx commit"))
         return -1;
-    uint32_t nfail = 0;
-    PPCHK(hipMemcpyAsync(&nfail, P->fz_nfail, 4, hipMemcpyDeviceToHost,
-                         stream));
     PPCHK(hipStreamSynchronize(stream));
-    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
-        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    uint32_t nfail = 0;
+    if (pp_published(P, &nfail))
+        return -1;
     const bool ab = *(volatile uint32_t *)P->h_abort != 0;
     if (!ab && !nfail) {
         b->sorted = 1;
@@ -3653,6 +3701,7 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
     *sorted = false;
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    ((volatile uint32_t *)P->h_abort)[1] = ABORT_UNSET;
     unsigned long long *hi = (unsigned long long *)P->new_index;
     hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
                        P->abort, P->fz_cnt, hi, P->fz_emin, nullptr, nullptr,
@@ -4080,6 +4129,7 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
     const dim3 blk(256), gp((N + 255) / 256), gs((ns + 255) / 256);
     *sorted = false;
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
+    ((volatile uint32_t *)P->h_abort)[1] = ABORT_UNSET;
     unsigned long long *hi = (unsigned long long *)P->new_index;
     hipLaunchKernelGGL(k_fz_reset, dim3(ns / 256 + 1), blk, 0, stream,
                        P->abort, P->fz_cnt, hi, P->fz_emin, P->fz_hicand,
@@ -4130,16 +4180,15 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
                        hi, P->fz_hicand, P->fz_emin, P->fz_bmap, F.bmap2,
                        P->win, P->wnew, P->abort);
     hipLaunchKernelGGL(k_fzu_commit, gs, blk, 0, stream, P->st, ns, P->fz_cnt,
-                       hi, P->wnew, P->win, P->abort, P->h_abort_dev);
+                       hi, P->wnew, P->win, P->abort, P->h_abort_dev,
+                       P->fz_nfail);
     if (hipGetLastError() != hipSuccess ||
         pp_step(stream, "fused unprotect commit"))
         return fail();
-    uint32_t nfail = 0;
-    PPCHK(hipMemcpyAsync(&nfail, P->fz_nfail, 4, hipMemcpyDeviceToHost,
-                         stream));
     PPCHK(hipStreamSynchronize(stream));
-    if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
-        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+    uint32_t nfail = 0;
+    if (pp_published(P, &nfail))
+        return -1;
     const uint32_t ab = *(volatile uint32_t *)P->h_abort;
     *fallback = (int)ab;
     if (!ab && !nfail)
