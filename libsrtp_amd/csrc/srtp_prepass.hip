@@ -781,86 +781,80 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
 // 3157-3167), key uses (AES-ICM / HMAC the accepted packets, AES-GCM every
 // packet: srtp_unprotect_aead counts before the tag), the failures counted
 // for the host (their decryption is undone), the verdict published.
-constexpr uint32_t IO_RX_BLOCKS = 256;
+// Two launches: k_io_rx_status (one thread per packet: verdict, length,
+// each block's failure count -- no atomics, so a forged-heavy batch costs
+// no same-address serialisation) and k_io_rx_commit (one block: the sum,
+// the key uses, the window, the index, the publication).
+__global__ __launch_bounds__(256) void k_io_rx_status(
+    const uint32_t *in_len, const uint8_t *auth, uint32_t n,
+    const srtp_dev_stream_t *st, const uint32_t *abort, uint32_t *bfail,
+    int32_t *status, uint32_t *out_len)
+{
+    if (*abort)   // grid-uniform
+        return;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool f = false;
+    if (i < n) {
+        if (auth[i]) {
+            status[i] = 0;
+            out_len[i] = in_len[i] - st[0].trailer;
+        } else {
+            status[i] = 7;   // srtp_err_status_auth_fail
+            f = true;
+        }
+    }
+    __shared__ uint32_t s_f[4];
+    const uint64_t m = __ballot(f);
+    if ((threadIdx.x & 63) == 0)
+        s_f[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        bfail[blockIdx.x] = s_f[0] + s_f[1] + s_f[2] + s_f[3];
+}
 
-__global__ __launch_bounds__(1024) void k_io_rx_commit(const uint8_t *in, const uint64_t *in_off,
-                               const uint32_t *in_len, const uint8_t *auth,
-                               uint32_t n, srtp_dev_stream_t *st,
-                               uint32_t *win, const uint32_t *abort,
-                               uint32_t *nfail, uint32_t *pub,
-                               int32_t *status, uint32_t *out_len,
-                               uint64_t *e0_run, uint32_t *ticket)
+__global__ __launch_bounds__(1024) void k_io_rx_commit(
+    const uint8_t *in, const uint64_t *in_off, const uint8_t *auth, uint32_t n,
+    uint32_t nblk, srtp_dev_stream_t *st, uint32_t *win,
+    const uint32_t *abort, const uint32_t *bfail, uint32_t *nfail,
+    uint32_t *pub, uint64_t *e0_run)
 {
     const uint32_t ab = *abort;
     srtp_dev_stream_t &S = st[0];
-    __shared__ uint32_t s_acc, s_fail;
-    if (threadIdx.x == 0)
-        s_acc = s_fail = 0;
-    __syncthreads();
-    // a grid of at most IO_RX_BLOCKS blocks: one atomic per block on the
-    // stream's counters (same-address atomics serialise in L2)
-    uint32_t acc = 0, fail = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n && !ab;
-         i += gridDim.x * blockDim.x) {
-        if (auth[i]) {
-            status[i] = 0;
-            out_len[i] = in_len[i] - S.trailer;
-            acc++;
-        } else {
-            status[i] = 7;   // srtp_err_status_auth_fail
-            fail++;
-        }
-    }
-    if (acc)
-        atomicAdd(&s_acc, acc);
-    if (fail)
-        atomicAdd(&s_fail, fail);
-    __syncthreads();
-    if (threadIdx.x == 0 && !ab) {
-        const uint32_t used = (S.flags & SRTP_DS_AEAD) ? s_acc + s_fail : s_acc;
-        if (used)
-            atomicAdd((unsigned long long *)&S.uses, (unsigned long long)used);
-        if (s_acc)
-            atomicOr(&S.dir, (uint32_t)SRTP_DIR_RX);
-        if (s_fail)
-            atomicAdd(nfail, s_fail);
-    }
-    // the last block to finish publishes the abort word and the failed-tag
-    // count to pinned host memory (the host needs no copy after its sync)
-    auto finish = [&]() {
-        if (threadIdx.x != 0)
-            return;
-        __threadfence();
-        if (atomicAdd(ticket, 1u) != gridDim.x - 1)
-            return;
-        __threadfence();
-        *ticket = 0;
-        publish_nfail(pub, __hip_atomic_load(nfail, __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT));
-        if (pub)
-            __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-    };
-    if (blockIdx.x != 0) {
-        finish();
-        return;
-    }
+    __shared__ uint32_t s_fail;
     __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
     __shared__ int64_t s_last;
+    if (threadIdx.x == 0) {
+        s_fail = 0;
+        s_last = -1;
+    }
+    __syncthreads();
+    uint32_t f = 0;
+    for (uint32_t x = threadIdx.x; x < nblk && !ab; x += blockDim.x)
+        f += bfail[x];
+    if (f)
+        atomicAdd(&s_fail, f);
+    __syncthreads();
+    const uint32_t nf = s_fail;
+    if (threadIdx.x == 0 && !ab) {
+        // key uses: AES-GCM every packet (srtp_unprotect_aead counts before
+        // the tag), AES-ICM / HMAC the accepted ones
+        S.uses += (S.flags & SRTP_DS_AEAD) ? n : n - nf;
+        if (nf < n)
+            S.dir |= SRTP_DIR_RX;
+    }
     const uint32_t words = S.win_bits >> 5;
     const uint64_t old = S.index;
     uint32_t seq0;
     uint64_t e0;
     srtp_inorder_head(S, in + in_off[0], true, seq0, e0);
-    if (threadIdx.x == 0) {
-        s_last = -1;
+    if (threadIdx.x == 0)
         *e0_run = e0;   // for the undo of the rejected packets
-    }
-    __syncthreads();
     // the last accepted packet (usually the batch's last)
     for (int64_t c = (int64_t)n - 1; c >= 0 && !ab; c -= blockDim.x) {
         const int64_t j = c - (int64_t)threadIdx.x;
-        if (j >= 0 && auth[j])
+        // j falls with the lane: the wave's highest is its lowest set lane
+        const uint64_t m = __ballot(j >= 0 && auth[j]);
+        if (m && (threadIdx.x & 63) == (uint32_t)__ffsll((long long)m) - 1)
             atomicMax((long long *)&s_last, (long long)j);
         __syncthreads();
         if (s_last >= 0)
@@ -900,7 +894,13 @@ __global__ __launch_bounds__(1024) void k_io_rx_commit(const uint8_t *in, const 
             S.index = hi;
     }
     __syncthreads();
-    finish();
+    if (threadIdx.x == 0) {
+        *nfail = nf;
+        publish_nfail(pub, nf);
+        if (pub)
+            __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ... declined: the descriptors of the packets the kernel encrypted (the
@@ -3486,14 +3486,8 @@ static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
     ((volatile uint32_t *)P->h_abort)[1] = ABORT_UNSET;
     PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
-    PPCHK(hipMemsetAsync(P->fz_nfail, 0, 4, stream));
     if (!P->io_e0)
-    {
-        // [0] the run's e_0, [1] k_io_rx_commit's block ticket (zero
-        // between launches: its last block resets it)
-        PPCHK(hipMalloc((void **)&P->io_e0, 16));
-        PPCHK(hipMemsetAsync(P->io_e0, 0, 16, stream));
-    }
+        PPCHK(hipMalloc((void **)&P->io_e0, 8));
     IcmChain Q;
     Q.in_len = b->in_len;
     Q.cap = b->out_len;
@@ -3515,13 +3509,14 @@ static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
     cb.inorder = &Q;
     if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "in-order rx crypto"))
         return -1;
-    const uint32_t rxb = (N + 1023) / 1024 < IO_RX_BLOCKS ? (N + 1023) / 1024
-                                                         : IO_RX_BLOCKS;
-    hipLaunchKernelGGL(k_io_rx_commit, dim3(rxb), dim3(1024), 0, stream, b->in,
-                       b->in_off,
-                       b->in_len, P->auth, N, P->st, P->win, P->abort,
-                       P->fz_nfail, P->h_abort_dev, b->status, b->out_len,
-                       P->io_e0, (uint32_t *)(P->io_e0 + 1));
+    // the per-block failure counts in the metadata area, which the in-order
+    // form does not read (k_io_restore_meta writes it after the commit)
+    uint32_t *bfail = (uint32_t *)P->meta;
+    hipLaunchKernelGGL(k_io_rx_status, gp, blk, 0, stream, b->in_len, P->auth,
+                       N, P->st, P->abort, bfail, b->status, b->out_len);
+    hipLaunchKernelGGL(k_io_rx_commit, dim3(1), dim3(1024), 0, stream, b->in,
+                       b->in_off, P->auth, N, gp.x, P->st, P->win, P->abort,
+                       bfail, P->fz_nfail, P->h_abort_dev, P->io_e0);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order rx commit"))
         return -1;
