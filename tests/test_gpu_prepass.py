@@ -1553,6 +1553,7 @@ def test_one_stream_in_order_form(name):
     # device through the chain form
     assert (d - d0, h - h0) == (len(plan) - 1, 1), (d - d0, h - h0, where)
     assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)   # key uses (key.c:74-90)
     # the window the batches left: the last packets again (replay_fail /
     # replay_old on the sender's side) next to a new one
     pk = sent[-1][-40:] + sent[0][:3]
@@ -1589,8 +1590,10 @@ def test_one_stream_in_order_receive(name):
     (across a ROC wrap) with forged tags among them -- rejected, their
     decryption undone, the others accepted at the same indices -- and runs
     with a swapped pair, a repeated packet or a too-short packet (declined,
-    restored, the chain form decides); every status and every arena byte
-    against the oracle's srtp_unprotect per packet, then the window through
+    restored, the chain form decides), a one-packet run, a run with every
+    tag forged (the stream does not move) and one whose last 1,100 tags are
+    forged; every status and every arena byte against the oracle's
+    srtp_unprotect per packet, the key uses, then the window through
     replayed packets"""
     _gpu()
     rng = random.Random(733)
@@ -1634,13 +1637,31 @@ def test_one_stream_in_order_receive(name):
     def short(pk):
         pk[321] = pk[321][:8]
 
+    def forge_all(pk):   # nothing accepted: the stream does not move
+        if tag == 0:
+            return
+        for k in range(len(pk)):
+            b = bytearray(pk[k])
+            b[-1] ^= 0x01
+            pk[k] = bytes(b)
+
+    def forge_tail(pk):  # the last accepted packet 1,100 from the end
+        if tag == 0:
+            return
+        for k in range(len(pk) - 1100, len(pk)):
+            b = bytearray(pk[k])
+            b[-2] ^= 0x10
+            pk[k] = bytes(b)
+
     warm = run(8)   # the stream's first packets (host path: fresh index)
     st, before, after, offs = _arena_run_rx(lib, warm, [len(p) for p in warm],
                                             24, rng)
     _check_rx_arena(orc, warm, st, before, after, offs)
-    plan = [None, forge, swap, repeat, short, forge, None]
-    for b, tw in enumerate(plan):
-        pk = run(2000)
+    plan = [(2000, None), (2000, forge), (2000, swap), (2000, repeat),
+            (2000, short), (2000, forge), (2000, None), (1, None),
+            (300, forge_all), (2000, forge_tail), (2000, None)]
+    for b, (n, tw) in enumerate(plan):
+        pk = run(n)
         if tw:
             tw(pk)
         caps = [len(p) for p in pk]
@@ -1648,6 +1669,7 @@ def test_one_stream_in_order_receive(name):
         _check_rx_arena(orc, pk, st, before, after, offs,
                         "batch %d %s" % (b, tw.__name__ if tw else "clean"))
     assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)   # key uses (key.c:74-90)
     # the window: recent packets again (replay_fail) and older ones
     # (replay_old), then a new one
     pk = sent_all[-30:] + sent_all[-3000:-2990]
@@ -1655,6 +1677,7 @@ def test_one_stream_in_order_receive(name):
     st, before, after, offs = _arena_run_rx(lib, pk, [len(p) for p in pk], 24,
                                             rng)
     _check_rx_arena(orc, pk, st, before, after, offs)
+    _key_left_equal(lib, orc, [ssrc], 1)
 
 
 def _check_rx_arena(orc, pkts, st, before, after, offs, what=""):
