@@ -1514,10 +1514,12 @@ int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b)
     if (g->timing)
         HIPCHK(hipEventRecord(g->ev0, st));
     int rc = op == 0 ? run_dir<true>(g, b, st) : run_dir<false>(g, b, st);
+    // the elapsed time is read when asked for (srtp_gpu_last_kernel_ms,
+    // after the batch): waiting for ev1 here would hold back the launches
+    // that follow the crypto kernel by a host round trip
     if (g->timing) {
         HIPCHK(hipEventRecord(g->ev1, st));
-        HIPCHK(hipEventSynchronize(g->ev1));
-        HIPCHK(hipEventElapsedTime(&g->last_ms, g->ev0, g->ev1));
+        g->ms_pending = 1;
     }
     return rc;
 }
@@ -1681,7 +1683,16 @@ int srtp_gpu_mark_wait(srtp_gpu_t *g, int slot)
     return 0;
 }
 
-double srtp_gpu_last_kernel_ms(srtp_gpu_t *g) { return g->last_ms; }
+double srtp_gpu_last_kernel_ms(srtp_gpu_t *g)
+{
+    if (g->ms_pending) {
+        g->ms_pending = 0;
+        if (hipEventSynchronize(g->ev1) != hipSuccess ||
+            hipEventElapsedTime(&g->last_ms, g->ev0, g->ev1) != hipSuccess)
+            g->last_ms = 0;
+    }
+    return g->last_ms;
+}
 void srtp_gpu_set_timing(srtp_gpu_t *g, int on) { g->timing = on; }
 
 

@@ -23,6 +23,7 @@ struct srtp_gpu {
     uint32_t ghash_cap;
     hipEvent_t ev0, ev1;
     int timing;
+    int ms_pending;   // ev0 / ev1 recorded, last_ms not read yet
     float last_ms;
     void *pp;         // device pre-pass state (srtp_prepass.hip)
     int ncu;          // compute units (persistent grids)
