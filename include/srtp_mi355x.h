@@ -409,7 +409,9 @@ srtp_err_status_t srtp_mi355x_session_broadcast(srtp_t *session,
                                                 void *stream);
 
 /* Instrumentation for bench.py: device time (ms) of the crypto kernels of
- * the last batch, measured with HIP events on the stream they ran on. */
+ * the last batch, measured with HIP events on the stream they ran on.  The
+ * events are read once the batch has completed: timing adds no wait inside
+ * a batch (an asynchronous batch's time is read when it is asked for). */
 void srtp_mi355x_set_timing(srtp_t ctx, int on);
 double srtp_mi355x_last_kernel_ms(srtp_t ctx);
 /* device-API batches completed by the GPU pre-pass / by the host pre-pass
