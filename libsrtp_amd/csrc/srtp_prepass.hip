@@ -716,8 +716,8 @@ __global__ void k_pp_commit_stream(srtp_dev_stream_t *st, uint32_t ns,
 __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
                             const uint32_t *in_len, uint32_t n,
                             srtp_dev_stream_t *st, uint32_t *win,
-                            const uint32_t *abort, uint32_t *pub,
-                            int32_t *status, uint32_t *out_len)
+                            const uint32_t *abort, uint32_t *abort_next,
+                            uint32_t *pub, int32_t *status, uint32_t *out_len)
 {
     const uint32_t ab = *abort;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -768,6 +768,7 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
         if (pub)
             __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+        *abort_next = 0;   // the next batch's word (ch_abort pair)
     }
 }
 
@@ -815,8 +816,8 @@ __global__ __launch_bounds__(256) void k_io_rx_status(
 __global__ __launch_bounds__(1024) void k_io_rx_commit(
     const uint8_t *in, const uint64_t *in_off, const uint8_t *auth, uint32_t n,
     uint32_t nblk, srtp_dev_stream_t *st, uint32_t *win,
-    const uint32_t *abort, const uint32_t *bfail, uint32_t *nfail,
-    uint32_t *pub, uint64_t *e0_run)
+    const uint32_t *abort, uint32_t *abort_next, const uint32_t *bfail,
+    uint32_t *nfail, uint32_t *pub, uint64_t *e0_run)
 {
     const uint32_t ab = *abort;
     srtp_dev_stream_t &S = st[0];
@@ -900,6 +901,7 @@ __global__ __launch_bounds__(1024) void k_io_rx_commit(
         if (pub)
             __hip_atomic_store(pub, ab, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
+        *abort_next = 0;   // the next batch's word (ch_abort pair)
     }
 }
 
@@ -3377,11 +3379,11 @@ static bool inorder_on()
 // After the synchronize that ends a receive batch's commit: the abort word
 // and the failed-tag count its last kernel published to pinned memory, each
 // copied from device memory instead if the mapped store was not seen.
-static int pp_published(PpState *P, uint32_t *nfail)
+static int pp_published(PpState *P, const uint32_t *abort, uint32_t *nfail)
 {
     volatile uint32_t *h = (volatile uint32_t *)P->h_abort;
     if (h[0] == ABORT_UNSET)
-        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+        PPCHK(hipMemcpy(P->h_abort, abort, 4, hipMemcpyDeviceToHost));
     if (h[1] == ABORT_UNSET)
         PPCHK(hipMemcpy(nfail, P->fz_nfail, 4, hipMemcpyDeviceToHost));
     else
@@ -3409,20 +3411,25 @@ static int chain1_fail(PpState *P, hipStream_t stream)
 // packet's index from packet 0's (IcmChain) -- then k_io_commit.  A batch
 // that is not a run of consecutive sequence numbers (or has a packet with
 // a length / parse error) is restored and *declined: the chain form runs.
-static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
-                              srtp_gpu_pp_batch_t *b, hipStream_t stream,
-                              int *fallback, bool *declined)
+// The abort word is the chain form's pair (ch_abort[ch_par], zero at every
+// batch's start: each batch's last kernel clears the other word, and
+// chain1_fail both after an error), so no memset is queued per batch.
+static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
+                                  srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                                  int *fallback, bool *declined)
 {
     const uint32_t N = (uint32_t)b->n;
     const dim3 blk(256), gp((N + 255) / 256);
     *declined = false;
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
-    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
+    uint32_t *ab = P->ch_abort + P->ch_par;
+    uint32_t *ab_next = P->ch_abort + (P->ch_par ^ 1);
+    P->ch_par ^= 1;
     IcmChain Q;
     Q.in_len = b->in_len;
     Q.cap = b->out_len;
     Q.st = P->st;
-    Q.abort = P->abort;
+    Q.abort = ab;
     Q.tsave = P->tsave;
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
@@ -3440,14 +3447,14 @@ static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
     if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "in-order crypto"))
         return -1;
     hipLaunchKernelGGL(k_io_commit, gp, blk, 0, stream, b->in, b->in_off,
-                       b->in_len, N, P->st, P->win, P->abort, P->h_abort_dev,
-                       b->status, b->out_len);
+                       b->in_len, N, P->st, P->win, ab, ab_next,
+                       P->h_abort_dev, b->status, b->out_len);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order commit"))
         return -1;
     PPCHK(hipStreamSynchronize(stream));
     if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
-        PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
+        PPCHK(hipMemcpy(P->h_abort, ab, 4, hipMemcpyDeviceToHost));
     if (*(volatile uint32_t *)P->h_abort == 0) {
         b->sorted = 1;
         *fallback = 0;
@@ -3469,6 +3476,15 @@ static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
     return 0;
 }
 
+static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
+                              srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                              int *fallback, bool *declined)
+{
+    if (pp_protect_inorder_run(g, P, b, stream, fallback, declined))
+        return chain1_fail(P, stream);
+    return 0;
+}
+
 // The receive side: one stream, in place, one uniform-key AES-ICM / GCM
 // variant, no MKI.  The crypto kernel verifies and decrypts every packet of
 // the run (its index e_0 + i, srtp_fused.h inorder_meta), k_io_rx_commit
@@ -3476,23 +3492,25 @@ static int pp_protect_inorder(srtp_gpu_t *g, PpState *P,
 // undone.  A batch that is not one run (a reordered, repeated or missing-
 // header packet, a length error) comes back exactly and *declined: the
 // chain form (k_pu_chain1) runs it.
-static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
-                                srtp_gpu_pp_batch_t *b, hipStream_t stream,
-                                int *fallback, bool *declined)
+static int pp_unprotect_inorder_run(srtp_gpu_t *g, PpState *P,
+                                    srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                                    int *fallback, bool *declined)
 {
     const uint32_t N = (uint32_t)b->n;
     const dim3 blk(256), gp((N + 255) / 256);
     *declined = false;
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
     ((volatile uint32_t *)P->h_abort)[1] = ABORT_UNSET;
-    PPCHK(hipMemsetAsync(P->abort, 0, 4, stream));
     if (!P->io_e0)
         PPCHK(hipMalloc((void **)&P->io_e0, 8));
+    uint32_t *abw = P->ch_abort + P->ch_par;   // as pp_protect_inorder
+    uint32_t *ab_next = P->ch_abort + (P->ch_par ^ 1);
+    P->ch_par ^= 1;
     IcmChain Q;
     Q.in_len = b->in_len;
     Q.cap = b->out_len;
     Q.st = P->st;
-    Q.abort = P->abort;
+    Q.abort = abw;
     Q.tsave = nullptr;
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
@@ -3513,16 +3531,16 @@ static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
     // form does not read (k_io_restore_meta writes it after the commit)
     uint32_t *bfail = (uint32_t *)P->meta;
     hipLaunchKernelGGL(k_io_rx_status, gp, blk, 0, stream, b->in_len, P->auth,
-                       N, P->st, P->abort, bfail, b->status, b->out_len);
+                       N, P->st, abw, bfail, b->status, b->out_len);
     hipLaunchKernelGGL(k_io_rx_commit, dim3(1), dim3(1024), 0, stream, b->in,
-                       b->in_off, P->auth, N, gp.x, P->st, P->win, P->abort,
-                       bfail, P->fz_nfail, P->h_abort_dev, P->io_e0);
+                       b->in_off, P->auth, N, gp.x, P->st, P->win, abw,
+                       ab_next, bfail, P->fz_nfail, P->h_abort_dev, P->io_e0);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order rx commit"))
         return -1;
     PPCHK(hipStreamSynchronize(stream));
     uint32_t nfail = 0;
-    if (pp_published(P, &nfail))
+    if (pp_published(P, abw, &nfail))
         return -1;
     const bool ab = *(volatile uint32_t *)P->h_abort != 0;
     if (!ab && !nfail) {
@@ -3546,6 +3564,15 @@ static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
     }
     b->sorted = 1;
     *fallback = 0;
+    return 0;
+}
+
+static int pp_unprotect_inorder(srtp_gpu_t *g, PpState *P,
+                                srtp_gpu_pp_batch_t *b, hipStream_t stream,
+                                int *fallback, bool *declined)
+{
+    if (pp_unprotect_inorder_run(g, P, b, stream, fallback, declined))
+        return chain1_fail(P, stream);
     return 0;
 }
 
@@ -4182,7 +4209,7 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
         return fail();
     PPCHK(hipStreamSynchronize(stream));
     uint32_t nfail = 0;
-    if (pp_published(P, &nfail))
+    if (pp_published(P, P->abort, &nfail))
         return -1;
     const uint32_t ab = *(volatile uint32_t *)P->h_abort;
     *fallback = (int)ab;
