@@ -1483,8 +1483,9 @@ def _check_arena(orc, pkts, caps, st, before, after, offs):
         raise AssertionError("arena byte %d differs" % bad)
 
 
-@pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
-                                  "icm128_nullauth", "icm128_authonly",
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm192_hmac80",
+                                  "icm256_hmac32", "icm128_nullauth",
+                                  "icm128_authonly", "gcm128_16",
                                   "gcm256_16", "gcm256_8"])
 def test_one_stream_in_order_form(name):
     """a sender's batches of consecutive sequence numbers (across a ROC
@@ -1583,8 +1584,10 @@ def _arena_run_rx(sess, pkts, caps, slot_extra, rng):
     return st.cpu().tolist(), bytes(before), arena.cpu().numpy().tobytes(), offs
 
 
-@pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
-                                  "icm128_nullauth", "gcm256_16", "gcm256_8"])
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm192_hmac80",
+                                  "icm256_hmac32", "icm128_nullauth",
+                                  "icm128_authonly", "gcm128_16",
+                                  "gcm256_16", "gcm256_8"])
 def test_one_stream_in_order_receive(name):
     """the receive side of the in-order form: runs of consecutive packets
     (across a ROC wrap) with forged tags among them -- rejected, their
