@@ -425,6 +425,10 @@ void srtp_mi355x_prepass_stats(srtp_t ctx, uint64_t *device_batches,
  * order-free form (a stream with more packets in the batch than its replay
  * window, a gap of 2^15 or more) and ran the sorted chain path */
 uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx);
+/* one-stream device batches the in-order form (indices computed inside the
+ * crypto kernel, DESIGN.md "In-order form") committed / declined (restored,
+ * then the chain form ran) since the session was created */
+void srtp_mi355x_inorder_stats(srtp_t ctx, uint64_t *runs, uint64_t *declines);
 /* why the most recent srtp_protect_device fallback left the device
  * pre-pass (0: none so far): 1 unknown SSRC (template clone), 2 stream with MKI / pending ROC
  * / receiver direction, 4 sequence number not advancing by 1..2^15-1,

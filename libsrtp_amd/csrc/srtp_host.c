@@ -195,6 +195,8 @@ typedef struct {
     uint32_t rx_uniform, rx_mask; /* over the unprotect-eligible streams  */
     uint64_t fast_batches, host_batches;
     uint64_t sorted_batches; /* fast batches that needed the sorted path  */
+    uint64_t io_runs, io_declines; /* one-stream in-order form: batches it
+                                      committed / declined (chain form ran) */
     int last_abort;         /* reason of the most recent fallback         */
     int async_pending;      /* srtp_protect_device_async left its protect
                                kernel (and the tail of its commit) queued */
@@ -3331,9 +3333,11 @@ static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
         }
     }
     /* header-extension encryption / cryptex streams and routed keys: host
-     * pre-pass.  A pending ROC is resolved per batch (pend_resolve) */
+     * pre-pass.  A pending ROC is resolved per batch (pend_resolve), in
+     * either direction: a protect-eligible MKI stream with fewer keys than
+     * mki_j (receive-ineligible) still estimates from it (srtp.c:2069-2076) */
     const int xs = k->variant >= SRTP_VARIANT_X;
-    if (!templ && st->rdbx.pending_roc && mki_ok && !xs) {
+    if (!templ && st->rdbx.pending_roc && !xs) {
         d->flags |= SRTP_DS_PENDING;
         d->rsv = st->rdbx.pending_roc;
     }
@@ -3766,6 +3770,15 @@ static int fused_variant(uint32_t mask, uint32_t uniform)
     return (mask & 0x440000u) == mask && uniform == 0xffffffffu;
 }
 
+/* which way the one-stream in-order form went (srtp_mi355x_inorder_stats) */
+static void io_count(devtab_t *dt, const srtp_gpu_pp_batch_t *pb)
+{
+    if (pb->inorder == 1)
+        dt->io_runs++;
+    else if (pb->inorder == 2)
+        dt->io_declines++;
+}
+
 /* the device pre-pass; returns 1 when the batch was completed on the GPU,
  * 0 when the host path must run it, -1 on a device error */
 static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
@@ -3831,6 +3844,7 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
     free(mki8);
     if (rr)
         return -1;
+    io_count(dt, &pb);
     if (fallback) {
         dt->last_abort = fallback;
         return 0;
@@ -3966,6 +3980,7 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     if (pp_run(ctx, &pb, 1, &fallback))
         return -1;
+    io_count(dt, &pb);
     if (fallback) {
         dt->last_abort = fallback;
         return 0;
@@ -4804,6 +4819,14 @@ uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx)
     return ctx ? ctx->dt.sorted_batches : 0;
 }
 
+void srtp_mi355x_inorder_stats(srtp_t ctx, uint64_t *runs, uint64_t *declines)
+{
+    if (runs)
+        *runs = ctx ? ctx->dt.io_runs : 0;
+    if (declines)
+        *declines = ctx ? ctx->dt.io_declines : 0;
+}
+
 int srtp_mi355x_prepass_last_abort(srtp_t ctx)
 {
     return ctx ? ctx->dt.last_abort : 0;
@@ -5365,10 +5388,12 @@ out:
     if (dblob) {
         /* the device copy holds the same secrets: cleared before the free
          * (stream-ordered behind any copy still reading it) */
-        if (srtp_gpu_memset(dblob, 0, hlen, stream) ||
-            srtp_gpu_sync(NULL, stream))
-            (void)srtp_gpu_sync(NULL, NULL);
+        (void)srtp_gpu_memset(dblob, 0, hlen, stream);
     }
+    /* whatever failed above, nothing queued on the caller's stream (the
+     * broadcast, a copy, the clear) may still read the buffers freed below */
+    if ((dblob || dlen) && srtp_gpu_sync(NULL, stream))
+        (void)srtp_gpu_sync(NULL, NULL);
     srtp_gpu_free(dblob);
     srtp_gpu_free(dlen);
     return st;

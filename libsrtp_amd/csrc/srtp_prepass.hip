@@ -69,8 +69,10 @@ enum { AB_UNKNOWN_SSRC = 1, AB_INELIGIBLE = 2, AB_SEQUENCE = 4,
        AB_ORDER = 8, /* order-free form does not apply: sorted path */
        AB_STATIC = 16, /* unprotect: a packet with a length/capacity error */
        AB_MKI = 32, /* unprotect: a packet whose MKI is not the device key's */
-       AB_PENDING = 512 /* unprotect: the first packet of a stream whose
-                           pending ROC it resolved did not authenticate */ };
+       AB_PENDING = 512, /* unprotect: the first packet of a stream whose
+                            pending ROC it resolved did not authenticate */
+       AB_GAP = 2048 /* in-order unprotect: a packet 2^15 or more past the
+                        last accepted index (its estimate would differ) */ };
 
 struct PpState {
     // stream table
@@ -783,85 +785,144 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
 // packet: srtp_unprotect_aead counts before the tag), the failures counted
 // for the host (their decryption is undone), the verdict published.
 // Two launches: k_io_rx_status (one thread per packet: verdict, length,
-// each block's failure count -- no atomics, so a forged-heavy batch costs
-// no same-address serialisation) and k_io_rx_commit (one block: the sum,
-// the key uses, the window, the index, the publication).
+// each block's failure count and first / last accepted position -- no
+// atomics, so a forged-heavy batch costs no same-address serialisation) and
+// k_io_rx_commit (one block: the sums, the gap check, the key uses, the
+// window, the index, the publication).
+constexpr uint32_t IO_NONE = 0xffffffffu;   // a block with no accepted packet
+
 __global__ __launch_bounds__(256) void k_io_rx_status(
-    const uint32_t *in_len, const uint8_t *auth, uint32_t n,
-    const srtp_dev_stream_t *st, const uint32_t *abort, uint32_t *bfail,
+    const uint32_t *in_len, const uint8_t *auth, uint32_t n, uint32_t nblk,
+    const srtp_dev_stream_t *st, const uint32_t *abort, uint32_t *brec,
     int32_t *status, uint32_t *out_len)
 {
     if (*abort)   // grid-uniform
         return;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    bool f = false;
+    bool f = false, a = false;
     if (i < n) {
         if (auth[i]) {
             status[i] = 0;
             out_len[i] = in_len[i] - st[0].trailer;
+            a = true;
         } else {
             status[i] = 7;   // srtp_err_status_auth_fail
             f = true;
         }
     }
-    __shared__ uint32_t s_f[4];
-    const uint64_t m = __ballot(f);
-    if ((threadIdx.x & 63) == 0)
-        s_f[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __shared__ uint32_t s_f[4], s_lo[4], s_hi[4];
+    const uint64_t m = __ballot(f), am = __ballot(a);
+    const uint32_t w = threadIdx.x >> 6,
+                   wbase = blockIdx.x * blockDim.x + 64 * w;
+    if ((threadIdx.x & 63) == 0) {
+        s_f[w] = (uint32_t)__popcll(m);
+        s_lo[w] = am ? wbase + (uint32_t)__ffsll((long long)am) - 1 : IO_NONE;
+        s_hi[w] = am ? wbase + 63 - (uint32_t)__clzll((long long)am) : IO_NONE;
+    }
     __syncthreads();
-    if (threadIdx.x == 0)
-        bfail[blockIdx.x] = s_f[0] + s_f[1] + s_f[2] + s_f[3];
+    if (threadIdx.x == 0) {
+        uint32_t lo = IO_NONE, hi = IO_NONE;
+        for (int k = 0; k < 4; k++)
+            if (s_lo[k] != IO_NONE) {
+                if (lo == IO_NONE)
+                    lo = s_lo[k];
+                hi = s_hi[k];
+            }
+        brec[blockIdx.x] = s_f[0] + s_f[1] + s_f[2] + s_f[3];
+        brec[nblk + blockIdx.x] = lo;
+        brec[2 * nblk + blockIdx.x] = hi;
+    }
 }
 
+// brec: nblk failure counts, then nblk first and nblk last accepted
+// positions (IO_NONE: none).  Every packet's index is e_0 + i only while
+// the packet lies less than 2^15 past the last accepted one (or past the
+// stored index, position S.index - e_0 <= -1): beyond, index_guess
+// (rdbx.c:112-145) from that top returns another ROC and the reference
+// says replay_old or decrypts at another index.  So every gap between
+// consecutive accepted positions, and the tail after the last, is checked;
+// a batch with one of 2^15 or more is declined (AB_GAP) before anything is
+// committed -- the chain form decides it packet by packet (k_pu_verdict1).
 __global__ __launch_bounds__(1024) void k_io_rx_commit(
     const uint8_t *in, const uint64_t *in_off, const uint8_t *auth, uint32_t n,
-    uint32_t nblk, srtp_dev_stream_t *st, uint32_t *win,
-    const uint32_t *abort, uint32_t *abort_next, const uint32_t *bfail,
-    uint32_t *nfail, uint32_t *pub, uint64_t *e0_run)
+    uint32_t nblk, srtp_dev_stream_t *st, uint32_t *win, uint32_t *abort,
+    uint32_t *abort_next, const uint32_t *brec, uint32_t *nfail, uint32_t *pub,
+    uint64_t *e0_run)
 {
-    const uint32_t ab = *abort;
+    const uint32_t t = threadIdx.x, T = blockDim.x;
+    uint32_t ab = *abort;
     srtp_dev_stream_t &S = st[0];
     __shared__ uint32_t s_fail;
     __shared__ uint32_t s_win[SEQ_MEDIAN / 32];
-    __shared__ int64_t s_last;
-    if (threadIdx.x == 0) {
+    __shared__ int64_t s_scan[1024];
+    if (t == 0)
         s_fail = 0;
-        s_last = -1;
-    }
-    __syncthreads();
-    uint32_t f = 0;
-    for (uint32_t x = threadIdx.x; x < nblk && !ab; x += blockDim.x)
-        f += bfail[x];
-    if (f)
-        atomicAdd(&s_fail, f);
-    __syncthreads();
-    const uint32_t nf = s_fail;
-    if (threadIdx.x == 0 && !ab) {
-        // key uses: AES-GCM every packet (srtp_unprotect_aead counts before
-        // the tag), AES-ICM / HMAC the accepted ones
-        S.uses += (S.flags & SRTP_DS_AEAD) ? n : n - nf;
-        if (nf < n)
-            S.dir |= SRTP_DIR_RX;
-    }
     const uint32_t words = S.win_bits >> 5;
     const uint64_t old = S.index;
     uint32_t seq0;
     uint64_t e0;
     srtp_inorder_head(S, in + in_off[0], true, seq0, e0);
-    if (threadIdx.x == 0)
-        *e0_run = e0;   // for the undo of the rejected packets
-    // the last accepted packet (usually the batch's last)
-    for (int64_t c = (int64_t)n - 1; c >= 0 && !ab; c -= blockDim.x) {
-        const int64_t j = c - (int64_t)threadIdx.x;
-        // j falls with the lane: the wave's highest is its lowest set lane
-        const uint64_t m = __ballot(j >= 0 && auth[j]);
-        if (m && (threadIdx.x & 63) == (uint32_t)__ffsll((long long)m) - 1)
-            atomicMax((long long *)&s_last, (long long)j);
-        __syncthreads();
-        if (s_last >= 0)
-            break;
+    // the stored index as a batch position: e_0 is its guess, >= old + 1
+    const int64_t virt = (int64_t)old - (int64_t)e0;
+    constexpr int64_t NO_POS = INT64_MIN;
+    // this thread's run of block records, in batch order
+    const uint32_t per = (nblk + T - 1) / T;
+    const uint32_t r0 = t * per < nblk ? t * per : nblk;
+    const uint32_t r1 = r0 + per < nblk ? r0 + per : nblk;
+    uint32_t f = 0;
+    int64_t cfirst = NO_POS, clast = NO_POS;
+    bool gap = false;
+    for (uint32_t b = r0; b < r1 && !ab; b++) {
+        f += brec[b];
+        const uint32_t lo = brec[nblk + b];
+        if (lo == IO_NONE)
+            continue;
+        if (clast != NO_POS && (int64_t)lo - clast >= (int64_t)SEQ_MEDIAN)
+            gap = true;
+        if (cfirst == NO_POS)
+            cfirst = lo;
+        clast = brec[2 * nblk + b];
     }
-    const int64_t last = s_last;
+    __syncthreads();   // s_fail zeroed
+    if (f)
+        atomicAdd(&s_fail, f);
+    // inclusive max-scan of the runs' last accepted positions
+    s_scan[t] = clast;
+    __syncthreads();
+    for (uint32_t d = 1; d < T; d <<= 1) {
+        const int64_t v = t >= d ? s_scan[t - d] : NO_POS;
+        __syncthreads();
+        if (v > s_scan[t])
+            s_scan[t] = v;
+        __syncthreads();
+    }
+    int64_t before = t ? s_scan[t - 1] : NO_POS;
+    if (before < virt)
+        before = virt;
+    if (cfirst != NO_POS && cfirst - before >= (int64_t)SEQ_MEDIAN)
+        gap = true;
+    int64_t lastpos = s_scan[T - 1];
+    if (t == 0 && (int64_t)n - 1 - (lastpos < virt ? virt : lastpos) >=
+                      (int64_t)SEQ_MEDIAN)
+        gap = true;
+    // every thread reads the same verdict, and no shared word is written
+    // after it: a uniform decision
+    if (__syncthreads_or(gap ? 1 : 0) && !ab)
+        ab = AB_GAP;
+    const uint32_t nf = s_fail;
+    const int64_t last = lastpos;   // NO_POS: nothing accepted
+    if (t == 0) {
+        if (ab && !*abort)
+            *abort = ab;   // declined: the host restores, the chain form runs
+        *e0_run = e0;   // for the undo of the rejected packets
+        if (!ab) {
+            // key uses: AES-GCM every packet (srtp_unprotect_aead counts
+            // before the tag), AES-ICM / HMAC the accepted ones
+            S.uses += (S.flags & SRTP_DS_AEAD) ? n : n - nf;
+            if (nf < n)
+                S.dir |= SRTP_DIR_RX;
+        }
+    }
     if (!ab && last >= 0) {
         const uint64_t hi = e0 + (uint64_t)last;
         const uint64_t adv = hi - old;
@@ -3527,14 +3588,15 @@ static int pp_unprotect_inorder_run(srtp_gpu_t *g, PpState *P,
     cb.inorder = &Q;
     if (srtp_gpu_run(g, 1, &cb) || pp_step(stream, "in-order rx crypto"))
         return -1;
-    // the per-block failure counts in the metadata area, which the in-order
-    // form does not read (k_io_restore_meta writes it after the commit)
-    uint32_t *bfail = (uint32_t *)P->meta;
+    // the per-block records (failure count, first / last accepted: 3 words
+    // per 256-packet block) in the metadata area, which the in-order form
+    // does not read (k_io_restore_meta writes it after the commit)
+    uint32_t *brec = (uint32_t *)P->meta;
     hipLaunchKernelGGL(k_io_rx_status, gp, blk, 0, stream, b->in_len, P->auth,
-                       N, P->st, abw, bfail, b->status, b->out_len);
+                       N, gp.x, P->st, abw, brec, b->status, b->out_len);
     hipLaunchKernelGGL(k_io_rx_commit, dim3(1), dim3(1024), 0, stream, b->in,
                        b->in_off, P->auth, N, gp.x, P->st, P->win, abw,
-                       ab_next, bfail, P->fz_nfail, P->h_abort_dev, P->io_e0);
+                       ab_next, brec, P->fz_nfail, P->h_abort_dev, P->io_e0);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order rx commit"))
         return -1;
@@ -3824,6 +3886,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
             bool declined = false;
             if (pp_protect_inorder(g, P, b, stream, fallback, &declined))
                 return -1;
+            b->inorder = declined ? 2 : 1;
             if (!declined)
                 return 0;
         }
@@ -3941,8 +4004,10 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     mki_keys(P, b, P->abort, stream);
 
     srtp_gpu_batch_t cb = {};
+    // (not with MKI streams: k_mki_keys gave their packets a key each, and
+    // the bucketed kernel takes one key per 64-record group)
     if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&
-        bucket_pass(P, N, b, &cb, stream))
+        !b->mki && bucket_pass(P, N, b, &cb, stream))
         return -1;
     cb.n = n;
     cb.in = b->in;
@@ -4264,6 +4329,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
             bool declined = false;
             if (pp_unprotect_inorder(g, P, b, stream, fallback, &declined))
                 return -1;
+            b->inorder = declined ? 2 : 1;
             if (!declined)
                 return 0;
         }

@@ -149,6 +149,8 @@ def lib():
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
         "srtp_mi355x_prepass_sorted_batches": ([P], C.c_uint64),
+        "srtp_mi355x_inorder_stats": ([P, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_debug_key_left": ([P, C.c_uint32, C.c_size_t,
                                         C.POINTER(C.c_uint64)], C.c_int),
         "srtp_mi355x_debug_set_key_limit": ([P, C.c_uint32, C.c_uint64],
@@ -562,6 +564,12 @@ class Session:
     def prepass_sorted_batches(self):
         """device pre-pass batches that needed the sorted chain path"""
         return self.L.srtp_mi355x_prepass_sorted_batches(self.h)
+
+    def inorder_stats(self):
+        """(batches the one-stream in-order form committed, declined)"""
+        r, d = C.c_uint64(), C.c_uint64()
+        self.L.srtp_mi355x_inorder_stats(self.h, C.byref(r), C.byref(d))
+        return r.value, d.value
 
     def unprotect_stats(self):
         """(rounds, crypto launches, undo launches) of the last unprotect

@@ -1696,3 +1696,186 @@ def _check_rx_arena(orc, pkts, st, before, after, offs, what=""):
         raise AssertionError("%s: arena byte %d differs: packet %d (len %d, "
                              "status %d) byte %d" % (what, bad, i, len(pkts[i]),
                                                      st[i], bad - offs[i]))
+
+
+def _rx_stream(name, ssrc, seed):
+    pols = [policy(name, ssrc=ssrc, seed=seed)]
+    return O.Session(pols), L.Session(pols), O.Session(pols)
+
+
+def _sender_run(snd, rng, ssrc, seq, n, payloads=(0, 7, 40)):
+    out = []
+    for k in range(n):
+        p = rtp_packet(rng, ssrc, (seq + k) & 0xffff, rng.choice(payloads))
+        rc, ref = snd.protect(p, len(p) + 64)
+        assert rc == 0
+        out.append(ref)
+    return out
+
+
+def _forge(pk, ks, bit=0x10):
+    for k in ks:
+        b = bytearray(pk[k])
+        b[-1] ^= bit
+        pk[k] = bytes(b)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_in_order_receive_long_forged_tail(name):
+    """a run whose last 4,500 of 5,000 tags are forged: the last accepted
+    packet lies 4,500 from the end (k_io_rx_commit finds it from the block
+    records, no LDS flag loop), the in-order form commits it (no decline),
+    and every status, arena byte, key use and the window through replays
+    equal the oracle's (srtp.c:3157-3167: replay add after the tag;
+    rdbx.c:253-270)"""
+    _gpu()
+    rng = random.Random(741)
+    ssrc = 0x29200000
+    snd, lib, orc = _rx_stream(name, ssrc, 4)
+    seq = 0xffff - 700          # across a ROC wrap
+    warm = _sender_run(snd, rng, ssrc, seq, 4)
+    seq += 4
+    st, before, after, offs = _arena_run_rx(lib, warm, [len(p) for p in warm],
+                                            24, rng)
+    _check_rx_arena(orc, warm, st, before, after, offs, "warm")
+    sent = []
+    for b, forged in enumerate([range(500, 5000), range(0, 4990),
+                                range(100, 5000)]):
+        pk = _sender_run(snd, rng, ssrc, seq, 5000)
+        seq += 5000
+        _forge(pk, forged)
+        r0, d0 = lib.inorder_stats()
+        st, before, after, offs = _arena_run_rx(lib, pk, [len(p) for p in pk],
+                                                24, rng)
+        _check_rx_arena(orc, pk, st, before, after, offs, "batch %d" % b)
+        assert lib.inorder_stats() == (r0 + 1, d0), ("in-order form", b)
+        sent += pk
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)
+    # the window: accepted and forged packets again, then a new one
+    pk = sent[-5000 + 95:-5000 + 130] + sent[-20:]
+    pk += _sender_run(snd, rng, ssrc, seq, 1)
+    st, before, after, offs = _arena_run_rx(lib, pk, [len(p) for p in pk], 24,
+                                            rng)
+    _check_rx_arena(orc, pk, st, before, after, offs, "window")
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+@pytest.mark.parametrize("case", ["long_reject", "gap_then_reject",
+                                  "just_below"])
+def test_in_order_receive_reject_run_past_2_15(name, case):
+    """rejected runs that carry a packet 2^15 or more past the last accepted
+    index (or the stored one): the reference's estimate from that top
+    (rdbx.c:112-145) is then another ROC -- replay_old, or a decryption at
+    another index -- so the in-order form must decline the batch (AB_GAP)
+    and the chain form / host decide; a run just below 2^15 stays in the
+    in-order form.  Every status and arena byte against the oracle"""
+    _gpu()
+    rng = random.Random(743)
+    ssrc = 0x29300000
+    snd, lib, orc = _rx_stream(name, ssrc, 5)
+    # a stored index above 2^15 (below it index_guess keeps ROC 0 and the
+    # estimates would not diverge inside one ROC)
+    seq = 40000
+    warm = _sender_run(snd, rng, ssrc, seq, 4)
+    seq += 4
+    st, before, after, offs = _arena_run_rx(lib, warm, [len(p) for p in warm],
+                                            24, rng)
+    _check_rx_arena(orc, warm, st, before, after, offs, "warm")
+    if case == "long_reject":          # 33,000 forged, then authentic ones
+        n, skip, forged, declined = 34000, 0, range(0, 33000), True
+    elif case == "gap_then_reject":    # 20,000 skipped, then 13,000 forged
+        n, skip, forged, declined = 14000, 20000, range(0, 13000), True
+    else:                              # a reject run of 32,000: in the form
+        n, skip, forged, declined = 33000, 0, range(500, 32500), False
+    seq += skip
+    pk = _sender_run(snd, rng, ssrc, seq, n, payloads=(0, 12))
+    seq += n
+    _forge(pk, forged)
+    r0, d0 = lib.inorder_stats()
+    st, before, after, offs = _arena_run_rx(lib, pk, [len(p) for p in pk], 24,
+                                            rng)
+    _check_rx_arena(orc, pk, st, before, after, offs, case)
+    assert lib.inorder_stats() == ((r0, d0 + 1) if declined else (r0 + 1, d0))
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)
+    pk = _sender_run(snd, rng, ssrc, seq, 50)
+    st, before, after, offs = _arena_run_rx(lib, pk, [len(p) for p in pk], 24,
+                                            rng)
+    _check_rx_arena(orc, pk, st, before, after, offs, "after")
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_mki_mixed_keys_with_key_buckets(name):
+    """key buckets on (srtp_mi355x_set_key_buckets(1)): a many-stream MKI
+    protect batch whose packets pick different master keys must not take
+    the bucketed kernel, which runs one key per 64-record group -- every
+    packet on the key its mki_index selects (srtp.c:2536-2545), every byte,
+    status and per-key use against the oracle"""
+    _gpu()
+    rng = random.Random(751)
+    ssrcs = [0x22600000 + 5 * k for k in range(12)]
+    pols = [policy(name, ssrc=s, seed=40 + k, mki=4, nkeys=3)
+            for k, s in enumerate(ssrcs)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
+    L.lib().srtp_mi355x_set_key_buckets(1)
+    try:
+        d0, h0 = lib.prepass_stats()
+        for b in range(2):
+            pk = _interleaved(rng, ssrcs, seq0, 96, payloads=(0, 20, 172))
+            mki = [rng.randrange(3) for _ in pk]
+            caps = [len(p) + 32 for p in pk]
+            st, out = _device_run(lib, pk, caps, "protect", mki)
+            for i, p in enumerate(pk):
+                rc, ref = orc.protect(p, caps[i], mki[i])
+                assert st[i] == rc, (b, i, st[i], rc)
+                assert rc or out[i] == ref, (b, i, mki[i])
+        assert lib.prepass_stats() == (d0 + 2, h0)
+        _key_left_equal(lib, orc, ssrcs, 3)
+    finally:
+        L.lib().srtp_mi355x_set_key_buckets(0)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_mki_pending_roc_stream_with_fewer_keys_than_rx_hint(name):
+    """a session receiving on an MKI stream with 3 keys (the host path
+    matched key 2 last, so receive batches use master key 2) and sending on
+    an MKI stream with ONE key whose ROC the application set: the sender is
+    receive-ineligible (fewer keys than 2) but protect-eligible, and its
+    packets must still be estimated as pending_roc || seq (srtp.c:2069-2076)
+    -- every byte, status and the ROC afterwards against the oracle"""
+    _gpu()
+    rng = random.Random(753)
+    ra, sb = 0x22700000, 0x22700001
+    pols = [policy(name, ssrc=ra, seed=61, mki=4, nkeys=3),
+            policy(name, ssrc=sb, seed=62, mki=4, nkeys=1)]
+    peer = O.Session(pols)
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq = 300
+    for b in range(3):   # key 2 on the receive stream: host, then device
+        pk = []
+        for k in range(40):
+            p = rtp_packet(rng, ra, seq, 40)
+            seq += 1
+            rc, ref = peer.protect(p, len(p) + 64, 2)
+            assert rc == 0
+            pk.append(ref)
+        st, out = _device_run(lib, pk, [len(p) for p in pk], "unprotect")
+        for i, p in enumerate(pk):
+            rc, ref = orc.unprotect(p, len(p))
+            assert st[i] == rc == 0 and out[i] == ref, (b, i)
+    assert lib.set_roc(sb, 7) == 0 and orc.set_roc(sb, 7) == 0
+    d0, h0 = lib.prepass_stats()
+    for b, s0 in enumerate((0x1000, 0x1000 + 64)):
+        pk = [rtp_packet(rng, sb, s0 + k, rng.choice((0, 30, 160)))
+              for k in range(64)]
+        caps = [len(p) + 32 for p in pk]
+        st, out = _device_run(lib, pk, caps, "protect", [0] * len(pk))
+        for i, p in enumerate(pk):
+            rc, ref = orc.protect(p, caps[i], 0)
+            assert st[i] == rc == 0, (b, i, st[i], rc)
+            assert out[i] == ref, (b, i)
+    d, h = lib.prepass_stats()
+    assert d - d0 >= 1, (d - d0, h - h0)
+    assert lib.get_roc(sb)[1] == orc.get_roc(sb)[1] == 7
