@@ -44,9 +44,10 @@ max over ranks, the one JSON line) over gloo on the CPU with a stub step
 (rank r sleeps (r + 1) ms), for tests without a GPU.
 
 Extra fields: roofline (dominant kernel, HIP-event timed on the stream the
-kernels ran on; `traffic` = FETCH_SIZE + WRITE_SIZE per launch from
-separate rocprofv3 PMC passes, `traffic_over_algorithmic` = that over the
-algorithmic bytes, `issue` = VALU / LDS instruction floors, `additive_frac`
+kernels ran on; `traffic` = the L2's 32/64/128-B fabric read requests at
+their size + WRITE_SIZE per launch from separate rocprofv3 PMC passes,
+`traffic_over_algorithmic` = that over the algorithmic bytes,
+`traffic_split` = read and write amplification separately, `issue` = VALU / LDS instruction floors, `additive_frac`
 their sum over the launch), cpu_baseline (the reference, cisco/libsrtp built from
 its own sources, srtp_protect() per packet on host threads, rank 0 only).
 """
@@ -186,9 +187,32 @@ def pmc_counter(path, kernels, counter):
 
 
 # PMC passes (MI355X_MICROARCH.md: one pass holds at most 4 TCC counters,
-# FETCH_SIZE takes 3 and WRITE_SIZE 2, so they run separately)
-PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
+# FETCH_SIZE takes 3 and WRITE_SIZE 2, so they run separately).  The read
+# bytes come from the L2's memory-side read requests by size: gfx950's
+# FETCH_SIZE tallies a 128-byte request at 64 B (MI355X_MICROARCH.md:298),
+# so it is kept only as a raw secondary figure.
+RDREQ = ("TCC_EA0_RDREQ_32B_sum", "TCC_EA0_RDREQ_64B_sum",
+         "TCC_EA0_RDREQ_128B_sum", "TCC_EA0_RDREQ_sum")
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), RDREQ,
               ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_WAVES"))
+
+
+def read_bytes(pmc):
+    """bytes the L2 requested from the fabric per launch: 32 / 64 / 128-B
+    read requests at their size (None without the request-size pass)"""
+    if any(c not in pmc for c in RDREQ[:3]):
+        return None
+    return (32.0 * pmc[RDREQ[0]] + 64.0 * pmc[RDREQ[1]] +
+            128.0 * pmc[RDREQ[2]])
+
+
+def traffic_bytes(pmc):
+    """roofline.traffic: read requests at their size + WRITE_SIZE (exact for
+    streaming stores, MI355X_MICROARCH.md:299); None if a pass is missing"""
+    rd = read_bytes(pmc)
+    if rd is None or "WRITE_SIZE" not in pmc:
+        return None
+    return rd + pmc["WRITE_SIZE"] * 1024.0
 
 
 DIST_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
@@ -199,25 +223,34 @@ DIST_VARS = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE",
 
 
 def traffic_split(a, n, rtp_len, tag, pmc):
-    """FETCH_SIZE and WRITE_SIZE per launch as counted, each against the
-    algorithmic bytes of its direction (profiles/r04_fetch_calibration.md
-    measures what a byte-exact copy of each access shape counts: 16-B
-    per-lane pieces count up to 2-2.8x their bytes)"""
-    if "FETCH_SIZE" not in pmc or "WRITE_SIZE" not in pmc:
+    """read and write bytes per launch, each against the algorithmic bytes
+    of its direction (read / write amplification), the request counts they
+    come from, and FETCH_SIZE as counted (raw, 128-B requests at half).
+    The counters see the L2's fabric requests, Infinity-Cache hits included
+    (MI355X_MICROARCH.md:297): re-read key records served on-die count."""
+    rd_alg = n * (rtp_len + (tag if a.op == "unprotect" else 0))
+    wr_alg = n * (rtp_len + (0 if a.op == "unprotect" else tag))
+    rd = read_bytes(pmc)
+    w = pmc["WRITE_SIZE"] * 1024.0 if "WRITE_SIZE" in pmc else None
+    if rd is None and w is None:
         return None
-    rd = n * (rtp_len + (tag if a.op == "unprotect" else 0))
-    wr = n * (rtp_len + (0 if a.op == "unprotect" else tag))
-    f, w = pmc["FETCH_SIZE"] * 1024.0, pmc["WRITE_SIZE"] * 1024.0
-    return {"fetch": f, "write": w, "fetch_over_read_bytes": f / rd,
-            "write_over_written_bytes": w / wr}
+    out = {"read_bytes": rd, "write_bytes": w,
+           "read_algorithmic": rd_alg, "write_algorithmic": wr_alg,
+           "read_amplification": rd / rd_alg if rd is not None else None,
+           "write_amplification": w / wr_alg if w is not None else None,
+           "rdreq": {k.replace("TCC_EA0_", "").replace("_sum", ""): pmc[k]
+                     for k in RDREQ if k in pmc}}
+    if "FETCH_SIZE" in pmc:
+        out["fetch_size_raw"] = pmc["FETCH_SIZE"] * 1024.0
+    return out
 
 
 def measure_pmc(a, kernels, device=0):
     """per-launch PMC counters of the dominant kernel over a short run of
     this same workload, one rocprofv3 --pmc pass per entry of PMC_PASSES,
     each a child process started before this process touches the GPU.
-    FETCH_SIZE is TCC_EA0_RDREQ x 64 B.  `traffic` is FETCH_SIZE +
-    WRITE_SIZE as counted (traffic_split() per direction)."""
+    `traffic` is the read requests at their size plus WRITE_SIZE
+    (traffic_bytes(); traffic_split() per direction)."""
     import glob
     import shutil
     import subprocess
@@ -782,9 +815,7 @@ def run_gpu(a, world, rank, local, json_out):
     pmc = {}
     if rank == 0 and a.traffic == "auto":
         pmc = measure_pmc(a, kernels, devno)
-    traffic = None
-    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
-        traffic = (pmc["FETCH_SIZE"] + pmc["WRITE_SIZE"]) * 1024.0
+    traffic = traffic_bytes(pmc)
     import torch
     import torch.distributed as dist
     # SRTP_FORCE_DIST=1: a one-rank process group, so the RCCL barrier,

@@ -35,3 +35,23 @@ def test_bounded_leg_result_and_limit():
     # a leg past its limit reports nothing instead of stalling the bench
     assert bench._bounded("_ref_rate", lib, "protect", 160, False, 2, 60.0,
                           limit=1) is None
+
+
+def test_traffic_counts_read_requests_at_their_size():
+    """roofline.traffic: 32/64/128-B read requests at their size plus
+    WRITE_SIZE; gfx950's FETCH_SIZE (128-B requests at 64 B) stays a raw
+    secondary figure, and a missing pass gives no number"""
+    class A:
+        op = "protect"
+    pmc = {"TCC_EA0_RDREQ_32B_sum": 10.0, "TCC_EA0_RDREQ_64B_sum": 100.0,
+           "TCC_EA0_RDREQ_128B_sum": 1000.0, "TCC_EA0_RDREQ_sum": 1110.0,
+           "WRITE_SIZE": 200.0, "FETCH_SIZE": 70.0}
+    rd = 32 * 10 + 64 * 100 + 128 * 1000
+    assert bench.read_bytes(pmc) == rd
+    assert bench.traffic_bytes(pmc) == rd + 200 * 1024
+    sp = bench.traffic_split(A(), 100, 172, 10, pmc)
+    assert sp["read_bytes"] == rd and sp["write_bytes"] == 200 * 1024
+    assert sp["read_amplification"] == rd / (100 * 172)
+    assert sp["write_amplification"] == 200 * 1024 / (100 * 182)
+    assert sp["fetch_size_raw"] == 70 * 1024
+    assert bench.traffic_bytes({"WRITE_SIZE": 1.0}) is None
