@@ -309,10 +309,15 @@ typedef struct srtp_gpu_pp_batch {
                                classify inside the crypto kernel */
     uint32_t max_trailer;   /* protect: the largest tag + MKI of the streams
                                the device may encrypt */
-    int inorder_ok;         /* protect: in place, one uniform-key AES-ICM / GCM
-                               variant, trailers <= 16 bytes, synchronous: a
-                               one-stream batch may try the in-order form
-                               (indices computed in the crypto kernel) */
+    int inorder_ok;         /* one uniform-key AES-ICM / GCM variant,
+                               trailers <= 16 bytes: a one-stream batch may
+                               try the in-order form (indices computed in the
+                               crypto kernel; protect out of place or async:
+                               checked first by k_io_check) */
+    int mki_rx;             /* unprotect: the table has MKI streams -- each
+                               packet's MKI selects its master key on the
+                               device (srtp.c:1961-2016), charged per key;
+                               no key buckets */
     int inorder;            /* out: 1 the in-order form committed the batch,
                                2 it declined it (the chain form ran), 0 not
                                tried */

@@ -377,8 +377,9 @@ DEV void fzu_verdict(const ARGS &A, uint32_t i, FzLane &z,
 
 // One stream's in-order batch (IcmChain): the descriptor of packet i from
 // its header (srtp_rtp_hdr.h srtp_inorder_desc), else no crypto and the
-// batch is declined (*abort).  Protect saves the trailer bytes the tag will
-// overwrite, for the decline's restore.
+// batch is declined (*abort).  Protect in place saves the trailer bytes the
+// tag will overwrite, for the decline's restore (Q.tsave; null when
+// k_io_check verified the batch first).  The output is at out_off.
 template <bool RX, class ARGS>
 DEV srtp_dev_meta_t inorder_meta(const ARGS &A, uint32_t i, uint64_t off,
                                  const srtp_dev_stream_t &S, uint32_t seq0,
@@ -393,9 +394,12 @@ DEV srtp_dev_meta_t inorder_meta(const ARGS &A, uint32_t i, uint64_t off,
         return m;
     }
     if constexpr (!RX) {
-        u32x4 w;
-        fz_tail_save(A.out + off + len, S.trailer < 16 ? S.trailer : 16, w);
-        *(u32x4 *)Q.tsave[i] = w;
+        if (Q.tsave) {
+            u32x4 w;
+            fz_tail_save(A.out + off + len, S.trailer < 16 ? S.trailer : 16,
+                         w);
+            *(u32x4 *)Q.tsave[i] = w;
+        }
     }
     return m;
 }

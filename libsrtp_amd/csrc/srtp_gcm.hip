@@ -257,7 +257,7 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
                 const uint64_t off = A.in_off[i];
                 gcm_packet<NR, PROTECT, UNIFORM, true>(
                     A, inorder_meta<!PROTECT>(A, i, off, S, seq0, e0, e0ok),
-                    off, off, i, T, G, rk);
+                    off, A.out_off[i], i, T, G, rk);
             }
             return;
         }

@@ -95,6 +95,8 @@ constexpr uint32_t FZ_GL_WAVES = 4096;   // waves of a persistent grid, max
 // consecutive packets (rdbx.c:112-145: every advance is 1).  A packet
 // outside that (or with a length / parse error) is not encrypted and sets
 // *abort; the pre-pass then restores the batch and runs the chain form.
+// Out of place or asynchronous, k_io_check has checked every packet before
+// the kernel runs (nothing to restore): tsave is null then.
 struct IcmChain {
     const uint32_t *in_len;
     const uint32_t *cap;

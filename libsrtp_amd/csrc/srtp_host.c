@@ -204,13 +204,11 @@ typedef struct {
     int async_err;          /* a queued batch failed on the GPU: sticky,
                                every later packet call returns _fail      */
     /* MKI streams (srtp.c:1961-2036): protect batches run each packet on
-     * the master key its mki_index selects (the slots of every stream's
-     * keys in mkslot, the packets charged to each counted in kuses);
-     * receive batches use master key mki_j, the key the host path last
-     * matched (rx_hint) */
+     * the master key its mki_index selects, receive batches on the key its
+     * MKI bytes select (the slots of every stream's keys in mkslot, the
+     * packets charged to each counted in kuses) */
     int has_mki;
-    uint32_t mki_j;
-    uint32_t rx_hint;
+    int rx_multi;           /* a receive-eligible MKI stream has > 1 key   */
     uint32_t *mkslot, nmk;  /* key slots of the MKI streams' keys          */
     uint64_t *kuses;        /* downloaded per-key protect charges          */
     uint32_t mki_nmin;      /* fewest master keys of a protect-eligible
@@ -2045,8 +2043,6 @@ static int pre_unprotect(srtp_t ctx, provset_t *ps, const pkt_sum_t *s,
     u->sverdict = un_static(kst, s, cap, mki_bytes, &k, meta);
     if (u->sverdict)
         return 0;
-    if (kst->use_mki)   /* the key the next device batch takes to be in use */
-        ctx->dt.rx_hint = (uint32_t)(k - kst->keys->k);
     meta->roc = (uint32_t)(est >> 16);
     const int known = u->gpu && u->est == est;
     int accept, run = 0;
@@ -3309,11 +3305,10 @@ static srtp_err_status_t dev_results(srtp_t ctx, const srtp_device_batch_t *b,
 static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
                        srtp_dev_stream_t *d, int *first, int *rx_first)
 {
-    /* MKI streams: receive batches use master key mki_j (ineligible if the
-     * stream has fewer); protect batches pick a key per packet from the
-     * stream's list in mkslot */
-    const int mki_ok = !st->use_mki || dt->mki_j < st->keys->n;
-    const hkey_t *k = &st->keys->k[st->use_mki && mki_ok ? dt->mki_j : 0];
+    /* MKI streams: every packet picks its key from the stream's list in
+     * mkslot -- by mki_index on protect, by its MKI bytes on receive; the
+     * record's own key is master key 0 */
+    const hkey_t *k = &st->keys->k[0];
     memset(d, 0, sizeof *d);
     d->ssrc = st->ssrc;
     d->key = k->slot;
@@ -3334,8 +3329,7 @@ static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
     }
     /* header-extension encryption / cryptex streams and routed keys: host
      * pre-pass.  A pending ROC is resolved per batch (pend_resolve), in
-     * either direction: a protect-eligible MKI stream with fewer keys than
-     * mki_j (receive-ineligible) still estimates from it (srtp.c:2069-2076) */
+     * either direction (srtp.c:2069-2076) */
     const int xs = k->variant >= SRTP_VARIANT_X;
     if (!templ && st->rdbx.pending_roc && !xs) {
         d->flags |= SRTP_DS_PENDING;
@@ -3358,10 +3352,12 @@ static void dev_record(devtab_t *dt, srtp_stream_ctx_t *st, int templ,
         if (tr > dt->max_trailer)
             dt->max_trailer = tr;
     }
-    if (mki_ok && !xs && (templ || st->direction != DIR_SENDER)) {
+    if (!xs && (templ || st->direction != DIR_SENDER)) {
         d->flags |= SRTP_DS_RX_ELIGIBLE;
-        if (k->num_left < dt->num_left_min)
-            dt->num_left_min = k->num_left;
+        if (left < dt->num_left_min)   /* every key of an MKI stream */
+            dt->num_left_min = left;
+        if (st->use_mki && st->keys->n > 1)
+            dt->rx_multi = 1;
         if (*rx_first)
             dt->rx_uniform = k->slot;
         else if (dt->rx_uniform != k->slot)
@@ -3393,8 +3389,7 @@ static int dev_build(srtp_t ctx)
         nwords += ctx->list[i]->rdbx.bits / 32;
     /* template sessions: spare records for the streams a batch creates */
     srtp_stream_ctx_t *tp = ctx->templ;
-    const int tmpl_ok = tp && (!tp->use_mki || dt->mki_j < tp->keys->n) &&
-                        tp->keys->k[0].variant < SRTP_VARIANT_X;
+    const int tmpl_ok = tp && tp->keys->k[0].variant < SRTP_VARIANT_X;
     const uint32_t spare = tmpl_ok ? (ns > DEV_SPARE_MIN ? ns : DEV_SPARE_MIN)
                                    : 0;
     const size_t tw = tmpl_ok ? tp->rdbx.bits / 32 : 0;
@@ -3439,6 +3434,7 @@ static int dev_build(srtp_t ctx)
     int first = 1, rx_first = 1;
     uint32_t woff = 0;
     dt->has_mki = 0;
+    dt->rx_multi = 0;
     for (uint32_t sid = 0; sid < ns; sid++) {
         srtp_stream_ctx_t *st = ctx->list[sid];
         srtp_dev_stream_t *d = &dt->hs[sid];
@@ -3546,21 +3542,6 @@ static int dev_mki_index(srtp_t ctx, const uint8_t *m8, const size_t *m64,
     return 0;
 }
 
-/* ... and the key a receive batch's MKI streams are taken to use: the one
- * the host path matched last (a packet carrying another key's MKI sends the
- * batch back to the host, srtp_prepass.hip AB_MKI) */
-static int dev_mki_rx(srtp_t ctx)
-{
-    devtab_t *dt = &ctx->dt;
-    if (dt->rx_hint != dt->mki_j) {
-        dev_pull(ctx);
-        dt->mki_j = dt->rx_hint;
-        if (dev_build(ctx))
-            return 1;
-    }
-    return 0;
-}
-
 static void dev_pull(srtp_t ctx)
 {
     devtab_t *dt = &ctx->dt;
@@ -3587,12 +3568,10 @@ static void dev_pull(srtp_t ctx)
         const srtp_dev_stream_t *d = &dt->hs[sid];
         st->rdbx.index = d->index;
         memcpy(st->rdbx.w, dt->hwin + d->win_off, st->rdbx.bits / 8);
-        /* uses: the packets charged to the stream's device key (receive
-         * batches of MKI streams: key mki_j); kuses: protect packets of
-         * MKI streams, per master key */
-        const size_t kj = st->use_mki ? dt->mki_j : 0;
-        if (kj < st->keys->n)
-            st->keys->k[kj].num_left -= d->uses;
+        /* uses: the packets charged to the stream's key (an MKI stream's
+         * charges all moved to kuses: srtp_prepass.hip k_mki_keys,
+         * k_mki_rx_charge); kuses: per master key */
+        st->keys->k[0].num_left -= d->uses;
         for (uint32_t j = 0; j < d->nkeys; j++)
             st->keys->k[j].num_left -= dt->kuses[d->kbase + j];
         /* a device batch never used a stream against its direction (the
@@ -3614,9 +3593,7 @@ static void dev_pull(srtp_t ctx)
             tp->keys->k[j].num_left -= dt->kuses[dt->tmpl_kbase + j];
     for (uint32_t sid = dt->ns; tp && sid < ns_now; sid++) {
         const srtp_dev_stream_t *d = &dt->hs[sid];
-        const size_t kj = tp->use_mki ? dt->mki_j : 0;
-        if (kj < tp->keys->n)
-            tp->keys->k[kj].num_left -= d->uses;
+        tp->keys->k[0].num_left -= d->uses;
         if (!(d->dir & (SRTP_DIR_TX | SRTP_DIR_RX)))
             continue;
         srtp_stream_ctx_t *st = stream_clone(tp, d->ssrc);
@@ -3830,14 +3807,13 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
                   dt->max_trailer <= 16 && !async && !mki8;
     pb.max_trailer = dt->max_trailer;
     /* one stream in order: indices in the crypto kernel (uniform key, one
-     * AES-ICM or AES-GCM variant, in place, synchronous; srtp_prepass.hip
-     * pp_protect_inorder) */
-    pb.inorder_ok = b->in == b->out && b->in_off == b->out_off &&
-                    dt->mask && (dt->mask & (dt->mask - 1)) == 0 &&
+     * AES-ICM or AES-GCM variant; srtp_prepass.hip pp_protect_inorder --
+     * out of place or asynchronous with the batch checked first) */
+    pb.inorder_ok = dt->mask && (dt->mask & (dt->mask - 1)) == 0 &&
                     ((dt->mask & 0xfc00u) == dt->mask ||
                      (dt->mask & 0x440000u) == dt->mask) &&
                     dt->uniform != 0xffffffffu && dt->max_trailer <= 16 &&
-                    !async && !mki8;
+                    !mki8;
     int fallback = 1;
     srtp_gpu_set_timing(ctx->gpu, ctx->timing);
     const int rr = pp_run(ctx, &pb, 0, &fallback);
@@ -3945,8 +3921,6 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     }
     if (!dt->valid && dev_build(ctx))
         return -1;
-    if (dt->has_mki && dev_mki_rx(ctx))
-        return -1;
     if (dt->num_left_min == UINT64_MAX ||
         dt->num_left_min < dt->uses_bound + b->n + SOFT_LIMIT) {
         dt->last_abort = 128;
@@ -3963,16 +3937,19 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
     pb.out_len = b->out_len;
     pb.status = b->status;
     pb.stream = b->stream;
-    pb.uniform_key = dt->rx_uniform;
+    /* an MKI stream with several keys: a key per packet */
+    pb.uniform_key = dt->rx_multi ? 0xffffffffu : dt->rx_uniform;
+    pb.mki_rx = dt->has_mki;
     pb.mask = dt->rx_mask;
     /* the order-free receive form may classify inside the AES-ICM kernel:
-     * in place (a declined batch is restored), one AES-ICM kernel variant */
+     * in place (a declined batch is restored), one AES-ICM kernel variant,
+     * no MKI streams (their per-packet keys are k_pu_classify's) */
     pb.fused_ok = b->in == b->out && b->in_off == b->out_off && dt->rx_mask &&
                   (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
-                  fused_variant(dt->rx_mask, dt->rx_uniform);
-    /* one stream in order (srtp_prepass.hip pp_unprotect_inorder) */
-    pb.inorder_ok = b->in == b->out && b->in_off == b->out_off &&
-                    dt->rx_mask && (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
+                  fused_variant(dt->rx_mask, dt->rx_uniform) && !dt->has_mki;
+    /* one stream in order (srtp_prepass.hip pp_unprotect_inorder), in place
+     * or not (a rejected packet's output is undone to its ciphertext) */
+    pb.inorder_ok = dt->rx_mask && (dt->rx_mask & (dt->rx_mask - 1)) == 0 &&
                     ((dt->rx_mask & 0xfc00u) == dt->rx_mask ||
                      (dt->rx_mask & 0x440000u) == dt->rx_mask) &&
                     dt->rx_uniform != 0xffffffffu && !dt->has_mki;

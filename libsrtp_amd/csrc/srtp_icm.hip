@@ -674,7 +674,7 @@ void k_icm_hmac(IcmArgs A)
                     const uint64_t off = A.in_off[i];
                     icm_packet<NR, TAB4, AUTH, PROTECT, KM>(
                         A, inorder_meta<!PROTECT>(A, i, off, S, seq0, e0, e0ok),
-                        off, off, i, A.uni, T, rk);
+                        off, A.out_off[i], i, A.uni, T, rk);
                 }
                 return;
             }

@@ -94,6 +94,7 @@ struct PpState {
     uint64_t *val = nullptr, *est = nullptr;
     srtp_dev_meta_t *meta = nullptr;
     uint8_t *auth = nullptr;        // unprotect: tag verdict per packet
+    uint8_t *rxj = nullptr;         // unprotect, MKI streams: key index
     uint64_t *top = nullptr;        // unprotect chain: highest accepted before
     uint32_t *bcount2 = nullptr;    // unprotect: authenticated per stream
     uint64_t *new_index2 = nullptr; // unprotect: highest authenticated
@@ -221,6 +222,23 @@ __device__ __forceinline__ uint32_t map_hash(uint32_t k, uint32_t mask)
     return h & mask;
 }
 
+// the stream of an SSRC in the device hash (NOCHAIN: none)
+__device__ __forceinline__ uint32_t lookup_sid(const uint32_t *hkey,
+                                               const uint32_t *hval,
+                                               uint32_t hmask, uint32_t ssrc)
+{
+    uint32_t p = map_hash(ssrc, hmask);
+    for (uint32_t probe = 0; probe <= hmask; probe++) {
+        const uint32_t v = hval[p];
+        if (v == NOCHAIN)
+            return NOCHAIN;
+        if (hkey[p] == ssrc)
+            return v;
+        p = (p + 1) & hmask;
+    }
+    return NOCHAIN;
+}
+
 struct ClassifyArgs {
     const uint8_t *in;
     const uint64_t *in_off;
@@ -240,27 +258,41 @@ struct ClassifyArgs {
     unsigned long long *new_index;
     srtp_dev_meta_t *meta;
     uint32_t *olen;
-    // unprotect: the key records (MKI streams compare the packet's MKI with
-    // their device key's)
+    // unprotect: the key records and the slots of the MKI streams' master
+    // keys (a packet's MKI selects its key, mki_match), and per packet the
+    // key index found (rxj: MKI_NONE = bad_mki)
     const srtp_dev_key_t *keys;
+    const uint32_t *mkslot;
+    uint8_t *rxj;
 };
 
-// an MKI stream's packet (length checks passed) carries its device key's
-// MKI (srtp.c:1961-2016 srtp_get_session_keys_for_packet; any other MKI,
-// including an unknown one, is the host path's: bad_mki or another key)
-__device__ __forceinline__ bool mki_is_device_key(const srtp_dev_key_t *keys,
-                                                  const srtp_dev_stream_t &S,
-                                                  const uint8_t *pkt,
-                                                  uint32_t len)
+// the master key an MKI stream's packet (length checks passed) selects: the
+// first of the stream's keys whose MKI equals the packet's (srtp.c:1961-2016
+// srtp_get_session_keys_for_packet, keys in list order), MKI_NONE for none
+// (srtp_err_status_bad_mki, after the replay check: srtp.c:2884-2912)
+constexpr uint32_t MKI_NONE = 0xffu, ST_BAD_MKI = 25;
+__device__ __forceinline__ uint32_t mki_match(const srtp_dev_key_t *keys,
+                                              const uint32_t *mkslot,
+                                              const srtp_dev_stream_t &S,
+                                              const uint8_t *pkt, uint32_t len)
 {
     const uint32_t sz = S.mki & 0xffffu, back = S.mki >> 16;
     const uint8_t *p = pkt + len - back;
-    const uint8_t *m = keys[S.key].mki;
-    uint32_t d = 0;
-    for (uint32_t b = 0; b < sz; b++)
-        d |= p[b] ^ m[b];
-    return d == 0;
+    for (uint32_t j = 0; j < S.nkeys; j++) {
+        const uint8_t *m = keys[mkslot[S.kbase + j]].mki;
+        uint32_t d = 0;
+        for (uint32_t b = 0; b < sz; b++)
+            d |= p[b] ^ m[b];
+        if (d == 0)
+            return j;
+    }
+    return MKI_NONE;
 }
+
+// the tag verdict byte of unprotect (auth[]): 1 authenticated (or no tag
+// check), 0 the tag failed, AUTH_BAD_MKI no key matched the packet's MKI (no
+// crypto ran)
+constexpr uint8_t AUTH_BAD_MKI = 2;
 
 // index_guess against a stream's stored index (srtp_host.c estimate /
 // index_guess = rdbx.c:112-145, 280-299); returns delta
@@ -774,6 +806,41 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
     }
 }
 
+// ... out of place or asynchronous: the in-order conditions checked for
+// every packet BEFORE the crypto kernel (the same test as inorder_meta,
+// srtp_inorder_desc), so that a declined batch has written nothing -- out of
+// place there is no input copy of the output to restore, and an
+// asynchronous caller returns on the verdict while the kernel runs
+// (k_io_publish).  One thread per packet, one atomic per wave.
+__global__ void k_io_check(const uint8_t *in, const uint64_t *in_off,
+                           const uint32_t *in_len, const uint32_t *cap,
+                           uint32_t n, const srtp_dev_stream_t *st,
+                           uint32_t *abort)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const srtp_dev_stream_t &S = st[0];
+    uint32_t seq0;
+    uint64_t e0;
+    const bool e0ok = srtp_inorder_head(S, in + in_off[0], false, seq0, e0);
+    bool bad = false;
+    if (i < n) {
+        const uint64_t off = in_off[i];
+        const uint32_t len = in_len[i];
+        const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, len);
+        srtp_dev_meta_t m;
+        bad = !srtp_inorder_desc(S, h, i, len, cap[i], seq0, e0, e0ok, false,
+                                 m);
+    }
+    if (__ballot(bad) && (threadIdx.x & 63) == 0)
+        atomicOr(abort, 1u);
+}
+
+// the checked verdict to host memory (asynchronous callers wait on it)
+__global__ void k_io_publish(const uint32_t *abort, uint32_t *pub)
+{
+    publish_abort(pub, abort);
+}
+
 // The receive side of it (pp_unprotect_inorder): the crypto kernel
 // verified and decrypted every packet of the run (auth[]); a rejected
 // packet (auth_fail) changes no other packet's index -- every estimate is
@@ -1057,6 +1124,44 @@ __global__ void k_mki_keys(const uint8_t *in, const uint64_t *in_off,
         meta[i].key = mkslot[k];
 }
 
+// MKI streams on unprotect (srtp.c:1961-2016 per packet, 2908; key.c:74-90
+// per master key): after the commit, every packet the commit charged to its
+// stream's `uses` -- AES-ICM / HMAC the accepted ones, AES-GCM every
+// candidate past the replay check (srtp_unprotect_aead counts before the
+// tag) -- moves that charge to kuses[kbase + j], j the key its MKI selected;
+// a bad_mki packet's charge (AES-GCM candidates) is dropped: the reference
+// returns before it uses a key.  The final statuses say which: 0 accepted,
+// 7 auth_fail, 25 bad_mki.  ab_a / ab_b: the batch's abort words (nothing
+// was committed when one is set).
+__global__ void k_mki_rx_charge(const uint8_t *in, const uint64_t *in_off,
+                                const uint32_t *in_len, srtp_dev_stream_t *st,
+                                const uint32_t *hkey, const uint32_t *hval,
+                                uint32_t hmask, uint32_t n, const uint8_t *rxj,
+                                unsigned long long *kuses,
+                                const int32_t *status, const uint32_t *ab_a,
+                                const uint32_t *ab_b)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || *ab_a || (ab_b && *ab_b))
+        return;
+    const int32_t v = status[i];
+    if (v != 0 && v != 7 && v != (int32_t)ST_BAD_MKI)
+        return;
+    const uint64_t off = in_off[i];
+    const srtp_dev_hdr_t h = srtp_parse_rtp(in + off, off, in_len[i]);
+    if (h.enc_start >> 24)
+        return;
+    const uint32_t sid = lookup_sid(hkey, hval, hmask, h.ssrc);
+    if (sid == NOCHAIN || !st[sid].mki)
+        return;
+    const bool aead = (st[sid].flags & SRTP_DS_AEAD) != 0;
+    if (v != 0 && !aead)
+        return;   // not charged
+    atomicAdd((unsigned long long *)&st[sid].uses, ~0ull);   // - 1
+    if (v != (int32_t)ST_BAD_MKI)
+        atomicAdd(&kuses[st[sid].kbase + rxj[i]], 1ull);
+}
+
 // An in-place batch classified inside the crypto kernel that the pre-pass
 // then declined: the bytes past every encrypted packet that its tag
 // overwrote come back (its payload is restored by k_undo_wave)
@@ -1194,7 +1299,7 @@ __global__ void k_pend_authchk(const uint32_t *pos, uint32_t nr,
                                const uint8_t *auth, uint32_t *abort)
 {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < nr && !auth[pos[k]])
+    if (k < nr && auth[pos[k]] != 1)
         atomicOr(abort, (uint32_t)AB_PENDING);
 }
 
@@ -1515,21 +1620,6 @@ __global__ void k_fz_meta(const uint8_t *in, const uint64_t *in_off,
 // crypto kernel has verified the tags, only authenticated packets move the
 // replay window and index (rdbx_add after the tag check, srtp.c:3157-3167).
 
-__device__ __forceinline__ uint32_t lookup_sid(const uint32_t *hkey,
-                                               const uint32_t *hval,
-                                               uint32_t hmask, uint32_t ssrc)
-{
-    uint32_t p = map_hash(ssrc, hmask);
-    for (uint32_t probe = 0; probe <= hmask; probe++) {
-        const uint32_t v = hval[p];
-        if (v == NOCHAIN)
-            return NOCHAIN;
-        if (hkey[p] == ssrc)
-            return v;
-        p = (p + 1) & hmask;
-    }
-    return NOCHAIN;
-}
 
 __global__ void k_pu_classify(ClassifyArgs A)
 {
@@ -1562,10 +1652,10 @@ __global__ void k_pu_classify(ClassifyArgs A)
                     ((S.flags & SRTP_DS_ICM_CONF) &&
                      (len - tag - h.enc_start + 15) / 16 > 0xffffu)) {
                     atomicOr(A.abort, AB_STATIC);
-                } else if (S.mki &&
-                           !mki_is_device_key(A.keys, S, A.in + off, len)) {
-                    atomicOr(A.abort, AB_MKI);
                 } else {
+                    if (S.mki)   // the key of the packet's MKI (k_pu_meta)
+                        A.rxj[i] = (uint8_t)mki_match(A.keys, A.mkslot, S,
+                                                      A.in + off, len);
                     key = sid;
                     if (A.est) {   // order-free form
                         const uint32_t seq = h.seq_len & 0xffffu;
@@ -1594,7 +1684,8 @@ __global__ void k_pu_meta(const uint32_t *skey, const uint32_t *perm,
                           const uint64_t *est, const srtp_dev_hdr_t *hdr,
                           const srtp_dev_stream_t *st, uint32_t ns, uint32_t n,
                           const uint32_t *abort, srtp_dev_meta_t *meta,
-                          uint8_t *auth)
+                          uint8_t *auth, const uint32_t *mkslot,
+                          const uint8_t *rxj)
 {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n)
@@ -1606,16 +1697,22 @@ __global__ void k_pu_meta(const uint32_t *skey, const uint32_t *perm,
     m.len = 0;
     m.info = 0xff0000u;
     const uint32_t s = skey[k];
+    uint8_t a = 1;   // kernels without a tag check leave it: accepted
     if (!*abort && s < ns) {
         const srtp_dev_stream_t &S = st[s];
         const srtp_dev_hdr_t h = hdr[i];
-        m.key = S.key;
-        m.roc = (uint32_t)(est[k] >> 16);
-        m.info = h.enc_start | (S.variant << 24);
-        m.len = h.len - S.trailer;
+        const uint32_t j = S.mki ? rxj[i] : 0u;
+        if (j == MKI_NONE) {
+            a = AUTH_BAD_MKI;   // no key: no crypto, verdict bad_mki
+        } else {
+            m.key = S.mki ? mkslot[S.kbase + j] : S.key;
+            m.roc = (uint32_t)(est[k] >> 16);
+            m.info = h.enc_start | (S.variant << 24);
+            m.len = h.len - S.trailer;
+        }
     }
     meta[i] = m;
-    auth[i] = 1;   // kernels without a tag check leave it: accepted
+    auth[i] = a;
 }
 
 // chain form: the reference guesses each index from the highest ACCEPTED
@@ -1633,7 +1730,7 @@ __global__ void k_pu_accepted_est(const uint32_t *skey2, const uint32_t *perm2,
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n)
         return;
-    val[k] = skey2[k] < ns && auth[perm2[k]] ? est[k] : 0;
+    val[k] = skey2[k] < ns && auth[perm2[k]] == 1 ? est[k] : 0;
 }
 
 __global__ void k_pu_top_check(const uint32_t *skey2, const uint32_t *perm2,
@@ -1680,14 +1777,15 @@ __global__ __launch_bounds__(1024) void k_pu_accept(const uint32_t *skey, const 
         const uint32_t s = skey[k];
         if (s >= ns) {
             status[i] = (int32_t)pstat[i];   // header errors; out_len kept
-        } else if (auth[i]) {
+        } else if (auth[i] == 1) {
             key = s;
             e = est[k];
             status[i] = 0;
             out_len[i] = hdr[i].len - st[s].trailer;
             meta[i].info = 0xff0000u;        // keep: nothing to undo
         } else {
-            status[i] = 7;                   // srtp_err_status_auth_fail
+            // srtp_err_status_auth_fail, or bad_mki (no crypto ran)
+            status[i] = auth[i] == AUTH_BAD_MKI ? (int32_t)ST_BAD_MKI : 7;
         }
     }
     agg_stream(key, e, bcount2, new_index2);
@@ -1705,7 +1803,7 @@ __global__ void k_pu_setbits(const uint32_t *skey, const uint32_t *perm,
     if (k >= n || *abort)
         return;
     const uint32_t s = skey[k];
-    if (s >= ns || !auth[perm ? perm[k] : k])
+    if (s >= ns || auth[perm ? perm[k] : k] != 1)
         return;
     const uint32_t bits = st[s].win_bits;
     const uint64_t dist = new_index2[s] - est[k];
@@ -2351,6 +2449,7 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
     uint32_t bad = 0, nm = 0, abort = 0, chain = 0, cand = 0;
     uint64_t off[CH_ITEMS];
     uint32_t len[CH_ITEMS], cap[CH_ITEMS], code[CH_ITEMS], seq[CH_ITEMS];
+    uint32_t kj[CH_ITEMS];   // MKI streams: the key index of the packet
     srtp_dev_hdr_t hh[CH_ITEMS];
 #pragma unroll
     for (int k = 0; k < CH_ITEMS; k++) {
@@ -2358,6 +2457,7 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
         off[k] = C.in_off[i];
         len[k] = C.in_len[i];
         cap[k] = C.cap[i];
+        kj[k] = 0;
     }
 #pragma unroll
     for (int k = 0; k < CH_ITEMS; k++)
@@ -2385,10 +2485,9 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
                 ((S.flags & SRTP_DS_ICM_CONF) &&
                  (L - tag - h.enc_start + 15) / 16 > 0xffffu)) {
                 abort |= AB_STATIC;
-            } else if (S.mki &&
-                       !mki_is_device_key(C.keys, S, C.in + off[k], L)) {
-                abort |= AB_MKI;
             } else {
+                if (S.mki)   // the packet's key (MKI_NONE: bad_mki)
+                    kj[k] = mki_match(C.keys, C.mkslot, S, C.in + off[k], L);
                 chain |= 1u << k;
                 cand++;
                 seq[k] = h.seq_len & 0xffffu;
@@ -2447,21 +2546,28 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_chain1(PuChainArgs A)
         m.len = 0;
         m.info = 0xff0000u;   // no crypto
         uint64_t e = 0;
+        uint8_t au = 1;   // kernels without a tag check leave it: accepted
         if (chain >> k & 1) {
             cs_apply(has, idx, ChAgg{ 1, seq[k], seq[k], 0 }, stored, &nm, &bad);
             e = idx;
             umin = e < umin ? e : umin;
             umax = e > umax ? e : umax;
-            m.key = S.key;
-            m.roc = (uint32_t)(e >> 16);
-            m.info = hh[k].enc_start | (S.variant << 24);
-            m.len = hh[k].len - tag;
+            if (kj[k] == MKI_NONE) {
+                au = AUTH_BAD_MKI;   // a candidate without crypto: bad_mki
+            } else {
+                m.key = S.mki ? C.mkslot[S.kbase + kj[k]] : S.key;
+                m.roc = (uint32_t)(e >> 16);
+                m.info = hh[k].enc_start | (S.variant << 24);
+                m.len = hh[k].len - tag;
+            }
+            if (S.mki)
+                C.rxj[i] = (uint8_t)kj[k];
         }
         C.est[i] = e;
         C.skey[i] = (chain >> k & 1) ? 0u : NOCHAIN;
         C.pstat[i] = code[k];
         C.meta[i] = m;
-        A.auth[i] = 1;   // kernels without a tag check leave it: accepted
+        A.auth[i] = au;
     }
     if (bad)
         abort |= AB_SEQUENCE;
@@ -2504,7 +2610,7 @@ __global__ void k_pu_first(const uint32_t *skey, const uint64_t *est,
             atomicOr(&ctl->abort2, AB_ORDER);   // indices too spread: host
         return;
     }
-    if (i >= n || skey[i] != 0u || !auth[i])
+    if (i >= n || skey[i] != 0u || auth[i] != 1)
         return;
     const unsigned long long tagv = ((unsigned long long)(~gen) << 32) | i;
     atomicMin(&first[est[i] - lo], tagv);
@@ -2550,7 +2656,7 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
     const uint32_t gen = A.gen;
     const uint32_t base = tile * CH_TILE + t * CH_ITEMS;
     uint64_t u[CH_ITEMS];
-    uint32_t cand = 0, au = 0;
+    uint32_t cand = 0, au = 0, bm = 0;   // bm: bad_mki candidates
     // values are index + 1 so that 0 means "no authenticated packet"
     uint64_t mx = 0;
 #pragma unroll
@@ -2560,9 +2666,12 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
         if (i < A.n && A.skey[i] == 0u) {
             cand |= 1u << k;
             u[k] = A.est[i];
-            if (A.auth[i]) {
+            const uint8_t a = A.auth[i];
+            if (a == 1) {
                 au |= 1u << k;
                 mx = u[k] + 1 > mx ? u[k] + 1 : mx;
+            } else if (a == AUTH_BAD_MKI) {
+                bm |= 1u << k;
             }
         }
     }
@@ -2632,9 +2741,12 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
         guess_index(T, (uint32_t)u[k] & 0xffffu, &g);
         if (g != u[k])
             bad = 1;   // the reference estimates this packet differently
+        // not authenticated: the tag failed, or (after the replay check, as
+        // srtp.c:2905-2912 orders them) no key matched its MKI
+        const uint32_t rej = (bm >> k & 1) ? ST_BAD_MKI : ST_AUTH_FAIL;
         uint32_t v;
         if (u[k] > T) {
-            v = (au >> k & 1) ? 0u : ST_AUTH_FAIL;
+            v = (au >> k & 1) ? 0u : rej;
         } else if (T - u[k] >= bits) {
             v = ST_REPLAY_OLD;
         } else {
@@ -2648,7 +2760,7 @@ __global__ __launch_bounds__(CH_THREADS) void k_pu_verdict1(PuVerdictArgs A)
                 const unsigned long long f = A.first[u[k] - lo];
                 seen = (uint32_t)(f >> 32) == ~gen && (uint32_t)f < i;
             }
-            v = seen ? ST_REPLAY_FAIL : (au >> k & 1) ? 0u : ST_AUTH_FAIL;
+            v = seen ? ST_REPLAY_FAIL : (au >> k & 1) ? 0u : rej;
         }
         if (v == ST_REPLAY_FAIL || v == ST_REPLAY_OLD)
             rep++;
@@ -2995,7 +3107,7 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
         c *= 2;
     void *old[] = { P->hdr, P->pstat, P->skey, P->skey2, P->perm,
                     P->perm2, P->val, P->est, P->meta, P->agg, P->hist,
-                    P->auth, P->top, P->rec, P->rec_idx };
+                    P->auth, P->top, P->rec, P->rec_idx, P->rxj };
     for (void *o : old)
         if (o)
             PPCHK(hipFree(o));
@@ -3009,6 +3121,7 @@ int reserve_packets(PpState *P, size_t n, hipStream_t stream)
     PPCHK(hipMalloc((void **)&P->est, c * 8));
     PPCHK(hipMalloc((void **)&P->meta, c * sizeof(srtp_dev_meta_t)));
     PPCHK(hipMalloc((void **)&P->auth, c));
+    PPCHK(hipMalloc((void **)&P->rxj, c));
     PPCHK(hipMalloc((void **)&P->top, c * 8));
     if (P->fzrec)
         PPCHK(hipFree(P->fzrec));
@@ -3065,7 +3178,7 @@ void srtp_gpu_pp_free(void *p)
                      P->fz_glist, P->pd_first, P->pd_min, P->pd_max,
                      P->pd_sids, P->pd_info, P->pd_efirst, P->pd_bak,
                      P->pd_bakwin, P->pd_pos, P->cl_ctl, P->mkslot,
-                     P->kuses, P->mki8, P->io_e0 };
+                     P->kuses, P->mki8, P->io_e0, P->rxj };
     for (void *b : bufs)
         if (b)
             (void)hipFree(b);
@@ -3486,12 +3599,23 @@ static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
     uint32_t *ab = P->ch_abort + P->ch_par;
     uint32_t *ab_next = P->ch_abort + (P->ch_par ^ 1);
     P->ch_par ^= 1;
+    // out of place or asynchronous: checked first (k_io_check), so the
+    // crypto kernel runs only on a batch that commits
+    const bool pre = b->in != b->out || b->in_off != b->out_off || b->async;
+    if (pre) {
+        hipLaunchKernelGGL(k_io_check, gp, blk, 0, stream, b->in, b->in_off,
+                           b->in_len, b->out_len, N, P->st, ab);
+        if (b->async)
+            hipLaunchKernelGGL(k_io_publish, dim3(1), dim3(64), 0, stream, ab,
+                               P->h_abort_dev);
+        PPCHK(hipGetLastError());
+    }
     IcmChain Q;
     Q.in_len = b->in_len;
     Q.cap = b->out_len;
     Q.st = P->st;
     Q.abort = ab;
-    Q.tsave = P->tsave;
+    Q.tsave = pre ? nullptr : P->tsave;
     srtp_gpu_batch_t cb = {};
     cb.n = b->n;
     cb.in = b->in;
@@ -3503,7 +3627,8 @@ static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
     cb.uniform_key = b->uniform_key;
     cb.mask = b->mask;
     cb.stream = stream;
-    cb.abort = nullptr;   // the kernel itself classifies: it always runs
+    // the kernel itself classifies: it always runs, unless checked first
+    cb.abort = pre ? ab : nullptr;
     cb.inorder = &Q;
     if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "in-order crypto"))
         return -1;
@@ -3513,12 +3638,28 @@ static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order commit"))
         return -1;
+    if (b->async) {
+        hipError_t we;
+        const uint32_t v = wait_published(P, stream, &we);
+        if (we != hipSuccess)
+            return pp_fail(we, "waiting for the in-order verdict");
+        if (v == 0) {
+            // committed: the crypto kernel and the commit are queued
+            b->sorted = 1;
+            *fallback = 0;
+            return 0;
+        }
+    }
     PPCHK(hipStreamSynchronize(stream));
     if (*(volatile uint32_t *)P->h_abort == ABORT_UNSET)
         PPCHK(hipMemcpy(P->h_abort, ab, 4, hipMemcpyDeviceToHost));
     if (*(volatile uint32_t *)P->h_abort == 0) {
         b->sorted = 1;
         *fallback = 0;
+        return 0;
+    }
+    if (pre) {   // declined before the crypto ran: nothing was written
+        *declined = true;
         return 0;
     }
     // declined: the input comes back exactly
@@ -4119,6 +4260,8 @@ static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
     A.C.meta = P->meta;
     A.C.olen = nullptr;
     A.C.keys = g->d_keys;
+    A.C.mkslot = P->mkslot;
+    A.C.rxj = P->rxj;
     A.auth = P->auth;
     A.tile = tile;
     A.ctl = ctl;
@@ -4188,6 +4331,11 @@ static int pp_unprotect_chain1(srtp_gpu_t *g, PpState *P,
                        dim3((N + CH_COMMIT_THREADS - 1) / CH_COMMIT_THREADS),
                        dim3(CH_COMMIT_THREADS), 0, stream, K);
     PU1CHK(hipGetLastError(), "k_pu_commit1");
+    if (b->mki_rx)
+        hipLaunchKernelGGL(k_mki_rx_charge, gp, blk, 0, stream, b->in,
+                           b->in_off, b->in_len, P->st, P->hkey, P->hval,
+                           P->hcap - 1, N, P->rxj, P->kuses, b->status,
+                           &ctl->abort1, &ctl->abort2);
     if (pp_step(stream, "pu_commit1"))
         return pu1_fail(P, stream);
     // rejected packets (every candidate after a post-crypto abort): their
@@ -4372,6 +4520,8 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     C.est = unordered ? P->est : nullptr;
     C.new_index = unordered ? (unsigned long long *)P->new_index : nullptr;
     C.keys = g->d_keys;
+    C.mkslot = P->mkslot;
+    C.rxj = P->rxj;
     hipLaunchKernelGGL(k_pu_classify, gp, blk, 0, stream, C);
     PPCHK(hipGetLastError());
     const uint32_t *ks, *kp;   // the order the kernels below walk
@@ -4397,14 +4547,17 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         kp = P->perm2;
     }
     hipLaunchKernelGGL(k_pu_meta, gp, blk, 0, stream, ks, kp, P->est, P->hdr,
-                       P->st, ns, N, P->abort, P->meta, P->auth);
+                       P->st, ns, N, P->abort, P->meta, P->auth, P->mkslot,
+                       P->rxj);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "pu_prepass"))
         return -1;
 
     srtp_gpu_batch_t cb = {};
+    // (not with MKI streams: their packets carry a key each, and the
+    // bucketed kernel takes one key per 64-record group)
     if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&
-        bucket_pass(P, N, b, &cb, stream))
+        !b->mki_rx && bucket_pass(P, N, b, &cb, stream))
         return -1;
     cb.n = n;
     cb.in = b->in;
@@ -4450,6 +4603,11 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     hipLaunchKernelGGL(k_pu_commit_stream, gs, blk, 0, stream, P->st, ns,
                        P->new_index2, P->bcount, P->bcount2, P->wnew, P->win,
                        P->abort, P->h_abort_dev);
+    if (b->mki_rx)
+        hipLaunchKernelGGL(k_mki_rx_charge, gp, blk, 0, stream, b->in,
+                           b->in_off, b->in_len, P->st, P->hkey, P->hval,
+                           P->hcap - 1, N, P->rxj, P->kuses, b->status,
+                           P->abort, (const uint32_t *)nullptr);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "pu_commit"))
         return -1;

@@ -898,10 +898,9 @@ def test_mki_streams_on_device_prepass(name):
     selects -- one index for the batch or a different one per packet -- and
     charge the use to that key (key.c:74-90); a batch with an index past a
     stream's keys (bad_mki) takes the host path.  Receive batches run on the
-    device with the key the host path matched last; a batch carrying another
-    key's MKI goes back to the host (AB_MKI), the next one is on the device
-    again.  Every status and byte against the oracle, one packet at a time,
-    and every key's remaining uses."""
+    device whatever keys their MKIs select (srtp.c:1961-2016 per packet).
+    Every status and byte against the oracle, one packet at a time, and
+    every key's remaining uses."""
     _gpu()
     rng = random.Random(613)
     ssrcs = [0x22000000 + 3 * k for k in range(24)]
@@ -942,10 +941,9 @@ def test_mki_streams_on_device_prepass(name):
             assert st[i] == rc, ("rx", kind, i, st[i], rc)
             assert rc or out[i] == ref, ("rx", kind, i)
     rd, rh = rcv.prepass_stats()
-    # keys 0, 2, 2, mixed, mixed, mixed, 1, 1, mixed: the receiver takes the
-    # host path after a key change and for mixed batches, else the device
-    # (the first 1 may follow a mixed batch whose last match was key 1)
-    assert rd >= 3 and rh >= 5 and rd + rh == len(plan), (rd, rh)
+    # keys 0, 2, 2, mixed, mixed, mixed, 1, 1, mixed: every receive batch on
+    # the device, each packet on the key its MKI selects (k_pu_classify)
+    assert (rd, rh) == (len(plan), 0), (rd, rh)
     _key_left_equal(rcv, orc_r, ssrcs[::4], 3)
     for s in ssrcs[::5]:
         assert snd.get_roc(s)[1] == orc.get_roc(s)[1]
@@ -1879,3 +1877,242 @@ def test_mki_pending_roc_stream_with_fewer_keys_than_rx_hint(name):
     d, h = lib.prepass_stats()
     assert d - d0 >= 1, (d - d0, h - h0)
     assert lib.get_roc(sb)[1] == orc.get_roc(sb)[1] == 7
+
+
+def _set_mki(pkt, name, mki_size, val):
+    """the packet with its MKI bytes replaced (ICM: MKI || tag at the end;
+    AES-GCM: the MKI alone at the end)"""
+    tag = POLICIES[name][4]
+    back = mki_size + (0 if name.startswith("gcm") else tag)
+    b = bytearray(pkt)
+    b[len(b) - back:len(b) - back + mki_size] = val
+    return bytes(b)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+@pytest.mark.parametrize("shape", ["one_stream", "many_streams"])
+def test_mki_receive_bursts_of_several_keys_on_device(name, shape):
+    """a receiver during a rekey overlap (srtp.c:1961-2016, called at 2908):
+    bursts whose packets alternate between two master keys' MKIs, with
+    packets carrying an MKI no key has (bad_mki 25 -- after the replay
+    check, so a replayed one says replay_fail), forged tags under either
+    key, and (one stream: the chain form's verdicts) replays; every batch
+    on the device (host count 0), every
+    status and byte equal to the oracle's srtp_unprotect per packet, and
+    every master key's remaining uses equal (key.c:74-90: AES-ICM charges
+    the accepted packets, AES-GCM every packet past the replay check,
+    bad_mki none)"""
+    _gpu()
+    rng = random.Random(761)
+    mki = 4
+    ssrcs = [0x22800000] if shape == "one_stream" else \
+        [0x22810000 + 7 * k for k in range(40)]
+    pols = [policy(name, ssrc=s, seed=70 + k, mki=mki, nkeys=3)
+            for k, s in enumerate(ssrcs)]
+    snd = O.Session(pols)
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq0 = {s: rng.randrange(1, 0xff00) for s in ssrcs}
+    per = 600 if shape == "one_stream" else 24
+    sent = []
+    for b in range(4):
+        pk = _interleaved(rng, ssrcs, seq0, per, payloads=(0, 20, 172))
+        out = []
+        for k, p in enumerate(pk):
+            j = (k + b) % 2 if b < 3 else 2     # keys 0/1 alternate, then 2
+            rc, ref = snd.protect(p, len(p) + 64, j)
+            assert rc == 0
+            out.append(ref)
+        for k in rng.sample(range(len(out)), 9):        # unknown MKI
+            out[k] = _set_mki(out[k], name, mki, b"\xee" * mki)
+        for k in rng.sample(range(len(out)), 5):        # forged tag
+            x = bytearray(out[k])
+            x[-1 if name.startswith("icm") else -mki - 1] ^= 0x20
+            out[k] = bytes(x)
+        if sent and shape == "one_stream":   # replays (k_pu_verdict1), one bad
+            old = rng.sample(sent[-1], 4)
+            old[0] = _set_mki(old[0], name, mki, b"\xee" * mki)
+            out[len(out) // 2:len(out) // 2] = old
+        d0, h0 = lib.prepass_stats()
+        st, res = _device_run(lib, out, [len(p) for p in out], "unprotect")
+        codes = set()
+        for i, p in enumerate(out):
+            rc, ref = orc.unprotect(p, len(p))
+            codes.add(rc)
+            assert st[i] == rc, (b, i, st[i], rc)
+            assert rc or res[i] == ref, (b, i)
+        assert lib.prepass_stats() == (d0 + 1, h0), b
+        assert {0, 7, 25} <= codes, codes
+        _key_left_equal(lib, orc, ssrcs[:6], 3)
+        sent.append(out)
+    for s in ssrcs[:6]:
+        assert lib.get_roc(s)[1] == orc.get_roc(s)[1]
+
+
+def _arena_run_oop(sess, pkts, caps, slot_extra, rng, op="protect"):
+    """srtp_{un}protect_device out of place: input and output arenas with
+    random bytes around the packets -> (statuses, input before, input after,
+    output before, output after, offsets)"""
+    import torch
+    offs, pos = [], 0
+    for p, c in zip(pkts, caps):
+        offs.append(pos)
+        pos += (max(len(p), c) + slot_extra + 15) & ~15
+    bin_ = bytearray(rng.randbytes(pos + 16))
+    for o, p in zip(offs, pkts):
+        bin_[o:o + len(p)] = p
+    bout = rng.randbytes(pos + 16)
+    ain = torch.frombuffer(bytearray(bin_), dtype=torch.uint8).cuda()
+    aout = torch.frombuffer(bytearray(bout), dtype=torch.uint8).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor([len(p) for p in pkts], dtype=torch.int32).cuda()
+    cap = torch.tensor(caps, dtype=torch.int32).cuda()
+    st = torch.full((len(pkts),), -1, dtype=torch.int32).cuda()
+    fn = sess.protect_device if op == "protect" else sess.unprotect_device
+    assert fn(ain, off, ln, aout, off, cap, st) == 0
+    return (st.cpu().tolist(), bytes(bin_), ain.cpu().numpy().tobytes(), bout,
+            aout.cpu().numpy().tobytes(), offs)
+
+
+def _arena_run_async(sess, pkts, caps, slot_extra, rng):
+    """srtp_protect_device_async in place, then the stream drained"""
+    import torch
+    offs, pos = [], 0
+    for p, c in zip(pkts, caps):
+        offs.append(pos)
+        pos += (max(len(p), c) + slot_extra + 15) & ~15
+    before = bytearray(rng.randbytes(pos + 16))
+    for o, p in zip(offs, pkts):
+        before[o:o + len(p)] = p
+    arena = torch.frombuffer(bytearray(before), dtype=torch.uint8).cuda()
+    off = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor([len(p) for p in pkts], dtype=torch.int32).cuda()
+    cap = torch.tensor(caps, dtype=torch.int32).cuda()
+    st = torch.full((len(pkts),), -1, dtype=torch.int32).cuda()
+    torch.cuda.synchronize()
+    b = sess.prepare_device(arena, off, ln, arena, off, cap, st)
+    assert sess.protect_prepared_async(b) == 0
+    torch.cuda.synchronize()
+    return st.cpu().tolist(), bytes(before), arena.cpu().numpy().tobytes(), offs
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "icm256_hmac32",
+                                  "gcm256_16"])
+@pytest.mark.parametrize("mode", ["out_of_place", "async"])
+def test_one_stream_in_order_form_out_of_place_and_async(name, mode):
+    """the in-order form for the reference's other callers: out of place
+    (test/srtp_driver.c:262-264's not-in-place wrapper) and asynchronous
+    (srtp_protect_device_async) -- k_io_check verifies the batch before the
+    crypto kernel, so a declined batch (a duplicate, a gap, a too-small
+    buffer) has written nothing and the chain form runs it.  Every status,
+    every output byte (out of place: the output arena's bytes around and
+    after the packets untouched, the input arena unchanged) against the
+    oracle; clean batches commit in the in-order form, the others decline"""
+    _gpu()
+    rng = random.Random(771)
+    ssrc = 0x29400000
+    pols = [policy(name, ssrc=ssrc, seed=6)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq = 0xffff - 1200
+
+    def batch(n, tweak=None):
+        nonlocal seq
+        seqs = [(seq + k) & 0xffff for k in range(n)]
+        seq += n
+        pk = [rtp_packet(rng, ssrc, q, rng.choice((0, 7, 160, 1000)),
+                         cc=rng.choice((0, 0, 2)), xwords=rng.choice((-1, 1)))
+              for q in seqs]
+        caps = [len(p) + 32 for p in pk]
+        if tweak:
+            tweak(pk, caps)
+        return pk, caps
+
+    def dup(pk, caps):
+        pk[700] = pk[699]
+
+    def gap(pk, caps):
+        nonlocal seq
+        seq += 1
+        for k in range(900, len(pk)):
+            p = bytearray(pk[k])
+            q = ((p[2] << 8) | p[3]) + 1
+            p[2], p[3] = (q >> 8) & 0xff, q & 0xff
+            pk[k] = bytes(p)
+
+    def small(pk, caps):
+        caps[1234] = len(pk[1234]) + 3
+
+    def run(pk, caps):
+        if mode == "async":
+            st, before, after, offs = _arena_run_async(lib, pk, caps, 24, rng)
+            _check_arena(orc, pk, caps, st, before, after, offs)
+            return
+        st, bin_, ain, bout, aout, offs = _arena_run_oop(lib, pk, caps, 24, rng)
+        assert ain == bin_, "input arena changed"
+        expect = bytearray(bout)
+        for i, p in enumerate(pk):
+            rc, ref = orc.protect(p, caps[i])
+            assert st[i] == rc, (i, st[i], rc)
+            if rc == 0:
+                expect[offs[i]:offs[i] + len(ref)] = ref
+        if bytes(expect) != aout:
+            bad = next(k for k in range(len(aout)) if aout[k] != expect[k])
+            i = max(k for k in range(len(offs)) if offs[k] <= bad)
+            raise AssertionError("output byte %d differs: packet %d status %d"
+                                 % (bad, i, st[i]))
+
+    run(*batch(16))   # the fresh stream's first packets
+    r0, d0 = lib.inorder_stats()
+    for n, tw in [(3000, None), (2000, dup), (2000, gap), (2000, small),
+                  (3000, None)]:
+        run(*batch(n, tw))
+    assert lib.inorder_stats() == (r0 + 2, d0 + 3)
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_one_stream_in_order_receive_out_of_place(name):
+    """the receive side's in-order form out of place: forged tags rejected
+    (their output never holds plaintext), the rest decrypted at e_0 + i,
+    a reordered batch declined to the chain form; statuses, accepted
+    plaintexts and the unchanged input against the oracle"""
+    _gpu()
+    rng = random.Random(773)
+    ssrc = 0x29500000
+    pols = [policy(name, ssrc=ssrc, seed=7)]
+    snd, lib, orc = O.Session(pols), L.Session(pols), O.Session(pols)
+    tag = POLICIES[name][4]
+    seq = 0xffff - 900
+    r0 = d0 = None
+    for b, n in enumerate((8, 2000, 2000, 2000)):
+        pk = []
+        for k in range(n):
+            p = rtp_packet(rng, ssrc, (seq + k) & 0xffff,
+                           rng.choice((0, 7, 160, 1000)))
+            rc, ref = snd.protect(p, len(p) + 64)
+            assert rc == 0
+            pk.append(ref)
+        seq += n
+        if b >= 1:
+            for k in rng.sample(range(n), 30):
+                x = bytearray(pk[k])
+                x[-1] ^= 0x08
+                pk[k] = bytes(x)
+        if b == 3:
+            pk[400], pk[401] = pk[401], pk[400]
+        if b == 1:
+            r0, d0 = lib.inorder_stats()
+        st, bin_, ain, bout, aout, offs = _arena_run_oop(
+            lib, pk, [len(p) for p in pk], 24, rng, op="unprotect")
+        assert ain == bin_, "input arena changed"
+        for i, p in enumerate(pk):
+            rc, ref = orc.unprotect(p, len(p))
+            assert st[i] == rc, (b, i, st[i], rc)
+            o, m = offs[i], len(p) - tag
+            if rc == 0:
+                assert aout[o:o + len(ref)] == ref, (b, i)
+            else:
+                assert aout[o:o + m] in (bout[o:o + m], p[:m]), (b, i)
+    assert lib.inorder_stats() == (r0 + 2, d0 + 1)
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)
