@@ -151,6 +151,12 @@ def parse():
                     "ssrc_any_inbound receiver) instead of 64k specific "
                     "streams with distinct keys (SURVEY 8(d) configs[3] "
                     "variant); the first warmup batch creates the streams")
+    ap.add_argument("--percall", action="store_true",
+                    help="the drop-in per-call path instead: one 1400-B "
+                    "packet per srtp_protect() / srtp_unprotect() call "
+                    "(tools/percall_bench, srtp_driver.c:1202-1268's loop), "
+                    "next to the reference's per-call time on one host core")
+    ap.add_argument("--percall-calls", type=int, default=100000)
     ap.add_argument("--traffic", default="auto", choices=["auto", "off"],
                     help="auto: measure roofline.traffic and roofline.issue "
                          "with rocprofv3 PMC passes (child processes, N=1 "
@@ -693,6 +699,53 @@ def resolve_world(a):
             int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def run_percall(a, json_out):
+    """--percall: an unchanged libsrtp caller's shape -- every packet its
+    own srtp_protect() / srtp_unprotect() call, i.e. a GPU batch of one --
+    timed in C (tools/percall_bench, a child process), for AES-128-ICM +
+    HMAC-SHA1-80 and AES-256-GCM-16; the cpu_baseline leg times the
+    reference's own per-packet call on ONE host core (oracle/_ref, the
+    internal crypto kernel for AES-ICM, OpenSSL for AES-GCM)"""
+    import subprocess
+    exe = os.path.join(ROOT, "tools", "percall_bench")
+    if not os.path.exists(exe):
+        raise SystemExit("bench: tools/percall_bench not built "
+                         "(make -C libsrtp_amd percall)")
+    res, cpu = {}, {}
+    ref = os.path.join(ROOT, "oracle", "_ref")
+    for c, gcm, lib in (("icm128", False, "bench_ref_int.so"),
+                        ("gcm256", True, "bench_ref_ossl.so")):
+        note("per-call %s: %d calls per op" % (c, a.percall_calls))
+        r = subprocess.run([exe, str(a.percall_calls), "gcm" if gcm else "icm"],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode:
+            raise SystemExit("bench: percall_bench failed: " + r.stderr[-400:])
+        res[c] = json.loads(r.stdout.strip().splitlines()[-1])
+        path = os.path.join(ref, lib)
+        if a.no_cpu_baseline or not os.path.exists(path):
+            continue
+        for op in ("protect", "unprotect"):
+            note("cpu baseline per call: %s %s, 1 thread" % (c, op))
+            rr = _bounded("_ref_rate", path, op, 1400, gcm, 1, 4.0)
+            if rr:
+                cpu["%s_%s_us_per_call" % (c, op)] = 1e6 / rr[0]
+    out = {"metric": "per-call latency of srtp_protect() / srtp_unprotect(), "
+                     "one 1412-B RTP packet per call (drop-in path)",
+           "value": res["icm128"]["protect_calls_per_s"], "unit": "calls/s",
+           "higher_is_better": True, "n_gpus": 1, "dtype": "u8",
+           "data": "synthetic (one reused packet, seq advanced per call)",
+           "config": {"workload": "srtp_driver.c srtp_bits_per_second loop: "
+                      "%d calls per op, 1400-B payload" % a.percall_calls},
+           "percall": {c: {k: v for k, v in d.items()
+                           if k.endswith(("_us_per_call", "_calls_per_s"))}
+                       for c, d in res.items()},
+           "cpu_baseline": {"kind": "reference", "cores": 1,
+                            "sample": "srtp_protect()/srtp_unprotect() per "
+                                      "packet, 1400-B payload, one thread "
+                                      "(oracle/_ref)", **cpu}}
+    print(json.dumps(out), file=json_out, flush=True)
+
+
 def dry_run(a, world, rank, json_out):
     """the multi-rank orchestration without a GPU: gloo process group, a
     stub step that takes (rank + 1) ms, the same timing and JSON line"""
@@ -788,6 +841,9 @@ def main():
     os.dup2(2, 1)
     if a.dry_run:
         dry_run(a, world, rank, json_out)
+        return
+    if a.percall:
+        run_percall(a, json_out)
         return
     try:
         run_gpu(a, world, rank, local, json_out)

@@ -811,11 +811,15 @@ __global__ void k_io_commit(const uint8_t *in, const uint64_t *in_off,
 // srtp_inorder_desc), so that a declined batch has written nothing -- out of
 // place there is no input copy of the output to restore, and an
 // asynchronous caller returns on the verdict while the kernel runs
-// (k_io_publish).  One thread per packet, one atomic per wave.
-__global__ void k_io_check(const uint8_t *in, const uint64_t *in_off,
-                           const uint32_t *in_len, const uint32_t *cap,
-                           uint32_t n, const srtp_dev_stream_t *st,
-                           uint32_t *abort)
+// It writes every packet's descriptor as it goes, so the crypto kernel then
+// runs from descriptors (its in-order classification -- the header, length
+// and capacity loads -- is not repeated).  One thread per packet, one
+// atomic per wave.  (A last-block ticket in place of k_io_publish cost
+// 0.5 ms: every block's agent-scope release fence writes back L2 on gfx950.)
+__global__ __launch_bounds__(256) void k_io_check(
+    const uint8_t *in, const uint64_t *in_off, const uint32_t *in_len,
+    const uint32_t *cap, uint32_t n, const srtp_dev_stream_t *st,
+    uint32_t *abort, srtp_dev_meta_t *meta)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const srtp_dev_stream_t &S = st[0];
@@ -830,6 +834,7 @@ __global__ void k_io_check(const uint8_t *in, const uint64_t *in_off,
         srtp_dev_meta_t m;
         bad = !srtp_inorder_desc(S, h, i, len, cap[i], seq0, e0, e0ok, false,
                                  m);
+        meta[i] = m;
     }
     if (__ballot(bad) && (threadIdx.x & 63) == 0)
         atomicOr(abort, 1u);
@@ -3604,7 +3609,7 @@ static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
     const bool pre = b->in != b->out || b->in_off != b->out_off || b->async;
     if (pre) {
         hipLaunchKernelGGL(k_io_check, gp, blk, 0, stream, b->in, b->in_off,
-                           b->in_len, b->out_len, N, P->st, ab);
+                           b->in_len, b->out_len, N, P->st, ab, P->meta);
         if (b->async)
             hipLaunchKernelGGL(k_io_publish, dim3(1), dim3(64), 0, stream, ab,
                                P->h_abort_dev);
@@ -3622,14 +3627,15 @@ static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
     cb.in_off = b->in_off;
     cb.out = b->out;
     cb.out_off = b->out_off;
-    cb.meta = P->meta;   // not read
+    cb.meta = P->meta;   // checked first: k_io_check's descriptors
     cb.auth_ok = nullptr;
     cb.uniform_key = b->uniform_key;
     cb.mask = b->mask;
     cb.stream = stream;
-    // the kernel itself classifies: it always runs, unless checked first
+    // the kernel itself classifies (it always runs), unless checked first:
+    // then it runs from the descriptors, or not at all when declined
     cb.abort = pre ? ab : nullptr;
-    cb.inorder = &Q;
+    cb.inorder = pre ? nullptr : &Q;
     if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "in-order crypto"))
         return -1;
     hipLaunchKernelGGL(k_io_commit, gp, blk, 0, stream, b->in, b->in_off,

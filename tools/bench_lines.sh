@@ -10,6 +10,7 @@
 #   ktrace:<name>:<bench args> rocprofv3 kernel trace + stats -> <outdir>/kt_<name>
 #   pmc:<name>:<bench args>    SQ / HBM counter passes -> <outdir>/pmc_<name>
 #   e2e:<op>                   tools/e2e_bench (PCIe-inclusive) -> <outdir>/e2e_<op>.json
+#   percall:<calls>            bench.py --percall (one packet per call) -> <outdir>/percall.json
 # bench args use ',' for spaces: line:g711:--config,g711,--steps,10
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 out=gpurun_out/${1:?outdir}; shift
@@ -55,6 +56,11 @@ for step in "$@"; do
       timeout -k 10 300 ./tools/e2e_bench $((1<<20)) 1400 5 16 "$rest" > "$out/e2e_$rest.json" \
           2> "$out/e2e_$rest.err" || exit 1
       cat "$out/e2e_$rest.json" ;;
+    percall)
+      timeout -k 10 400 python3 bench.py --percall --percall-calls "$rest" \
+          > "$out/percall.json" 2> "$out/percall.err" ||
+          { tail -5 "$out/percall.err"; exit 1; }
+      cat "$out/percall.json" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
