@@ -201,6 +201,21 @@ typedef struct srtp_gpu_batch {
 
 int srtp_gpu_run(srtp_gpu_t *g, int op, const srtp_gpu_batch_t *b);
 
+/* The per-call path (srtp_one.hip k_one): ONE packet by one workgroup,
+ * straight from / to a pinned staging buffer.  srtp_gpu_one_buf returns the
+ * buffer's host address (SRTP_ONE_MAX bytes; NULL on allocation failure);
+ * the caller copies the packet there, srtp_gpu_one runs `op` (0 protect, 1
+ * unprotect: verify, then decrypt only an authentic packet) with the host
+ * pre-pass's descriptor and waits for the kernel's done flag; the result is
+ * in the buffer (protect: packet + MKI + tag; unprotect, *ok: plaintext).
+ * Packets up to SRTP_ONE_MAX bytes, trailer included. */
+#define SRTP_ONE_MAX 4096u
+#define SRTP_ONE_FLAG SRTP_ONE_MAX   /* offset of the verdict / done word */
+#define SRTP_ONE_TRAILER 160u        /* room for tag + MKI past the packet */
+uint8_t *srtp_gpu_one_buf(srtp_gpu_t *g);
+int srtp_gpu_one(srtp_gpu_t *g, int op, uint32_t len, const srtp_dev_meta_t *m,
+                 void *stream, int *ok);
+
 /* re-apply the keystream of the given (speculative) meta to the packets at
  * arena+off: undoes an in-place speculative decryption before a re-run */
 int srtp_gpu_undo(srtp_gpu_t *g, size_t n, uint8_t *arena,

@@ -1366,6 +1366,8 @@ void srtp_gpu_close(srtp_gpu_t *g)
     (void)hipFree(g->d_ghash);
     (void)hipFree(g->d_raw);
     (void)hipFree(g->d_undo);
+    if (g->one_h)
+        (void)hipHostFree(g->one_h);
     for (int k = 0; k < SRTP_GPU_MARKS; k++)
         if (g->marks[k])
             (void)hipEventDestroy(g->marks[k]);

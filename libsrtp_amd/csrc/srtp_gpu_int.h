@@ -36,6 +36,9 @@ struct srtp_gpu {
     size_t undo_cap;
     hipEvent_t marks[SRTP_GPU_MARKS];   // srtp_gpu_mark / _mark_wait
     hipStream_t aux[2];                 // srtp_gpu_aux_stream: copy streams
+    // srtp_gpu_one (srtp_one.hip): the pinned, mapped staging buffer of the
+    // per-call path, host and device addresses
+    uint8_t *one_h, *one_d;
 };
 
 // The order-free protect pre-pass's classification done by k_icm_hmac

@@ -2853,6 +2853,104 @@ static int batch_device_run(srtp_t ctx, int unprotect, size_t n,
     return fast;
 }
 
+/* ------------------------------------------------------------------------
+ * the per-call path: ONE packet, the host pre-pass's descriptor, the crypto
+ * by one workgroup straight from a pinned copy (srtp_one.hip k_one) -- an
+ * unchanged libsrtp caller's srtp_protect / srtp_unprotect per packet
+ * ---------------------------------------------------------------------- */
+static int one_fits(const srtp_dev_meta_t *m, size_t len)
+{
+    return SRTP_META_VARIANT(m->info) < SRTP_VARIANT_X &&
+           len + SRTP_ONE_TRAILER <= SRTP_ONE_MAX &&
+           m->len + SRTP_ONE_TRAILER <= SRTP_ONE_MAX;
+}
+
+/* the tag's verdict (protect: 1), -1 on a device error.  Protect: the
+ * protected packet (out_len bytes) to `out`; unprotect leaves the plaintext
+ * in the staging buffer (srtp_gpu_one_buf) for the caller to take once the
+ * post-pass accepted it -- a rejected packet's buffer is never written. */
+static int one_run(srtp_t ctx, int op, const uint8_t *in, size_t len,
+                   const srtp_dev_meta_t *m, uint8_t *out, size_t out_len)
+{
+    uint8_t *ob = srtp_gpu_one_buf(ctx->gpu);
+    if (!ob)
+        return -1;
+    memcpy(ob, in, len);
+    int ok = 0;
+    srtp_gpu_set_timing(ctx->gpu, 0);
+    if (srtp_gpu_one(ctx->gpu, op, (uint32_t)len, m, HS(ctx), &ok))
+        return -1;
+    if (op == 0)
+        memcpy(out, ob, out_len);
+    return ok;
+}
+
+/* srtp_unprotect of one packet (unprotect_core for n = 1: the speculative
+ * pre-pass, the crypto, the exact post-pass); 1 done, 0 not this path (a
+ * header-extension / routed stream, a packet too large), -1 device error */
+static int one_unprotect(srtp_t ctx, const uint8_t *srtp, size_t srtp_len,
+                         uint8_t *rtp, size_t *rtp_len,
+                         srtp_err_status_t *status)
+{
+    if (srtp_len + SRTP_ONE_TRAILER > SRTP_ONE_MAX)
+        return 0;
+    pkt_sum_t s;
+    summarize(srtp, srtp_len, &s);
+    s.inplace = srtp == rtp;
+    const srtp_stream_ctx_t *st = s.err ? NULL : map_get(ctx, s.ssrc);
+    if (!st)
+        st = ctx->templ;
+    const uint8_t *mki = NULL;
+    if (st) {
+        if (st->keys->k[0].variant >= SRTP_VARIANT_X)
+            return 0;
+        const hkey_t *k0 = &st->keys->k[0];
+        const size_t tl = k0->family == SRTP_DEV_GCM ? 0 : k0->tag_len;
+        if (st->use_mki && tl <= srtp_len && st->mki_size <= srtp_len - tl)
+            mki = srtp + srtp_len - tl - st->mki_size;
+    }
+    sset_t blk;
+    if (sset_init(&blk, 1)) {
+        sset_free(&blk);
+        return -1;
+    }
+    provset_t ps;
+    memset(&ps, 0, sizeof ps);
+    upkt_t u;
+    memset(&u, 0, sizeof u);
+    srtp_dev_meta_t m;
+    memset(&m, 0, sizeof m);
+    memset(&ctx->ustat, 0, sizeof ctx->ustat);
+    ctx->epoch++;
+    blk.gen++;
+    const int run = pre_unprotect(ctx, &ps, &s, *rtp_len, mki, &u, &m,
+                                  UNP_OPTIMISTIC, &blk);
+    provset_free(&ps);
+    sset_free(&blk);
+    ctx->ustat.rounds = 1;
+    size_t olen = 0;
+    if (run) {
+        ctx->ustat.launches = 1;
+        const int ok = one_run(ctx, 1, srtp, srtp_len, &m, NULL, 0);
+        if (ok < 0)
+            return -1;
+        u.gpu = 1;
+        u.auth = ok;
+        u.failed = !ok;
+        u.dirty = 0;   /* nothing reached rtp unless it authenticated */
+        u.dm = m;
+    }
+    const int rc = post_unprotect(ctx, &s, &u, &olen);
+    if (rc < 0)
+        return 0;   /* (not for one packet) nothing committed: the batch path */
+    if (rc == 0) {   /* accepted: the plaintext from the staging buffer */
+        memcpy(rtp, srtp_gpu_one_buf(ctx->gpu), olen);
+        *rtp_len = olen;
+    }
+    *status = (srtp_err_status_t)rc;
+    return 1;
+}
+
 srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
                                      const uint8_t *const *rtp,
                                      const size_t *rtp_len,
@@ -2916,6 +3014,24 @@ srtp_err_status_t srtp_protect_batch(srtp_t ctx, size_t n,
         off += r16(rtp_len[i] + SRTP_MAX_TRAILER_LEN);
     }
     srtp_err_status_t ret = srtp_err_status_ok;
+    if (n == 1 && status[0]) {   /* one packet, rejected by the pre-pass */
+        free(olen);
+        return ret;
+    }
+    if (n == 1 && one_fits(&sg->h_meta[0], rtp_len[0])) {
+        /* one packet (srtp_protect): the per-call kernel on a pinned copy */
+        const int r = one_run(ctx, 0, rtp[0], rtp_len[0], &sg->h_meta[0],
+                              srtp[0], olen[0]);
+        if (r < 0) {
+            log_msg(srtp_log_level_error, srtp_gpu_last_error());
+            status[0] = srtp_err_status_cipher_fail;
+            ret = srtp_err_status_fail;
+        } else {
+            srtp_len[0] = olen[0];
+        }
+        free(olen);
+        return ret;
+    }
     if (srtp_gpu_h2d(ctx->gpu, sg->d_arena, sg->h_arena, off, HS(ctx)) ||
         srtp_gpu_h2d(ctx->gpu, sg->d_off, sg->h_off, n * 8, HS(ctx)) ||
         run_gpu(ctx, 0, n, sg->d_arena, sg->d_off, sg->d_arena, sg->d_off,
@@ -3156,6 +3272,17 @@ srtp_err_status_t srtp_unprotect_batch(srtp_t ctx, size_t n,
     rtp_len += done;
     status += done;
     dev_pull(ctx);
+    if (n == 1) {   /* srtp_unprotect: the per-call path */
+        const int r = one_unprotect(ctx, srtp[0], srtp_len[0], rtp[0],
+                                    &rtp_len[0], &status[0]);
+        if (r < 0) {
+            log_msg(srtp_log_level_error, srtp_gpu_last_error());
+            status[0] = srtp_err_status_cipher_fail;
+            return srtp_err_status_fail;
+        }
+        if (r)
+            return srtp_err_status_ok;
+    }
     size_t arena = 0;
     for (size_t i = 0; i < n; i++)
         arena += r16(srtp_len[i]);
