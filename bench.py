@@ -74,22 +74,31 @@ CONFIGS = {
     "g711": (dict(cipher_type=1, cipher_key_len=30, auth_type=3,
                   auth_key_len=20, auth_tag_len=10, sec_serv=3), 160,
              1 << 23, 10),
+    # configs[3]'s shape under AES-256-GCM-16 (not a BASELINE config: the
+    # many-stream GCM forms, e.g. --template's one key for 64k clones)
+    "g711gcm": (dict(cipher_type=7, cipher_key_len=44, auth_type=0,
+                     auth_key_len=0, auth_tag_len=16, sec_serv=3), 160,
+                1 << 23, 16),
 }
 WORKLOAD = {
     "icm128": "AES-128-ICM + HMAC-SHA1-80 {op}, 1M packets x 1400B, 1 stream",
     "gcm256": "AES-256-GCM-16 {op}, 1M packets x 1400B per GPU, 1 stream",
     "g711": "AES-128-ICM + HMAC-SHA1-80 {op}, 8M packets x 160B, "
             "64k SSRC streams (distinct keys, round-robin)",
+    "g711gcm": "AES-256-GCM-16 {op}, 8M packets x 160B, 64k SSRC streams "
+               "(distinct keys, round-robin)",
 }
 
 
 def workload(a):
     """config.workload: the configuration and the operation timed"""
     if a.template:
-        return ("AES-128-ICM + HMAC-SHA1-80 {op}, 8M packets x 160B, 64k SSRC "
+        return ("{c} {op}, 8M packets x 160B, 64k SSRC "
                 "streams under ONE template key (ssrc_any_outbound / "
                 "_inbound; streams created on the device by the warmup's "
-                "first batch)").format(op=a.op)
+                "first batch)").format(
+                    op=a.op, c="AES-256-GCM-16" if a.config == "g711gcm"
+                    else "AES-128-ICM + HMAC-SHA1-80")
     return WORKLOAD[a.config].format(op=a.op)
 
 
@@ -97,7 +106,7 @@ def workload(a):
 TEST_KEY = ("e1f97a0d3e018be0d64fa32c06de41390ec675ad498afeebb6960b3aabe6"
             "c173c317f2dabe357793b6960b3aabe6")
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-STREAMS = {"icm128": 1, "gcm256": 1, "g711": 65536}
+STREAMS = {"icm128": 1, "gcm256": 1, "g711": 65536, "g711gcm": 65536}
 # (config, multi-GPU) -> the BASELINE.json configs[] entry the line measures
 BASELINE_CONFIG = {("icm128", False): 1, ("gcm256", False): 2,
                    ("g711", False): 3, ("gcm256", True): 4}
@@ -146,7 +155,8 @@ def parse():
                     "copy of a packet up to 64 places earlier (duplicates; "
                     "the packet they displace is lost): replay_fail")
     ap.add_argument("--template", action="store_true",
-                    help="--config g711 only: the 64k SSRCs under one "
+                    help="--config g711 / g711gcm only: the 64k SSRCs "
+                    "under one "
                     "template policy (ssrc_any_outbound sender, "
                     "ssrc_any_inbound receiver) instead of 64k specific "
                     "streams with distinct keys (SURVEY 8(d) configs[3] "
@@ -448,24 +458,26 @@ def _ref_rate_streams(lib_path, payload, nstreams, threads, cycles=1):
 
 
 def _ref_rate_template(lib_path, payload, nstreams, threads, cycles=2,
-                       op="protect"):
+                       op="protect", gcm=False):
     """the reference with ONE ssrc_any_outbound template per srtp_t and
     packets round-robin over nstreams SSRCs: the first pass clones every
     stream (srtp.c:2540-2559), later ones scan the cloned list; unprotect:
     one ssrc_any_inbound srtp_t per thread receiving a template sender's
-    packets (clones on first authentication, srtp.c:3117-3155)"""
+    packets (clones on first authentication, srtp.c:3117-3155); gcm: the
+    template policy is AES-256-GCM-16"""
     L = C.CDLL(lib_path)
-    fn = L.ref_bench_template if op == "protect" else \
-        L.ref_bench_template_unprotect
-    fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.POINTER(C.c_double)]
+    fn = L.ref_bench_template_policy
+    fn.argtypes = [C.c_int, C.c_long, C.c_int, C.c_int, C.c_int, C.c_int,
+                   C.POINTER(C.c_double)]
     secs = C.c_double()
-    done = fn(threads, cycles * nstreams, payload, nstreams, C.byref(secs))
+    done = fn(threads, cycles * nstreams, payload, nstreams,
+              int(op != "protect"), int(gcm), C.byref(secs))
     if done <= 0 or secs.value <= 0:
         return None
     return done / secs.value, done
 
 
-def cpu_baseline_template(payload, nstreams, op="protect"):
+def cpu_baseline_template(payload, nstreams, op="protect", gcm=False):
     """--template: the reference's own template path (oracle/bench_ref.c
     ref_bench_template / ref_bench_template_unprotect), both crypto
     backends, the faster one as value"""
@@ -481,7 +493,7 @@ def cpu_baseline_template(payload, nstreams, op="protect"):
         note("cpu baseline %s template path, %d SSRCs, %d threads"
              % (k, nstreams, th))
         r = _bounded("_ref_rate_template", path, payload, nstreams, th, 2, op,
-                     limit=240)
+                     gcm, limit=240)
         if r:
             res[k] = r
     if not res:
@@ -491,12 +503,13 @@ def cpu_baseline_template(payload, nstreams, op="protect"):
                "int": "built-in crypto kernel"}
     return {"value": res[mk][0], "unit": "pkt/s", "cores": th,
             "kind": "reference",
-            "sample": "%d x srtp_%s(), one ssrc_any_%s template "
+            "sample": "%d x srtp_%s(), one ssrc_any_%s %stemplate "
                       "per srtp_t, %d SSRCs round-robin (first pass clones "
                       "them), %d threads, cisco/libsrtp 3.0.0 with the %s, "
                       "built from source (oracle/Makefile.ref)"
                       % (res[mk][1], op,
                          "outbound" if op == "protect" else "inbound",
+                         "AES-256-GCM-16 " if gcm else "",
                          nstreams, th, backend[mk]),
             "backends": {"openssl": res["ossl"][0] if "ossl" in res else None,
                          "internal_kernel": res["int"][0] if "int" in res
@@ -516,7 +529,7 @@ def cpu_baseline(cfg, op, payload, seconds):
     (g711) adds `many_ssrc`: the reference with its 65,536 streams in one
     srtp_t, packets round-robin -- its own stream lookup is a linear scan
     (srtp/srtp.c:5292-5305)."""
-    gcm = cfg == "gcm256"
+    gcm = cfg in ("gcm256", "g711gcm")
     ref = os.path.join(ROOT, "oracle", "_ref")
     ossl = os.path.join(ref, "bench_ref_ossl.so")
     intk = os.path.join(ref, "bench_ref_int.so")
@@ -832,8 +845,9 @@ def main():
     if "WORLD_SIZE" not in os.environ and (a.gpus or 1) > 1:
         sys.exit(launch_ranks(a, sys.argv[1:]))
     world, rank, local = resolve_world(a)
-    if a.template and a.config != "g711":
-        raise SystemExit("bench: --template applies to --config g711")
+    if a.template and a.config not in ("g711", "g711gcm"):
+        raise SystemExit("bench: --template applies to --config g711 / "
+                         "g711gcm")
     # stdout carries exactly the one JSON line: native libraries' banners
     # (RCCL prints its version block at communicator init) go to stderr
     sys.stdout.flush()
@@ -855,7 +869,7 @@ def main():
 
 def run_gpu(a, world, rank, local, json_out):
     pol, payload, npk, tag = CONFIGS[a.config]
-    kname = "k_gcm" if a.config == "gcm256" else "k_icm_hmac"
+    kname = "k_gcm" if a.config in ("gcm256", "g711gcm") else "k_icm_hmac"
     kernels = (kname,)
     if a.config == "g711" and os.environ.get("SRTP_ICM_STG", "1") != "0":
         # configs[3]'s fused batches: the LDS-staged kernel, then the
@@ -1065,7 +1079,8 @@ def run_gpu(a, world, rank, local, json_out):
     cpu = None
     if not a.no_cpu_baseline:
         # the host cores beside rank 0's GPU, after the timed region
-        cpu = cpu_baseline_template(payload, nstreams, a.op) if a.template else \
+        cpu = cpu_baseline_template(payload, nstreams, a.op,
+                                    a.config == "g711gcm") if a.template else \
             cpu_baseline(a.config, a.op, payload, a.cpu_seconds)
     roofline = {"bound": "hbm", "achieved": achieved,
                 "peak": HBM_PEAK_GBPS, "unit": "GB/s",

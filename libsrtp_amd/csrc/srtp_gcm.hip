@@ -202,9 +202,10 @@ DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
 #endif
 constexpr int GCM_THREADS = GCM_THREADS_N;
 
-// FUSED (per-lane keys, in place): the order-free classification in the
-// kernel (srtp_fused.h; srtp_prepass.hip pp_protect_fused /
-// pp_unprotect_fused), as k_icm_hmac does it for AES-ICM
+// FUSED (in place): the order-free classification in the kernel
+// (srtp_fused.h; srtp_prepass.hip pp_protect_fused / pp_unprotect_fused), as
+// k_icm_hmac does it for AES-ICM -- with per-lane keys, or one key for every
+// stream (a template session's clones) and its LDS tables
 template <int NR, bool PROTECT, bool UNIFORM, bool FUSED = false>
 __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 {
@@ -242,9 +243,51 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
     if (UNIFORM)
         rk.load(A.keys + A.uni);
     const uint32_t stride = gridDim.x * blockDim.x;
+    FzLane z;
+    if constexpr (FUSED) {
+        z.ssrc = 0;
+        z.sid = FZ_NOCHAIN;
+        z.run_sid = FZ_NOCHAIN;
+        z.run_cnt = 0;
+        z.run_max = 0;
+        z.run_min = ~0ull;
+        z.run_cmax = 0;
+        z.bw_idx = 0;
+        z.bw_bits = 0;
+    }
+    constexpr uint32_t vid = gcm_vid<NR>();
+    // one fused packet: classified here, then sealed / opened
+    auto fused_packet = [&](uint32_t i, auto &G) {
+        // fused batches are in place: one offset
+        const uint64_t off = A.in_off[i];
+        const GlbSrc S{ A.in + off };
+        const uint32_t len = A.fz.in_len[i], cap = A.fz.cap[i];
+        if constexpr (PROTECT) {
+            const srtp_dev_meta_t m =
+                fz_classify(A, i, z, vid, off, len, cap, S);
+            gcm_packet<NR, PROTECT, UNIFORM, TAB4>(A, m, off, off, i, T, G,
+                                                   rk);
+        } else {
+            uint64_t e;
+            uint32_t sid;
+            const srtp_dev_meta_t m =
+                fzu_classify(A, i, z, vid, off, len, cap, S, e, sid);
+            gcm_packet<NR, PROTECT, UNIFORM, TAB4>(A, m, off, off, i, T, G,
+                                                   rk);
+            if (sid != FZ_NOCHAIN)
+                fzu_verdict(A, i, z, m, e, sid, A.auth_ok[i] != 0);
+        }
+    };
     if constexpr (TAB4) {
         GhPos8 G;
         G.init(lds, (uint32_t)AES_TAB4_BYTES, threadIdx.x);
+        if constexpr (FUSED) {
+            for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+                 i += stride)
+                fused_packet(i, G);
+            fz_flush<PROTECT>(A.fz, z);
+            return;
+        }
         if (A.ch.st) {
             // one stream in order (IcmChain, srtp_fused.h inorder_meta)
             const srtp_dev_stream_t S = *A.ch.st;
@@ -270,39 +313,9 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
     GhGlobal G;   // set per packet from its key
     G.g = nullptr;
     if constexpr (FUSED) {
-        FzLane z;
-        z.ssrc = 0;
-        z.sid = FZ_NOCHAIN;
-        z.run_sid = FZ_NOCHAIN;
-        z.run_cnt = 0;
-        z.run_max = 0;
-        z.run_min = ~0ull;
-        z.run_cmax = 0;
-        z.bw_idx = 0;
-        z.bw_bits = 0;
-        constexpr uint32_t vid = gcm_vid<NR>();
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
-             i += stride) {
-            // fused batches are in place: one offset
-            const uint64_t off = A.in_off[i];
-            const GlbSrc S{ A.in + off };
-            const uint32_t len = A.fz.in_len[i], cap = A.fz.cap[i];
-            if constexpr (PROTECT) {
-                const srtp_dev_meta_t m =
-                    fz_classify(A, i, z, vid, off, len, cap, S);
-                gcm_packet<NR, PROTECT, UNIFORM, false>(A, m, off, off, i, T,
-                                                        G, rk);
-            } else {
-                uint64_t e;
-                uint32_t sid;
-                const srtp_dev_meta_t m =
-                    fzu_classify(A, i, z, vid, off, len, cap, S, e, sid);
-                gcm_packet<NR, PROTECT, UNIFORM, false>(A, m, off, off, i, T,
-                                                        G, rk);
-                if (sid != FZ_NOCHAIN)
-                    fzu_verdict(A, i, z, m, e, sid, A.auth_ok[i] != 0);
-            }
-        }
+             i += stride)
+            fused_packet(i, G);
         fz_flush<PROTECT>(A.fz, z);
         return;
     }
@@ -317,13 +330,19 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 template <int NR>
 int launch_gcm_nr(const GcmArgs &A, bool prot, int ncu, hipStream_t st)
 {
-    // persistent grid: one workgroup per CU (128 KiB of tables) for uniform
+    // persistent grid: one workgroup per CU (160 KiB of tables) for uniform
     // keys, two otherwise (64 KiB)
-    const bool uni = A.uni != 0xffffffffu && !A.fused;
+    const bool uni = A.uni != 0xffffffffu;
     const size_t wgs = (A.n + GCM_THREADS - 1) / GCM_THREADS;
     const size_t cap = (size_t)ncu * (uni ? 1 : 2);
     const dim3 grid((unsigned)(wgs < cap ? wgs : cap)), block(GCM_THREADS);
-    if (A.fused && prot)
+    if (A.fused && uni && prot)
+        hipLaunchKernelGGL((k_gcm<NR, true, true, true>), grid, block, 0, st,
+                           A);
+    else if (A.fused && uni)
+        hipLaunchKernelGGL((k_gcm<NR, false, true, true>), grid, block, 0, st,
+                           A);
+    else if (A.fused && prot)
         hipLaunchKernelGGL((k_gcm<NR, true, false, true>), grid, block, 0, st,
                            A);
     else if (A.fused)

@@ -3865,13 +3865,14 @@ static int pp_run(srtp_t ctx, srtp_gpu_pp_batch_t *pb, int unprotect,
 }
 
 /* the kernel variant (one bit of a variant mask) whose kernel classifies
- * order-free batches itself: AES-ICM (variant ids 10..15, any key mode) and,
- * with a key per stream, AES-GCM (ids 18, 22: k_gcm's per-lane form) */
+ * order-free batches itself: AES-ICM (variant ids 10..15) and AES-GCM (ids
+ * 18, 22: k_gcm's per-lane form), any key mode -- one key for every stream
+ * (a template session's clones) runs the per-lane form too, its key the
+ * same in every lane */
 static int fused_variant(uint32_t mask, uint32_t uniform)
 {
-    if ((mask & 0xfc00u) == mask)
-        return 1;
-    return (mask & 0x440000u) == mask && uniform == 0xffffffffu;
+    (void)uniform;
+    return (mask & 0xfc00u) == mask || (mask & 0x440000u) == mask;
 }
 
 /* which way the one-stream in-order form went (srtp_mi355x_inorder_stats) */

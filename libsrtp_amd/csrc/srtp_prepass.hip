@@ -3962,7 +3962,9 @@ static int pp_protect_fused(srtp_gpu_t *g, PpState *P, srtp_gpu_pp_batch_t *b,
     cb.out_off = b->out_off;
     cb.meta = P->meta;
     cb.auth_ok = nullptr;
-    cb.uniform_key = 0xffffffffu;
+    // one key for every stream: k_gcm's fused form with its LDS tables
+    // (k_icm_hmac's fused form takes per-lane keys)
+    cb.uniform_key = (b->mask & 0x440000u) ? b->uniform_key : 0xffffffffu;
     cb.mask = b->mask;
     cb.stream = stream;
     cb.abort = nullptr;   // the kernel itself classifies: it always runs
@@ -4403,7 +4405,9 @@ static int pp_unprotect_fused(srtp_gpu_t *g, PpState *P,
     cb.out_off = b->out_off;
     cb.meta = P->meta;
     cb.auth_ok = P->auth;
-    cb.uniform_key = 0xffffffffu;
+    // one key for every stream: k_gcm's fused form with its LDS tables
+    // (k_icm_hmac's fused form takes per-lane keys)
+    cb.uniform_key = (b->mask & 0x440000u) ? b->uniform_key : 0xffffffffu;
     cb.mask = b->mask;
     cb.stream = stream;
     cb.abort = nullptr;   // the kernel itself classifies: it always runs

@@ -174,6 +174,7 @@ typedef struct {
     long n;
     int payload, nstreams;
     int rx;      /* run_template: time a receiver's template path instead */
+    int gcm;     /* run_template: AES-256-GCM-16 instead of the default */
     long done;
     double secs; /* protect (or unprotect) time, setup excluded */
 } sjob_t;
@@ -254,8 +255,13 @@ static void *run_template(void *arg)
     const int ns = j->nstreams;
     srtp_policy_t p;
     memset(&p, 0, sizeof p);
-    srtp_crypto_policy_set_rtp_default(&p.rtp);
-    srtp_crypto_policy_set_rtcp_default(&p.rtcp);
+    if (j->gcm) {
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(&p.rtp);
+        srtp_crypto_policy_set_aes_gcm_256_16_auth(&p.rtcp);
+    } else {
+        srtp_crypto_policy_set_rtp_default(&p.rtp);
+        srtp_crypto_policy_set_rtcp_default(&p.rtcp);
+    }
     p.ssrc.type = ssrc_any_outbound;
     p.key = (uint8_t *)key46;
     p.window_size = 128;
@@ -342,6 +348,14 @@ int ref_bench_template_unprotect(int threads, long pkts_per_thread,
                        nstreams, 1, seconds);
 }
 
+/* either direction (rx), either policy (gcm: AES-256-GCM-16) */
+int ref_bench_template_policy(int threads, long pkts_per_thread, int payload,
+                              int nstreams, int rx, int gcm, double *seconds)
+{
+    return bench_sjobs(run_template, threads, pkts_per_thread, payload,
+                       nstreams, (rx ? 1 : 0) | (gcm ? 2 : 0), seconds);
+}
+
 int ref_bench_streams(int threads, long pkts_per_thread, int payload,
                       int nstreams, double *seconds)
 {
@@ -364,7 +378,8 @@ static int bench_sjobs(void *(*fn)(void *), int threads, long pkts_per_thread,
         jobs[t].n = pkts_per_thread;
         jobs[t].payload = payload;
         jobs[t].nstreams = nstreams;
-        jobs[t].rx = rx;
+        jobs[t].rx = rx & 1;
+        jobs[t].gcm = rx >> 1 & 1;
         pthread_create(&th[t], NULL, fn, &jobs[t]);
     }
     long done = 0;

@@ -173,8 +173,9 @@ def test_template_clone_then_device_path():
         assert lib.get_roc(s) == orc.get_roc(s)
 
 
-@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
-def test_template_clones_on_device_both_directions(name):
+@pytest.mark.parametrize("fixed_stream", [True, False])
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16", "gcm128_16"])
+def test_template_clones_on_device_both_directions(name, fixed_stream):
     """Template sessions (ssrc_any_outbound sender, ssrc_any_inbound
     receiver; srtp_stream_clone srtp.c:762-863 at 2540 / 3141): the first
     batch of 300 unseen SSRCs creates every stream on the device, the
@@ -183,15 +184,18 @@ def test_template_clones_on_device_both_directions(name):
     stream known on the host (specific policy) beside them; three batches,
     every status and byte against the oracle called per packet, no batch on
     the host path, and the created streams' state visible through the host
-    API (srtp_stream_get_roc) afterwards"""
+    API (srtp_stream_get_roc) afterwards.  Without the fixed stream every
+    stream has the template's key (one key for the batch: the order-free
+    kernels' per-lane forms with one key in every lane)"""
     _gpu()
-    rng = random.Random(808 + len(name))
+    rng = random.Random(808 + len(name) + fixed_stream)
     tx = policy(name, ssrc_type=3, seed=31)
     rx = dict(tx, ssrc_type=2)
-    fixed = policy(name, ssrc=0x0f0f0f0f, seed=32)
-    snd, osnd = L.Session([tx, fixed]), O.Session([tx, fixed])
-    rcv, orcv = L.Session([rx, fixed]), O.Session([rx, fixed])
-    ssrcs = [0x31000000 + 11 * k for k in range(300)] + [0x0f0f0f0f]
+    fixed = [policy(name, ssrc=0x0f0f0f0f, seed=32)] if fixed_stream else []
+    snd, osnd = L.Session([tx] + fixed), O.Session([tx] + fixed)
+    rcv, orcv = L.Session([rx] + fixed), O.Session([rx] + fixed)
+    ssrcs = [0x31000000 + 11 * k for k in range(300)] + \
+        ([0x0f0f0f0f] if fixed_stream else [])
     seq0 = {s: rng.randrange(1, 0xf000) for s in ssrcs}
     for b in range(3):
         pk = _interleaved(rng, ssrcs, seq0, 4, payloads=(0, 20, 160))
@@ -221,7 +225,9 @@ def test_template_clones_on_device_both_directions(name):
         assert rcv.get_roc(s) == orcv.get_roc(s), hex(s)
 
 
-def test_configs3_template_bench_shape():
+@pytest.mark.parametrize("name,tag", [("icm128_hmac80", 10),
+                                      ("gcm256_16", 16)])
+def test_configs3_template_bench_shape(name, tag):
     """BASELINE configs[3]'s template variant: 65,536 SSRCs
     under ONE ssrc_any_outbound key, 128 packets x 160 B each (8M packets,
     round-robin).  The first batch creates all 65,536 streams on the device
@@ -229,16 +235,16 @@ def test_configs3_template_bench_shape():
     978 sampled SSRCs (all 64 lane positions) against the C oracle's
     template session, and every packet back through a receiver template
     session (its streams created on the device as its packets
-    authenticate)"""
+    authenticate).  Under AES-256-GCM too (bench.py --config g711gcm)"""
     _gpu()
     import numpy as np
     import torch
-    ns, per, payload, tag = 65536, 128, 160, 10
+    ns, per, payload = 65536, 128, 160
     rtp_len = 12 + payload
     slot = (rtp_len + tag + 15) & ~15
     n = ns * per
     base = 0x10000000
-    tx = policy("icm128_hmac80", ssrc_type=3, seed=77)
+    tx = policy(name, ssrc_type=3, seed=77)
     rx = dict(tx, ssrc_type=2)
     snd, rcv = L.Session([tx]), L.Session([rx])
     sample = list(range(0, ns, 67))
