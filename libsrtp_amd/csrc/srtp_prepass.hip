@@ -3638,9 +3638,13 @@ static int pp_protect_inorder_run(srtp_gpu_t *g, PpState *P,
     cb.inorder = pre ? nullptr : &Q;
     if (srtp_gpu_run(g, 0, &cb) || pp_step(stream, "in-order crypto"))
         return -1;
+    // asynchronous: k_io_publish gave the verdict and the caller returns on
+    // it, so the commit must not publish -- it may run after the NEXT call
+    // has reset the word, and would hand that call this batch's verdict
     hipLaunchKernelGGL(k_io_commit, gp, blk, 0, stream, b->in, b->in_off,
                        b->in_len, N, P->st, P->win, ab, ab_next,
-                       P->h_abort_dev, b->status, b->out_len);
+                       b->async ? nullptr : P->h_abort_dev, b->status,
+                       b->out_len);
     PPCHK(hipGetLastError());
     if (pp_step(stream, "in-order commit"))
         return -1;

@@ -2077,6 +2077,67 @@ def test_one_stream_in_order_form_out_of_place_and_async(name, mode):
 
 
 @pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
+def test_async_in_order_batches_back_to_back(name):
+    """srtp_protect_device_async batches submitted one after another with no
+    synchronize between them (a pipelined sender): a long clean batch, one
+    the in-order check declines (a duplicate: the chain form runs it), then
+    clean ones again -- each call's verdict is its own batch's, never a
+    verdict an earlier batch's kernels publish after the call began.  Every
+    status and byte against the oracle run in submission order"""
+    _gpu()
+    import torch
+    rng = random.Random(779)
+    ssrc = 0x29600000
+    pols = [policy(name, ssrc=ssrc, seed=8)]
+    lib, orc = L.Session(pols), O.Session(pols)
+    seq = 0xffff - 30000
+    plan = [(16, None), (24000, None), (2000, "dup"), (3000, None),
+            (2000, "dup"), (20000, None), (1000, None)]
+    subs = []
+    for n, tw in plan:
+        pk = [rtp_packet(rng, ssrc, (seq + k) & 0xffff,
+                         rng.choice((160, 1000, 1400)) if n > 5000 else
+                         rng.choice((0, 7, 160)))
+              for k in range(n)]
+        seq += n
+        if tw == "dup":
+            pk[n // 3] = pk[n // 3 - 1]
+        caps = [len(p) + 32 for p in pk]
+        offs, pos = [], 0
+        for p, c in zip(pk, caps):
+            offs.append(pos)
+            pos += (max(len(p), c) + 24 + 15) & ~15
+        before = bytearray(rng.randbytes(pos + 16))
+        for o, p in zip(offs, pk):
+            before[o:o + len(p)] = p
+        arena = torch.frombuffer(bytearray(before), dtype=torch.uint8).cuda()
+        t = dict(pk=pk, caps=caps, offs=offs, before=bytes(before),
+                 arena=arena,
+                 off=torch.tensor(offs, dtype=torch.int64).cuda(),
+                 ln=torch.tensor([len(p) for p in pk],
+                                 dtype=torch.int32).cuda(),
+                 cap=torch.tensor(caps, dtype=torch.int32).cuda(),
+                 st=torch.full((n,), -1, dtype=torch.int32).cuda())
+        t["b"] = lib.prepare_device(t["arena"], t["off"], t["ln"],
+                                    t["arena"], t["off"], t["cap"], t["st"])
+        subs.append(t)
+    torch.cuda.synchronize()
+    assert lib.protect_prepared_async(subs[0]["b"]) == 0   # the first packets
+    torch.cuda.synchronize()
+    r0, d0 = lib.inorder_stats()
+    for t in subs[1:]:
+        assert lib.protect_prepared_async(t["b"]) == 0
+    torch.cuda.synchronize()
+    for t in subs:
+        _check_arena(orc, t["pk"], t["caps"], t["st"].cpu().tolist(),
+                     t["before"], t["arena"].cpu().numpy().tobytes(),
+                     t["offs"])
+    assert lib.inorder_stats() == (r0 + 4, d0 + 2)
+    assert lib.get_roc(ssrc) == orc.get_roc(ssrc)
+    _key_left_equal(lib, orc, [ssrc], 1)
+
+
+@pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
 def test_one_stream_in_order_receive_out_of_place(name):
     """the receive side's in-order form out of place: forged tags rejected
     (their output never holds plaintext), the rest decrypted at e_0 + i,
