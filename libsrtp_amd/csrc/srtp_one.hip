@@ -11,8 +11,8 @@
 //   * AES-ICM / AES-GCM keystream: one CTR block per lane (aes_icm.c:236-414,
 //     the GCM counter inc32(J0) + j), XORed into the LDS image;
 //   * HMAC-SHA1 (hmac.c:157-229, sha1.c:91-463): the lanes expand every
-//     block's message schedule W[0..79] in parallel into LDS, then one lane
-//     runs the 80 rounds of each compression -- the chain is serial by
+//     block's message schedule W[0..79] + K in parallel into LDS, then one
+//     lane runs the 80 rounds of each compression -- the chain is serial by
 //     definition;
 //   * GHASH (aes_gcm_ossl.c's EVP GCM): one lane, Shoup's 8-bit table of
 //     the key copied into LDS, while another lane computes E(J0);
@@ -113,23 +113,95 @@ DEV uint32_t sha_word(const uint8_t *img, uint32_t L, uint32_t roc,
     return v;
 }
 
+// W_t + K_t, t = 0..79, of one SHA-1 block from its 16 message words
+// (sha1.c's schedule and round constants)
+DEV void sha1_wk(const uint32_t *m16, uint32_t *wk)
+{
+    uint32_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; t++)
+        w[t] = m16[t];
+#pragma unroll
+    for (int t = 0; t < 80; t++) {
+        uint32_t wt;
+        if (t < 16) {
+            wt = w[t];
+        } else {
+            wt = rotl(xor3(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^
+                          w[t & 15],
+                      1);
+            w[t & 15] = wt;
+        }
+        const uint32_t k = t < 20   ? 0x5a827999u
+                           : t < 40 ? 0x6ed9eba1u
+                           : t < 60 ? 0x8f1bbcdcu
+                                    : 0xca62c1d6u;
+        wk[t] = wt + k;
+    }
+}
+
+// x + y + z in one v_add3_u32 (left to itself the compiler splits the
+// round's sum into three adds to start it early, which a lone wave pays for
+// in issue slots)
+DEV uint32_t add3(uint32_t x, uint32_t y, uint32_t z)
+{
+    uint32_t r;
+    asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    return r;
+}
+
+// the 80 rounds of one compression from W_t + K_t (sha1_compress without
+// the schedule): five VALU per round on the chain's lane -- f as one
+// v_bitop3 (Ch = 0xCA, parity, majority), e + W_t + K_t, rotl 5, one add3,
+// rotl 30
+DEV void sha1_rounds_wk(uint32_t h[5], const u32x4 (&wk)[20])
+{
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+#pragma unroll
+    for (int t = 0; t < 80; t++) {
+        const uint32_t x = wk[t >> 2][t & 3];
+        uint32_t f;
+        if (t < 20)
+            f = __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);   // b ? c : d
+        else if (t < 40 || t >= 60)
+            f = xor3(b, c, d);
+        else
+            f = maj3(b, c, d);
+        const uint32_t tmp = add3(rotl(a, 5), f, e + x);
+        e = d;
+        d = c;
+        c = rotl(b, 30);
+        b = a;
+        a = tmp;
+    }
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+    h[4] += e;
+}
+
 // HMAC-SHA1 tag of img[0, L) || be32(roc).  The lanes build every block's
-// padded big-endian message words in LDS in parallel; thread 0 then runs
-// the chain with each block's 16 words in registers (four 16-byte LDS
-// loads, the next block's issued before the current one's compression) --
-// the 80 rounds and the rolling schedule never wait on LDS.  The digest
-// (big-endian words) in oh, thread 0 only.
+// padded big-endian message words in LDS in parallel, then every block's
+// W_t + K_t (one lane per block; the schedule depends on the message
+// only); thread 0 then runs the chain with each block's 80 words in
+// registers (twenty 16-byte LDS loads, the next block's issued before the
+// current one's rounds).  The digest (big-endian words) in oh, thread 0 only.
 DEV void one_hmac(const srtp_dev_key_t *key, const uint8_t *img, uint32_t L,
-                  uint32_t roc, uint32_t *msg, uint32_t oh[5],
+                  uint32_t roc, uint32_t *msg, uint32_t *wk, uint32_t oh[5],
                   uint8_t *prof = nullptr)
 {
     const uint32_t nb = (L + 4 + 9 + 63) / 64;
     for (uint32_t x = threadIdx.x; x < 16 * nb; x += blockDim.x)
         msg[x] = sha_word(img, L, roc, nb, x >> 4, x & 15);
     __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x)
+        sha1_wk(msg + 16 * b, wk + 80 * b);
+    __syncthreads();
     // one lane runs the chain: ~5 cycles per instruction of a lone wave,
-    // at its issue floor (the same chain on the scalar unit, rotates as two
-    // SALU shifts, took 59 against 38 us: twice the instructions)
+    // at its issue floor, so the schedule's instructions are off it (the
+    // same chain on the scalar unit, rotates as two SALU shifts, took 59
+    // against 38 us with the schedule in the chain: twice the instructions)
     if (threadIdx.x != 0)
         return;
     if (prof)
@@ -137,25 +209,25 @@ DEV void one_hmac(const srtp_dev_key_t *key, const uint8_t *img, uint32_t L,
     uint32_t h[5];
     for (int k = 0; k < 5; k++)
         h[k] = key->ipad[k];
-    const u32x4 *mv = (const u32x4 *)msg;
-    u32x4 nx[4];
+    // two register sets, A and B, alternate (no copies between blocks)
+    const u32x4 *mv = (const u32x4 *)wk;
+    u32x4 A[20], B[20];
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-        nx[q] = mv[q];
-    for (uint32_t b = 0; b < nb; b++) {
-        uint32_t w[16];
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            w[4 * q] = nx[q].x;
-            w[4 * q + 1] = nx[q].y;
-            w[4 * q + 2] = nx[q].z;
-            w[4 * q + 3] = nx[q].w;
-        }
+    for (int q = 0; q < 20; q++)
+        A[q] = mv[q];
+    for (uint32_t b = 0; b < nb; b += 2) {
         if (b + 1 < nb)
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                nx[q] = mv[4 * (b + 1) + q];
-        sha1_compress(h, w);
+            for (int q = 0; q < 20; q++)
+                B[q] = mv[20 * (b + 1) + q];
+        sha1_rounds_wk(h, A);
+        if (b + 1 >= nb)
+            break;
+        if (b + 2 < nb)
+#pragma unroll
+            for (int q = 0; q < 20; q++)
+                A[q] = mv[20 * (b + 2) + q];
+        sha1_rounds_wk(h, B);
     }
     uint32_t ow[16];
     for (int k = 0; k < 5; k++)
@@ -312,6 +384,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
     __shared__ u32x4 s_ghk[256];                     // ... and b * H^K
     __shared__ u32x4 s_pw[40];                       // H^1..K, basis, Y_r
     __shared__ uint32_t s_msg[ONE_SCHED_BLOCKS * 16];   // SHA-1 / GHASH input
+    __shared__ u32x4 s_wk[ONE_SCHED_BLOCKS * 20];      // SHA-1 W_t + K_t
     __shared__ uint32_t s_tag[5], s_ok;
     uint8_t *img = (uint8_t *)s_img;
     const srtp_dev_key_t *key = a.keys + a.m.key;
@@ -412,7 +485,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
                     img[L + u] = key->mki[u];
             if (auth) {
                 uint32_t oh[5];
-                one_hmac(key, img, L, a.m.roc, s_msg, oh,
+                one_hmac(key, img, L, a.m.roc, s_msg, (uint32_t *)s_wk, oh,
                          a.prof ? a.buf + SRTP_ONE_FLAG + 8 + 8 * 4 : nullptr);
                 ONE_STAMP(5);
                 if (tid == 0) {
@@ -426,7 +499,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
         } else {
             if (auth) {
                 uint32_t oh[5];
-                one_hmac(key, img, L, a.m.roc, s_msg, oh);
+                one_hmac(key, img, L, a.m.roc, s_msg, (uint32_t *)s_wk, oh);
                 if (tid == 0) {
                     uint32_t tw[5];
                     for (int k = 0; k < 5; k++)
