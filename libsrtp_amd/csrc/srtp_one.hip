@@ -435,6 +435,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
         }
         __syncthreads();
         ONE_STAMP(3);
+        ONE_STAMP(4);   // (GCM: no schedule phase; "chain" is the GHASH)
         {
             uint32_t x[4];
             one_ghash((lds_u32x4)s_gh, s_ghk, s_pw, img, es, P,
