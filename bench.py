@@ -392,7 +392,7 @@ def _bounded(fn, *args, limit=120):
         r = subprocess.run([sys.executable, "-c", code, json.dumps(args)],
                            capture_output=True, text=True, timeout=limit)
         return tuple(json.loads(r.stdout.strip().splitlines()[-1]))
-    except (subprocess.TimeoutExpired, ValueError, IndexError):
+    except (subprocess.TimeoutExpired, ValueError, IndexError, TypeError):
         note("cpu baseline %s%r: no result within %d s" % (fn, args, limit))
         return None
 
@@ -486,7 +486,8 @@ def cpu_baseline_template(payload, nstreams, op="protect", gcm=False):
     quota = cgroup_cpus()
     th = max(1, min(HOST_SHARE, affinity, quota or affinity))
     res = {}
-    for k in ("ossl", "int"):
+    # (the built-in crypto kernel has no AES-GCM)
+    for k in ("ossl",) if gcm else ("ossl", "int"):
         path = os.path.join(ref, "bench_ref_%s.so" % k)
         if not os.path.exists(path):
             continue
