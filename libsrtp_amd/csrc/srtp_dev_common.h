@@ -90,6 +90,20 @@ DEV uint32_t aes_t0(uint32_t x)
     return s2 | (s << 8) | (s << 16) | ((s2 ^ s) << 24);
 }
 
+// The replicated tables from the T0 row s_t0 (written and synchronised
+// before): 16-byte stores, the 4 dwords of a store 4 copies of one entry
+template <bool TAB4>
+DEV void fill_aes_tables(void *lds, const uint32_t *s_t0)
+{
+    u32x4 *d = (u32x4 *)lds;
+    constexpr int N = (TAB4 ? AES_TAB4_BYTES : AES_TAB2_BYTES) / 16;
+    for (int e = threadIdx.x; e < N; e += blockDim.x) {
+        const int tab = ((e >> 12) << 1) | ((e >> 3) & 1);
+        const uint32_t v = rotl(s_t0[(e >> 4) & 255], 8 * tab);
+        d[e] = u32x4{ v, v, v, v };
+    }
+}
+
 // Fills the replicated tables; every thread of the block must call it.  The
 // caller synchronises the block before the first lookup.
 template <bool TAB4>
@@ -98,14 +112,7 @@ DEV void load_aes_tables(void *lds, uint32_t *s_t0)   // s_t0: 1 KiB of LDS
     for (int x = threadIdx.x; x < 256; x += blockDim.x)
         s_t0[x] = aes_t0((uint32_t)x);
     __syncthreads();
-    // 16-byte stores: the 4 dwords of a store are 4 copies of one entry
-    u32x4 *d = (u32x4 *)lds;
-    constexpr int N = (TAB4 ? AES_TAB4_BYTES : AES_TAB2_BYTES) / 16;
-    for (int e = threadIdx.x; e < N; e += blockDim.x) {
-        const int tab = ((e >> 12) << 1) | ((e >> 3) & 1);
-        const uint32_t v = rotl(s_t0[(e >> 4) & 255], 8 * tab);
-        d[e] = u32x4{ v, v, v, v };
-    }
+    fill_aes_tables<TAB4>(lds, s_t0);
 }
 
 template <bool TAB4>

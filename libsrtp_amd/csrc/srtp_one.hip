@@ -14,8 +14,8 @@
 //     block's message schedule W[0..79] + K in parallel into LDS, then one
 //     lane runs the 80 rounds of each compression -- the chain is serial by
 //     definition;
-//   * GHASH (aes_gcm_ossl.c's EVP GCM): one lane, Shoup's 8-bit table of
-//     the key copied into LDS, while another lane computes E(J0);
+//   * GHASH (aes_gcm_ossl.c's EVP GCM): 8 Horner chains with H^8 over
+//     per-position tables in LDS (one_ghash), E(J0) by another lane;
 //   * unprotect verifies the tag first and decrypts only an authentic
 //     packet (srtp.c:2994-3053 before 3091-3101), so a rejected packet's
 //     bytes are never touched;
@@ -241,16 +241,6 @@ DEV void one_hmac(const srtp_dev_key_t *key, const uint8_t *img, uint32_t L,
     sha1_compress(oh, ow);
 }
 
-// Shoup's table of H in LDS, read with LDS loads (ghash_mul's TAB)
-typedef const u32x4 __attribute__((address_space(3))) *lds_u32x4;
-struct GhLds {
-    lds_u32x4 g;
-    DEV u32x4 get(uint32_t w, int k) const   // byte k of BE word w
-    {
-        return g[(w >> (24 - 8 * k)) & 0xffu];
-    }
-};
-
 // X <- X * x in GF(2^128), GCM bit order (x^0 = bit 31 of word 0)
 DEV void gf_mulx(uint32_t v[4])
 {
@@ -261,19 +251,41 @@ DEV void gf_mulx(uint32_t v[4])
     v[0] = (v[0] >> 1) ^ (c ? 0xe1000000u : 0u);
 }
 
+// LDS layout past the (T0, T1) tables: GhPos8's per-position tables need
+// bases on 32-KiB boundaries of the one LDS object they are addressed from
+constexpr uint32_t ONE_POS_H = AES_TAB2_BYTES;             // tables of H
+constexpr uint32_t ONE_POS_HK = AES_TAB2_BYTES + 32768;    // ... of H^K
+constexpr uint32_t ONE_LDS_BIG = AES_TAB2_BYTES + 65536;
+
+// GhPos8's tables from a Shoup table M: entry b of table t = M[b] * x^(8t)
+DEV void one_pos_tables(const u32x4 *M, u32x4 *dst)
+{
+    for (uint32_t b = threadIdx.x; b < 256; b += blockDim.x) {
+        u32x4 z = M[b];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            dst[b * 8 + t] = z;
+            z = ghash_mulx8(z);
+        }
+    }
+}
+
 // GHASH of the AAD img[0, A) and the ciphertext img[A, A + C), length block
 // last (gcm_packet's order): Y = sum over blocks j < n of X_j * H^(n - j).
-// One chain of n dependent multiplies is ~0.6 us each on a lone lane, so
-// the blocks go to ONE_GH_LANES chains instead: lane r takes blocks
-// j = r (mod K) by Horner with H^K -- Z_r = sum_i X_(r+iK) H^(K(m-i)) --
-// then Y_r = Z_r * H^(n - j_last) (at most K multiplies by H) and Y is the
-// XOR of the Y_r.  H^K's Shoup table is built in LDS first: lane r
-// computes H^(r+1) (r multiplies by H), then the table's 8 basis values
-// H^K * x^i and its 256 entries (XORs of them).  blk: the zero-padded
-// big-endian blocks, built by all lanes; x: BE words, thread 0 only.
+// A lone lane's multiply through Shoup's table is 16 dependent LDS reads
+// (~0.6 us); through the per-position tables of k_gcm's uniform form
+// (GhPos8) its 16 reads are independent (~0.1 us).  So: H's per-position
+// tables from its Shoup table; H^K by K - 1 multiplies on one lane; H^K's
+// Shoup table (XORs of its 8 basis values H^K * x^i) and per-position
+// tables; then ONE_GH_LANES chains -- lane r takes blocks j = r (mod K) by
+// Horner with H^K, Z_r = sum_i X_(r+iK) H^(K(m-i)), then Y_r = Z_r *
+// H^(n - j_last) (at most K multiplies by H) -- and Y is the XOR of the Y_r.
+// blk: the zero-padded big-endian blocks, built by all lanes; lds: the LDS
+// object holding the per-position tables; x: BE words, thread 0 only.
 constexpr uint32_t ONE_GH_LANES = 8;
-DEV void one_ghash(lds_u32x4 tab, u32x4 *tabk, u32x4 *pw, const uint8_t *img,
-                   uint32_t A, uint32_t C, u32x4 *blk, uint32_t x[4])
+DEV void one_ghash(const char *lds, const u32x4 *tab, u32x4 *tabk, u32x4 *pw,
+                   const uint8_t *img, uint32_t A, uint32_t C, u32x4 *blk,
+                   uint32_t x[4])
 {
     const uint32_t na = (A + 15) / 16, nc = (C + 15) / 16, n = na + nc + 1;
     for (uint32_t q = threadIdx.x; q < 4 * n; q += blockDim.x) {
@@ -291,24 +303,16 @@ DEV void one_ghash(lds_u32x4 tab, u32x4 *tabk, u32x4 *pw, const uint8_t *img,
         }
         ((uint32_t *)blk)[q] = v;
     }
-    GhLds G;
-    G.g = tab;
-    const uint32_t t = threadIdx.x, K = ONE_GH_LANES;
-    if (t < K) {   // H^(t+1)
-        uint32_t h[4] = { 0, 0, 0, 0 };
-        const u32x4 h1 = tab[0x80];   // M[0x80] = H
-        h[0] = h1.x;
-        h[1] = h1.y;
-        h[2] = h1.z;
-        h[3] = h1.w;
-        for (uint32_t k = 0; k < t; k++)
-            ghash_mul(h, G);
-        pw[t] = u32x4{ h[0], h[1], h[2], h[3] };
-    }
+    one_pos_tables(tab, (u32x4 *)(lds + ONE_POS_H));
     __syncthreads();
-    if (t == 0) {   // the basis of H^K's table: H^K * x^i, i = 0..7
-        uint32_t v[4] = { pw[K - 1].x, pw[K - 1].y, pw[K - 1].z,
-                          pw[K - 1].w };
+    const uint32_t t = threadIdx.x, K = ONE_GH_LANES;
+    GhPos8 GH;
+    GH.init(lds, ONE_POS_H, t);
+    if (t == 0) {   // H^K, then the basis of its table: H^K * x^i, i = 0..7
+        const u32x4 h1 = tab[0x80];   // M[0x80] = H
+        uint32_t v[4] = { h1.x, h1.y, h1.z, h1.w };
+        for (uint32_t k = 1; k < K; k++)
+            ghash_mul(v, GH);
         for (int i = 0; i < 8; i++) {
             pw[K + i] = u32x4{ v[0], v[1], v[2], v[3] };
             gf_mulx(v);
@@ -323,9 +327,11 @@ DEV void one_ghash(lds_u32x4 tab, u32x4 *tabk, u32x4 *pw, const uint8_t *img,
         tabk[e] = acc;
     }
     __syncthreads();
+    one_pos_tables(tabk, (u32x4 *)(lds + ONE_POS_HK));
+    __syncthreads();
     if (t < K) {
-        GhLds GK;
-        GK.g = (lds_u32x4)tabk;
+        GhPos8 GK;
+        GK.init(lds, ONE_POS_HK, t);
         uint32_t z[4] = { 0, 0, 0, 0 };
         uint32_t last = t;
         for (uint32_t j = t; j < n; j += K) {
@@ -340,7 +346,7 @@ DEV void one_ghash(lds_u32x4 tab, u32x4 *tabk, u32x4 *pw, const uint8_t *img,
         }
         if (t < n)
             for (uint32_t k = 0; k < n - last; k++)
-                ghash_mul(z, G);
+                ghash_mul(z, GH);
         else
             z[0] = z[1] = z[2] = z[3] = 0;
         pw[2 * K + 8 + t] = u32x4{ z[0], z[1], z[2], z[3] };
@@ -378,31 +384,46 @@ struct OneArgs {
 
 __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
 {
-    __shared__ u32x4 s_tab[AES_TAB2_BYTES / 16];     // (T0, T1), 64 KiB
+    // (T0, T1) 64 KiB, then GCM: the per-position GHASH tables of H and
+    // H^K (32 KiB each) / ICM: the SHA-1 W_t + K_t
+    __shared__ u32x4 s_tab[ONE_LDS_BIG / 16];
+    __shared__ uint32_t s_t0[256];                   // the T0 row
     __shared__ u32x4 s_img[SRTP_ONE_MAX / 16 + 1];   // the packet
     __shared__ u32x4 s_gh[256];                      // GCM: M[b] = b * H
     __shared__ u32x4 s_ghk[256];                     // ... and b * H^K
     __shared__ u32x4 s_pw[40];                       // H^1..K, basis, Y_r
     __shared__ uint32_t s_msg[ONE_SCHED_BLOCKS * 16];   // SHA-1 / GHASH input
-    __shared__ u32x4 s_wk[ONE_SCHED_BLOCKS * 20];      // SHA-1 W_t + K_t
     __shared__ uint32_t s_tag[5], s_ok;
     uint8_t *img = (uint8_t *)s_img;
     const srtp_dev_key_t *key = a.keys + a.m.key;
     const uint32_t tid = threadIdx.x;
     const bool gcm = key->family == SRTP_DEV_GCM;
     ONE_STAMP(0);
-    // the packet into LDS (4-byte words: buf is the staging buffer's start)
-    const uint32_t nw = (a.len + 3) / 4;
-    for (uint32_t w = tid; w < nw; w += blockDim.x)
-        ((uint32_t *)img)[w] = ((const uint32_t *)a.buf)[w];
-    if (gcm) {
-        const u32x4 *src = (const u32x4 *)(a.ghash + 1024 * key->ghash_slot);
-        for (uint32_t b = tid; b < 256; b += blockDim.x)
-            s_gh[b] = src[b];
-    }
+    // the T0 row, then the packet's words (4-byte: buf is the staging
+    // buffer's start) and GCM's Shoup table loaded into registers while the
+    // replicated tables fill, then into LDS: the PCIe / L2 latency of the
+    // loads overlaps the table build
+    for (uint32_t x = tid; x < 256; x += blockDim.x)
+        s_t0[x] = aes_t0(x);
     __syncthreads();
     ONE_STAMP(1);
-    load_aes_tables<false>(s_tab);
+    constexpr uint32_t NWT = (SRTP_ONE_MAX / 4 + ONE_THREADS - 1) / ONE_THREADS;
+    const uint32_t nw = (a.len + 3) / 4;
+    uint32_t pkw[NWT];
+#pragma unroll
+    for (uint32_t k = 0; k < NWT; k++)
+        if (tid + ONE_THREADS * k < nw)
+            pkw[k] = ((const uint32_t *)a.buf)[tid + ONE_THREADS * k];
+    u32x4 ghv = { 0, 0, 0, 0 };
+    if (gcm)
+        ghv = ((const u32x4 *)(a.ghash + 1024 * key->ghash_slot))[tid];
+    fill_aes_tables<false>(s_tab, s_t0);
+#pragma unroll
+    for (uint32_t k = 0; k < NWT; k++)
+        if (tid + ONE_THREADS * k < nw)
+            ((uint32_t *)img)[tid + ONE_THREADS * k] = pkw[k];
+    if (gcm)
+        s_gh[tid] = ghv;
     __syncthreads();
     ONE_STAMP(2);
     const AesLds T = make_aes_lds(s_tab);
@@ -438,7 +459,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
         ONE_STAMP(4);   // (GCM: no schedule phase; "chain" is the GHASH)
         {
             uint32_t x[4];
-            one_ghash((lds_u32x4)s_gh, s_ghk, s_pw, img, es, P,
+            one_ghash((const char *)s_tab, s_gh, s_ghk, s_pw, img, es, P,
                       (u32x4 *)s_msg, x);
             ONE_STAMP(5);
             if (tid == 0) {
@@ -486,7 +507,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
                     img[L + u] = key->mki[u];
             if (auth) {
                 uint32_t oh[5];
-                one_hmac(key, img, L, a.m.roc, s_msg, (uint32_t *)s_wk, oh,
+                one_hmac(key, img, L, a.m.roc, s_msg, (uint32_t *)((char *)s_tab + ONE_POS_H), oh,
                          a.prof ? a.buf + SRTP_ONE_FLAG + 8 + 8 * 4 : nullptr);
                 ONE_STAMP(5);
                 if (tid == 0) {
@@ -500,7 +521,7 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
         } else {
             if (auth) {
                 uint32_t oh[5];
-                one_hmac(key, img, L, a.m.roc, s_msg, (uint32_t *)s_wk, oh);
+                one_hmac(key, img, L, a.m.roc, s_msg, (uint32_t *)((char *)s_tab + ONE_POS_H), oh);
                 if (tid == 0) {
                     uint32_t tw[5];
                     for (int k = 0; k < 5; k++)
