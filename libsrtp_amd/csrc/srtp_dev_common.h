@@ -13,7 +13,7 @@
 //    state word -> bits 15:8, the lane's copy offset -> bits 7:0).
 //  * GHASH (GCM) uses Shoup's 8-bit table M[b] = b*H, 16 B per entry: for
 //    uniform keys as 8 per-position tables M[b]*x^(8t) in LDS (GhPos8), for
-//    per-lane keys each key's table in global memory (GhGlobal).
+//    per-lane keys each key's 4-bit table in global memory (GhNib4).
 //  * v_bitop3_b32 (gfx950) gives 3-input XOR and majority in one op.
 #pragma once
 
@@ -644,15 +644,16 @@ struct CoopPtr {
 };
 
 // ---------------------------------------------------------------------------
-// GHASH: X held as big-endian words (x^0 = bit 31 of x0).  Per-lane keys
-// read their key's Shoup 8-bit table M[b] = b * H from global memory.
-struct GhGlobal {
-    const u32x4 *g;
-    DEV u32x4 get(uint32_t w, int k) const   // byte k of BE word w
-    {
-        return g[(w >> (24 - 8 * k)) & 0xffu];
-    }
-};
+// GHASH: X held as big-endian words (x^0 = bit 31 of x0).  The device arena
+// keeps each key's Shoup 8-bit table M[b] = b * H (16 B per entry, bit 7 of
+// b = x^0) with the nibbles of the entry index swapped: entry q holds
+// M[ghash_nswap(q)].  Its first 16 entries are then M[v << 4] = v * H (bit 3
+// of v = x^0) -- the 4-bit table, 256 contiguous bytes, that the per-lane
+// form (GhNib4) reads.
+__host__ __device__ __forceinline__ uint32_t ghash_nswap(uint32_t b)
+{
+    return ((b & 15u) << 4) | (b >> 4);
+}
 
 // multiplies a GHASH value by x^8: the byte shifted out of word 3 (x^128..
 // x^135) is folded back by x^128 = 1 + x + x^2 + x^7 (as in ghash_mul)
@@ -743,6 +744,54 @@ DEV void ghash_mul(uint32_t x[4], const TAB &T)
         nz.x = (z.x >> 8) ^ mv.x;
         z = nz;
         if (k % 4 == 3 || k == 0) {
+            z.x = xor3(xor3(z.x, o, o >> 1), o >> 2, o >> 7);
+            z.y = xor3(z.y, o << 31, o << 30) ^ (o << 25);
+            o = 0;
+        }
+    }
+    x[0] = z.x;
+    x[1] = z.y;
+    x[2] = z.z;
+    x[3] = z.w;
+}
+
+// Per-lane keys: X * H by Horner over the 32 nibbles of X with the key's
+// 4-bit table (GhNib4) in global memory, 256 bytes a key.  With 64k keys
+// the 8-bit tables (4 KiB each, 256 MiB in all) missed in L2 on almost
+// every lookup (116x the algorithmic read bytes); a 4-bit table is four
+// 64-byte lines that stay cached for a packet's multiplies.  The 32 lookups
+// depend only on X, so they go out in groups of 4 ahead of the shifts; the
+// bits shifted out collect in o and fold back every 8 steps, as in
+// ghash_mul above.
+struct GhNib4 {
+    const u32x4 *t;   // the key's 16 entries v * H
+};
+
+DEV void ghash_mul(uint32_t x[4], const GhNib4 &T)
+{
+    u32x4 z = { 0, 0, 0, 0 };   // (shifting the zero start is harmless)
+    uint32_t o = 0;
+    // a rolled loop: unrolled, the 32 lookups all go out at once and the
+    // per-lane kernel (256 VGPRs already) spills
+#pragma unroll 1
+    for (int q = 7; q >= 0; q--) {   // nibbles 4q .. 4q + 3 (word q / 2)
+        const uint32_t w = q >= 6 ? x[3] : q >= 4 ? x[2] : q >= 2 ? x[1] : x[0];
+        const uint32_t hi = (q & 1) ? 0u : 16u;
+        u32x4 e[4];
+#pragma unroll
+        for (int s = 0; s < 4; s++)
+            e[s] = T.t[(w >> (hi + 12 - 4 * s)) & 15u];
+#pragma unroll
+        for (int s = 3; s >= 0; s--) {
+            o = __builtin_amdgcn_alignbit(z.w, o, 4);
+            u32x4 nz;
+            nz.w = __builtin_amdgcn_alignbit(z.z, z.w, 4) ^ e[s].w;
+            nz.z = __builtin_amdgcn_alignbit(z.y, z.z, 4) ^ e[s].z;
+            nz.y = __builtin_amdgcn_alignbit(z.x, z.y, 4) ^ e[s].y;
+            nz.x = (z.x >> 4) ^ e[s].x;
+            z = nz;
+        }
+        if ((q & 1) == 0) {   // 8 shifts since the last fold
             z.x = xor3(xor3(z.x, o, o >> 1), o >> 2, o >> 7);
             z.y = xor3(z.y, o << 31, o << 30) ^ (o << 25);
             o = 0;

@@ -20,7 +20,7 @@ namespace {
 #endif
 // uniform-key batches: the four AES tables (128 KiB) with 8 per-position
 // GHASH tables (32 KiB, GhPos8); per-lane keys: (T0, T1) and each key's
-// Shoup table in global memory
+// 4-bit table in global memory (GhNib4)
 
 DEV void load_chunk4(u32x4 (&v)[4], const uint8_t *ip)
 {
@@ -54,7 +54,7 @@ DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
     const srtp_dev_key_t *key = A.keys + slot;
     if constexpr (!UNIFORM) {
         rk.reload(A.keys, slot);
-        G.g = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
+        G.t = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
     }
 
     const uint8_t *in = A.in + in_off;
@@ -225,7 +225,7 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
         u32x4 *dst = (u32x4 *)((char *)s_tab + AES_TAB4_BYTES);
         // per-position tables: entry b of table t = M[b] * x^(8t)
         for (int b = threadIdx.x; b < 256; b += blockDim.x) {
-            u32x4 z = src[b];
+            u32x4 z = src[ghash_nswap(b)];
 #pragma unroll
             for (int t = 0; t < 8; t++) {
                 dst[b * 8 + t] = z;
@@ -310,8 +310,8 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
                                                    A.out_off[i], i, T, G, rk);
         return;
     }
-    GhGlobal G;   // set per packet from its key
-    G.g = nullptr;
+    GhNib4 G;   // set per packet from its key
+    G.t = nullptr;
     if constexpr (FUSED) {
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
              i += stride)

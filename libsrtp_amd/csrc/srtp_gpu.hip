@@ -1062,14 +1062,15 @@ DEV void kdf_prf(const ArrKey<NR> &K, const uint8_t *salt, uint32_t label,
 
 // Shoup's table M[b] = b * H of the big-endian H words v (clobbered): powers
 // by halving (v * x = v >> 1, ^ 0xe1 on carry), then sums
-// (host_crypto.c hc_ghash_table, same layout)
+// (host_crypto.c hc_ghash_table), stored in the arena's layout: M[b] at
+// entry ghash_nswap(b) (srtp_dev_common.h)
 DEV void ghash_shoup(uint32_t v[4], uint32_t *tab)
 {
     for (int w = 0; w < 4; w++)
         tab[w] = 0;
     for (uint32_t bit = 0x80; bit; bit >>= 1) {
         for (int w = 0; w < 4; w++)
-            tab[4 * bit + w] = v[w];
+            tab[4 * ghash_nswap(bit) + w] = v[w];
         const uint32_t lsb = v[3] & 1u;
         v[3] = (v[3] >> 1) | (v[2] << 31);
         v[2] = (v[2] >> 1) | (v[1] << 31);
@@ -1081,7 +1082,8 @@ DEV void ghash_shoup(uint32_t v[4], uint32_t *tab)
         if (b == low)
             continue;
         for (int w = 0; w < 4; w++)
-            tab[4 * b + w] = tab[4 * low + w] ^ tab[4 * (b ^ low) + w];
+            tab[4 * ghash_nswap(b) + w] = tab[4 * ghash_nswap(low) + w] ^
+                                          tab[4 * ghash_nswap(b ^ low) + w];
     }
 }
 
@@ -1405,12 +1407,15 @@ int srtp_gpu_set_key(srtp_gpu_t *g, uint32_t slot, const srtp_dev_key_t *k,
         return -1;
     HIPCHK(hipMemcpyAsync(g->d_keys + slot, k, sizeof *k,
                           hipMemcpyHostToDevice, g->stream));
+    uint32_t dev_tab[1024];   // the arena's layout: M[b] at ghash_nswap(b)
     if (ghash_tab) {
         if (grow((void **)&g->d_ghash, &g->ghash_cap, k->ghash_slot + 1,
                  1024 * sizeof(uint32_t)))
             return -1;
+        for (uint32_t b = 0; b < 256; b++)
+            memcpy(dev_tab + 4 * ghash_nswap(b), ghash_tab + 4 * b, 16);
         HIPCHK(hipMemcpyAsync(g->d_ghash + 1024 * (size_t)k->ghash_slot,
-                              ghash_tab, 4096, hipMemcpyHostToDevice,
+                              dev_tab, 4096, hipMemcpyHostToDevice,
                               g->stream));
     }
     HIPCHK(hipStreamSynchronize(g->stream));

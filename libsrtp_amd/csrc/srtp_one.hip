@@ -422,8 +422,8 @@ __global__ __launch_bounds__(ONE_THREADS) void k_one(OneArgs a)
     for (uint32_t k = 0; k < NWT; k++)
         if (tid + ONE_THREADS * k < nw)
             ((uint32_t *)img)[tid + ONE_THREADS * k] = pkw[k];
-    if (gcm)
-        s_gh[tid] = ghv;
+    if (gcm)   // the arena's entry tid is M[ghash_nswap(tid)]
+        s_gh[ghash_nswap(tid)] = ghv;
     __syncthreads();
     ONE_STAMP(2);
     const AesLds T = make_aes_lds(s_tab);
