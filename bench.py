@@ -181,25 +181,26 @@ def note(msg):
 
 
 def pmc_counter(path, kernels, counter):
-    """one rocprofv3 --pmc counter per step of the crypto launches: for each
-    name in `kernels` (substrings; each kernel launches once per step) the
-    mean per dispatch of the kernels whose name contains it, summed over the
-    names present in counter_collection.csv"""
+    """one rocprofv3 --pmc counter per step of the crypto launches: the
+    total over every kernel whose name contains one of `kernels`
+    (substrings) divided by the launches of the most frequent of them -- one
+    per step (k_gcm matches both launches of the key-bucket form, k_gcm_bk
+    and k_gcm; a kernel of the warmup's first batch only is spread over the
+    steps instead of counted as if it ran in each)"""
     import csv
     tot, disp = {}, {}
     with open(path) as f:
         for row in csv.DictReader(f):
             if row.get("Counter_Name", "") != counter:
                 continue
-            for k in kernels:
-                if k in row.get("Kernel_Name", ""):
-                    tot[k] = tot.get(k, 0.0) + float(row.get("Counter_Value", 0)
-                                                     or 0)
-                    disp.setdefault(k, set()).add(row.get("Dispatch_Id"))
-                    break
+            name = row.get("Kernel_Name", "")
+            if any(k in name for k in kernels):
+                tot[name] = tot.get(name, 0.0) + float(
+                    row.get("Counter_Value", 0) or 0)
+                disp.setdefault(name, set()).add(row.get("Dispatch_Id"))
     if not disp:
         return None
-    return sum(tot[k] / len(disp[k]) for k in disp)
+    return sum(tot.values()) / max(len(d) for d in disp.values())
 
 
 # PMC passes (MI355X_MICROARCH.md: one pass holds at most 4 TCC counters,

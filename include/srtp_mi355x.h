@@ -456,8 +456,11 @@ srtp_err_status_t srtp_mi355x_debug_key_left(srtp_t ctx, uint32_t ssrc,
  * the session refusing packet calls (srtp_err_status_fail). */
 /* Device pre-pass tuning (process-wide): batches with many keys are laid
  * out in key buckets so that a wave's 64 packets share one key, instead of
- * one key per lane.  Off by default (no gain measured on
- * BASELINE configs[3]); SRTP_PP_BUCKETS=1 in the environment also sets it. */
+ * one key per lane: 1 always, 0 never, -1 (the default) for AES-GCM batches
+ * with a key per stream and at least 32 packets a stream on average (the
+ * key's GHASH table then sits in LDS; DESIGN.md §4 -- AES-ICM gains nothing
+ * on BASELINE configs[3]).  SRTP_PP_BUCKETS=1 / =0 in the environment sets
+ * 1 / 0. */
 void srtp_mi355x_set_key_buckets(int on);
 
 #define SRTP_MI355X_FAIL_VERDICT_WAIT 1

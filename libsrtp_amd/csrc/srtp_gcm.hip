@@ -41,16 +41,18 @@ constexpr uint32_t gcm_vid()
     return 16u + 2u * ((NR - 8) / 2);
 }
 
-// m: the packet's descriptor; in_off / out_off its offsets
+// m: the packet's descriptor; in_off / out_off its offsets.  UNIFORM: the
+// key of slot uslot is in rk and G already (the batch's, or the wave's in
+// the bucketed form); else the packet's key is loaded here
 template <int NR, bool PROTECT, bool UNIFORM, bool TAB4, class GT, class KEY>
 DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
                     uint64_t in_off, uint64_t out_off, uint32_t i,
-                    const AesLds &T, GT G, KEY &rk)
+                    const AesLds &T, GT G, KEY &rk, uint32_t uslot)
 {
     constexpr uint32_t VID = gcm_vid<NR>();
     if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
         return;
-    const uint32_t slot = UNIFORM ? A.uni : m.key;
+    const uint32_t slot = UNIFORM ? uslot : m.key;
     const srtp_dev_key_t *key = A.keys + slot;
     if constexpr (!UNIFORM) {
         rk.reload(A.keys, slot);
@@ -266,14 +268,14 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
             const srtp_dev_meta_t m =
                 fz_classify(A, i, z, vid, off, len, cap, S);
             gcm_packet<NR, PROTECT, UNIFORM, TAB4>(A, m, off, off, i, T, G,
-                                                   rk);
+                                                   rk, A.uni);
         } else {
             uint64_t e;
             uint32_t sid;
             const srtp_dev_meta_t m =
                 fzu_classify(A, i, z, vid, off, len, cap, S, e, sid);
             gcm_packet<NR, PROTECT, UNIFORM, TAB4>(A, m, off, off, i, T, G,
-                                                   rk);
+                                                   rk, A.uni);
             if (sid != FZ_NOCHAIN)
                 fzu_verdict(A, i, z, m, e, sid, A.auth_ok[i] != 0);
         }
@@ -300,14 +302,14 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
                 const uint64_t off = A.in_off[i];
                 gcm_packet<NR, PROTECT, UNIFORM, true>(
                     A, inorder_meta<!PROTECT>(A, i, off, S, seq0, e0, e0ok),
-                    off, A.out_off[i], i, T, G, rk);
+                    off, A.out_off[i], i, T, G, rk, A.uni);
             }
             return;
         }
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
              i += stride)
             gcm_packet<NR, PROTECT, UNIFORM, true>(A, A.meta[i], A.in_off[i],
-                                                   A.out_off[i], i, T, G, rk);
+                                                   A.out_off[i], i, T, G, rk, A.uni);
         return;
     }
     GhNib4 G;   // set per packet from its key
@@ -319,10 +321,84 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
         fz_flush<PROTECT>(A.fz, z);
         return;
     }
+    if (A.rec) {   // key buckets: the records of streams with few packets
+        const uint32_t end = A.range[1];
+        for (uint32_t pos = A.range[0] + blockIdx.x * blockDim.x + threadIdx.x;
+             pos < end; pos += stride) {
+            const srtp_dev_rec_t r = A.rec[pos];
+            gcm_packet<NR, PROTECT, UNIFORM, false>(
+                A, r.meta, r.in_off, r.out_off, PROTECT ? 0u : A.rec_idx[pos],
+                T, G, rk, A.uni);
+        }
+        return;
+    }
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
          i += stride)
         gcm_packet<NR, PROTECT, UNIFORM, false>(A, A.meta[i], A.in_off[i],
-                                                A.out_off[i], i, T, G, rk);
+                                                A.out_off[i], i, T, G, rk, A.uni);
+}
+
+// Shoup's 8-bit table of one key in LDS (ghash_mul's TAB): the 16 lookups
+// of a multiply depend only on X, so they go out together
+typedef const u32x4 __attribute__((address_space(3))) *lds_u32x4;
+struct GhLdsShoup {
+    lds_u32x4 g;
+    DEV u32x4 get(uint32_t w, int k) const   // byte k of BE word w
+    {
+        return g[(w >> (24 - 8 * k)) & 0xffu];
+    }
+};
+
+// Key buckets (srtp_prepass.hip bucket_pass): the 64 records of a wave group
+// belong to one stream, so one key -- its schedule in SGPRs (UniKey) and its
+// Shoup table copied into the wave's 4 KiB of LDS, where the per-lane form
+// reads every packet's table from global memory (each of 64k keys' tables
+// evicted from L2 between a lane's multiplies).  The four AES tables as in
+// the uniform form: 128 KiB + 8 waves x 4 KiB = the 160 KiB of a CU.
+template <int NR, bool PROTECT>
+__global__ __launch_bounds__(GCM_THREADS) void k_gcm_bk(GcmArgs A)
+{
+    constexpr uint32_t WAVES = GCM_THREADS / 64;
+    __shared__ u32x4 s_tab[(AES_TAB4_BYTES + WAVES * 4096) / 16];
+    if (A.abort && *A.abort)
+        return;
+    // the S-box row of the table build sits where the GHASH tables go
+    load_aes_tables<true>(s_tab, (uint32_t *)((char *)s_tab + AES_TAB4_BYTES));
+    __syncthreads();
+    const AesLds T = make_aes_lds(s_tab);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    u32x4 *gtab = (u32x4 *)((char *)s_tab + AES_TAB4_BYTES + 4096 * wv);
+    GhLdsShoup G;
+    G.g = (lds_u32x4)gtab;
+    constexpr uint32_t vid = gcm_vid<NR>();
+    const uint32_t end = A.range[1], nw = gridDim.x * WAVES;
+    for (uint32_t g = blockIdx.x * WAVES + wv; A.range[0] + 64 * g < end;
+         g += nw) {
+        const uint32_t g0 = A.range[0] + 64 * g;
+        const uint32_t info0 =
+            __builtin_amdgcn_readfirstlane(A.rec[g0].meta.info);
+        if (SRTP_META_STATUS(info0) || SRTP_META_VARIANT(info0) != vid)
+            continue;   // an empty group, or another kernel's stream
+        const uint32_t slot =
+            __builtin_amdgcn_readfirstlane(A.rec[g0].meta.key);
+        UniKey<NR> rk;
+        rk.load(A.keys + slot);
+        // arena entry q holds M[ghash_nswap(q)]; this wave's previous group
+        // finished its reads first (a wave's LDS operations run in order)
+        const u32x4 *src =
+            (const u32x4 *)(A.ghash + 1024 * A.keys[slot].ghash_slot);
+        for (uint32_t q = lane; q < 256; q += 64)
+            gtab[ghash_nswap(q)] = src[q];
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t pos = g0 + lane;
+        if (pos < end) {
+            const srtp_dev_rec_t r = A.rec[pos];
+            gcm_packet<NR, PROTECT, true, true>(
+                A, r.meta, r.in_off, r.out_off, PROTECT ? 0u : A.rec_idx[pos],
+                T, G, rk, slot);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 }   // namespace
@@ -330,6 +406,22 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
 template <int NR>
 int launch_gcm_nr(const GcmArgs &A, bool prot, int ncu, hipStream_t st)
 {
+    if (A.rec) {
+        // key buckets: the wave-aligned groups with a key per wave, then
+        // the streams with few packets with a key per lane (their range)
+        GcmArgs L = A;
+        L.range = A.range + 2;
+        const dim3 gb((unsigned)ncu), gl((unsigned)ncu * 2), block(GCM_THREADS);
+        if (prot) {
+            hipLaunchKernelGGL((k_gcm_bk<NR, true>), gb, block, 0, st, A);
+            hipLaunchKernelGGL((k_gcm<NR, true, false>), gl, block, 0, st, L);
+        } else {
+            hipLaunchKernelGGL((k_gcm_bk<NR, false>), gb, block, 0, st, A);
+            hipLaunchKernelGGL((k_gcm<NR, false, false>), gl, block, 0, st, L);
+        }
+        HIPCHK(hipGetLastError());
+        return 0;
+    }
     // persistent grid: one workgroup per CU (160 KiB of tables) for uniform
     // keys, two otherwise (64 KiB)
     const bool uni = A.uni != 0xffffffffu;

@@ -1279,6 +1279,9 @@ static int launch_gcm(srtp_gpu_t *g, const srtp_gpu_batch_t *b, hipStream_t st)
     A.abort = b->abort;
     A.n = (uint32_t)b->n;
     A.uni = b->uniform_key;
+    A.rec = b->rec;
+    A.rec_idx = b->rec_idx;
+    A.range = b->rec_range;
     A.fused = b->fused != nullptr;
     if (A.fused)
         A.fz = *(const IcmFused *)b->fused;

@@ -149,6 +149,12 @@ struct GcmArgs {
     const uint32_t *abort;   // device pre-pass fell back: do nothing
     uint32_t n;
     uint32_t uni;
+    // key buckets (srtp_gpu_batch_t rec / rec_idx / rec_range), or null: the
+    // bucketed launch walks rec[range[0] .. range[1]) one key per wave, the
+    // per-lane one rec[range[0] .. range[1]) of its own range pointer
+    const srtp_dev_rec_t *rec;
+    const uint32_t *rec_idx;
+    const uint32_t *range;
     // order-free form classified in the kernel (per-lane keys; in place):
     // fz valid when fused, meta then neither read nor written
     bool fused;

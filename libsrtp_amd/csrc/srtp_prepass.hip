@@ -3475,22 +3475,43 @@ static int bucket_pass(PpState *P, uint32_t N, const srtp_gpu_pp_batch_t *b,
     return pp_step(stream, "buckets");
 }
 
-// Many-key batches through the key buckets: srtp_mi355x_set_key_buckets()
-// or SRTP_PP_BUCKETS=1.  Off by default: measured on configs[3] (64k streams
-// x 128 packets, round-robin) the bucketed kernel (one key per wave) took
-// 2.51 ms against 2.53 ms with a key per lane, and the bucket pass 0.39 ms
-// on top.
-static int g_buckets = -1;
+// Many-key batches through the key buckets: srtp_mi355x_set_key_buckets(1)
+// or SRTP_PP_BUCKETS=1 always, (0) / =0 never, (-1, the default) for
+// AES-GCM only.  AES-ICM: measured on configs[3] (64k streams x 128
+// packets, round-robin) the bucketed kernel (one key per wave) took 2.51 ms
+// against 2.53 ms with a key per lane, and the bucket pass 0.39 ms on top
+// (DESIGN.md §4).  AES-GCM with a key per stream: the per-lane form reads
+// each packet's GHASH table from global memory, and 64k keys' tables miss
+// in L2 (9.8 ms for configs[3]'s shape); with a key per wave (k_gcm_bk, the
+// key's table in LDS) 3.9 ms in all.  So by default a GCM batch with
+// per-stream keys and at least BK_MIN packets a stream on average -- the
+// streams that get wave buckets -- takes them.
+static int g_buckets = -2;   // -2: not read from the environment yet
 
-extern "C" void srtp_gpu_pp_set_buckets(int on) { g_buckets = on ? 1 : 0; }
-
-static bool buckets_on()
+extern "C" void srtp_gpu_pp_set_buckets(int on)
 {
-    if (g_buckets < 0) {
+    g_buckets = on < 0 ? -1 : on ? 1 : 0;
+}
+
+static int buckets_mode()
+{
+    if (g_buckets == -2) {
         const char *e = getenv("SRTP_PP_BUCKETS");
-        g_buckets = e && *e == '1';
+        g_buckets = e && *e == '1' ? 1 : e && *e == '0' ? 0 : -1;
     }
-    return g_buckets == 1;
+    return g_buckets;
+}
+
+// the key buckets for an order-free batch of N packets over ns streams
+static bool buckets_for(const srtp_gpu_pp_batch_t *b, uint32_t N, uint32_t ns)
+{
+    if (b->uniform_key != 0xffffffffu)
+        return false;
+    const int m = buckets_mode();
+    if (m >= 0)
+        return m == 1;
+    return b->mask && (b->mask & 0x440000u) == b->mask &&
+           (uint64_t)N >= (uint64_t)BK_MIN * ns;
 }
 
 static hipError_t index_scan(PpState *P, uint32_t ns, uint32_t N,
@@ -4054,7 +4075,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     }();
     bool unordered = ns > 1 && !force_sorted;
     if (unordered && b->fused_ok && !b->mki && fused_of_on() &&
-        !(b->uniform_key == 0xffffffffu && buckets_on())) {
+        !buckets_for(b, N, ns)) {
         bool sorted = false;
         if (pp_protect_fused(g, P, b, stream, fallback, &sorted))
             return -1;
@@ -4159,8 +4180,8 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     srtp_gpu_batch_t cb = {};
     // (not with MKI streams: k_mki_keys gave their packets a key each, and
     // the bucketed kernel takes one key per 64-record group)
-    if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&
-        !b->mki && bucket_pass(P, N, b, &cb, stream))
+    if (unordered && buckets_for(b, N, ns) && !b->mki &&
+        bucket_pass(P, N, b, &cb, stream))
         return -1;
     cb.n = n;
     cb.in = b->in;
@@ -4499,7 +4520,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     }
     bool unordered = ns > 1 && !force_sorted;
     if (unordered && b->fused_ok && fused_of_on() &&
-        !(b->uniform_key == 0xffffffffu && buckets_on())) {
+        !buckets_for(b, N, ns)) {
         bool sorted = false;
         if (pp_unprotect_fused(g, P, b, stream, fallback, &sorted))
             return -1;
@@ -4570,8 +4591,8 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     srtp_gpu_batch_t cb = {};
     // (not with MKI streams: their packets carry a key each, and the
     // bucketed kernel takes one key per 64-record group)
-    if (unordered && b->uniform_key == 0xffffffffu && buckets_on() &&
-        !b->mki_rx && bucket_pass(P, N, b, &cb, stream))
+    if (unordered && buckets_for(b, N, ns) && !b->mki_rx &&
+        bucket_pass(P, N, b, &cb, stream))
         return -1;
     cb.n = n;
     cb.in = b->in;

@@ -55,3 +55,25 @@ def test_traffic_counts_read_requests_at_their_size():
     assert sp["write_amplification"] == 200 * 1024 / (100 * 182)
     assert sp["fetch_size_raw"] == 70 * 1024
     assert bench.traffic_bytes({"WRITE_SIZE": 1.0}) is None
+
+
+def test_pmc_counter_sums_every_matching_kernel_per_step(tmp_path):
+    """the key-bucket GCM form launches k_gcm_bk and k_gcm each step: the
+    counter per step is both kernels' total over the steps, not the mean
+    over all their dispatches"""
+    rows = ["Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value"]
+    d = 0
+    for step in range(3):
+        for name, v in (("k_gcm_bk<14, true>(GcmArgs)", 1000.0),
+                        ("k_gcm<14, true, false, false>(GcmArgs)", 10.0),
+                        ("k_pp_classify(...)", 5.0)):
+            d += 1
+            rows.append('%d,"%s",WRITE_SIZE,%s' % (d, name, v))
+            rows.append('%d,"%s",SQ_WAVES,1' % (d, name))
+    # a kernel of the warmup's first batch only: spread over the 3 steps
+    d += 1
+    rows.append('%d,"k_gcm<14, true, false, true>(GcmArgs)",WRITE_SIZE,300' % d)
+    p = tmp_path / "counter_collection.csv"
+    p.write_text("\n".join(rows) + "\n")
+    assert bench.pmc_counter(str(p), ["k_gcm"], "WRITE_SIZE") == 1110.0
+    assert bench.pmc_counter(str(p), ["k_icm"], "WRITE_SIZE") is None

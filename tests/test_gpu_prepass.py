@@ -457,14 +457,17 @@ def test_configs3_shape_64k_distinct_key_streams():
     assert lib.prepass_sorted_batches() == 0
 
 
+@pytest.mark.parametrize("buckets", [0, 1])
 @pytest.mark.parametrize("op", ["protect", "unprotect"])
-def test_configs3_shape_64k_gcm256_streams_fused(op):
+def test_configs3_shape_64k_gcm256_streams_fused(op, buckets):
     """65,536 AES-256-GCM streams with distinct keys, packets round-robin,
     in place: the order-free form classified inside k_gcm (srtp_fused.h,
-    per-lane keys), two batches; every status and byte against the oracle
-    called once per packet (protect, or the receive side of what the
-    oracle's sender protected)"""
+    per-lane keys), or with key buckets on the pre-pass form whose streams
+    of 2-3 packets take k_gcm's per-lane record walk; two batches; every
+    status and byte against the oracle called once per packet (protect, or
+    the receive side of what the oracle's sender protected)"""
     _gpu()
+    L.lib().srtp_mi355x_set_key_buckets(buckets)
     rng = random.Random(909)
     ns = 65536
     ssrcs = [0x11000000 + k for k in range(ns)]
@@ -478,6 +481,7 @@ def test_configs3_shape_64k_gcm256_streams_fused(op):
               for i in range(ns * per)]
         _pending_run(lib, orc, snd, op, pk)
         seq0 += per
+    L.lib().srtp_mi355x_set_key_buckets(-1)
     assert lib.prepass_stats() == (2, 0), lib.prepass_last_abort()
     assert lib.prepass_sorted_batches() == 0
 
@@ -503,7 +507,9 @@ def _rr_arena(ns, per, payload, seq0, base_ssrc, gen, slot):
 
 
 @pytest.mark.parametrize("buckets", [0, 1])
-def test_configs3_bench_shape_128_per_stream(buckets):
+@pytest.mark.parametrize("name,tag", [("icm128_hmac80", 10),
+                                      ("gcm256_16", 16)])
+def test_configs3_bench_shape_128_per_stream(name, tag, buckets):
     """BASELINE configs[3] at the bench's own shape: 65,536 streams with
     distinct master keys x 128 packets x 160 B (8M packets, round-robin), so
     every stream's batch spans hi - est = 127 against its 128-bit window --
@@ -511,16 +517,18 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     the key buckets (one key per wave).  Two consecutive batches.  Every
     packet of 978 sampled streams covering all 64 lane positions (125,184
     per batch) is compared byte for byte with the C oracle in stream order; every packet of the batch
-    must come back bit-identical through srtp_unprotect_device."""
+    must come back bit-identical through srtp_unprotect_device.  Under
+    AES-256-GCM too: per-lane keys read each key's 4-bit GHASH table, the
+    buckets give a wave one key (k_gcm_bk, the key's table in LDS)."""
     _gpu()
     import numpy as np
     import torch
-    ns, per, payload, tag = 65536, 128, 160, 10
+    ns, per, payload = 65536, 128, 160
     rtp_len = 12 + payload
     slot = (rtp_len + tag + 15) & ~15
     n = ns * per
     base = 0x10000000
-    pols = [policy("icm128_hmac80", ssrc=base + k, seed=k) for k in range(ns)]
+    pols = [policy(name, ssrc=base + k, seed=k) for k in range(ns)]
     snd, rcv = L.Session(pols), L.Session(pols)
     snd.L.srtp_mi355x_set_key_buckets(buckets)
     # packet i runs on lane i mod 64 of its wave and i = k * ns + s, so
@@ -568,7 +576,7 @@ def test_configs3_bench_shape_128_per_stream(buckets):
     assert snd.prepass_stats() == (2, 0), snd.prepass_last_abort()
     assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
     assert snd.prepass_sorted_batches() == 0
-    snd.L.srtp_mi355x_set_key_buckets(0)
+    snd.L.srtp_mi355x_set_key_buckets(-1)
 
 
 def _rtp_headers(a, lens, rng):
@@ -1838,7 +1846,7 @@ def test_mki_mixed_keys_with_key_buckets(name):
         assert lib.prepass_stats() == (d0 + 2, h0)
         _key_left_equal(lib, orc, ssrcs, 3)
     finally:
-        L.lib().srtp_mi355x_set_key_buckets(0)
+        L.lib().srtp_mi355x_set_key_buckets(-1)
 
 
 @pytest.mark.parametrize("name", ["icm128_hmac80", "gcm256_16"])
