@@ -180,13 +180,31 @@ def note(msg):
     print("bench: " + msg, file=sys.stderr, flush=True)
 
 
-def pmc_counter(path, kernels, counter):
+# where each crypto kernel's PROTECT template argument sits
+_DIR_ARG = {"k_icm_hmac": 2, "k_icm_stg": 2, "k_gcm": 1, "k_gcm_bk": 1}
+
+
+def kernel_protect(name):
+    """True / False from a crypto kernel's demangled name (its PROTECT
+    template argument), None when the name carries none"""
+    import re
+    m = re.search(r"(k_icm_hmac|k_icm_stg|k_gcm_bk|k_gcm)<([^>]*)>", name)
+    if not m:
+        return None
+    args = [x.strip() for x in m.group(2).split(",")]
+    i = _DIR_ARG[m.group(1)]
+    return args[i] == "true" if i < len(args) else None
+
+
+def pmc_counter(path, kernels, counter, protect=None):
     """one rocprofv3 --pmc counter per step of the crypto launches: the
     total over every kernel whose name contains one of `kernels`
     (substrings) divided by the launches of the most frequent of them -- one
     per step (k_gcm matches both launches of the key-bucket form, k_gcm_bk
     and k_gcm; a kernel of the warmup's first batch only is spread over the
-    steps instead of counted as if it ran in each)"""
+    steps instead of counted as if it ran in each).  protect: only the
+    kernels of that direction (an unprotect run's sender protects its
+    inputs with the same kernels)"""
     import csv
     tot, disp = {}, {}
     with open(path) as f:
@@ -194,6 +212,9 @@ def pmc_counter(path, kernels, counter):
             if row.get("Counter_Name", "") != counter:
                 continue
             name = row.get("Kernel_Name", "")
+            if protect is not None and kernel_protect(name) not in (None,
+                                                                    protect):
+                continue
             if any(k in name for k in kernels):
                 tot[name] = tot.get(name, 0.0) + float(
                     row.get("Counter_Value", 0) or 0)
@@ -305,7 +326,7 @@ def measure_pmc(a, kernels, device=0):
         if not csvs:
             break
         for c in ctrs:
-            v = pmc_counter(csvs[0], kernels, c)
+            v = pmc_counter(csvs[0], kernels, c, a.op == "protect")
             if v is not None:
                 got[c] = v
     shutil.rmtree(base, ignore_errors=True)

@@ -77,3 +77,24 @@ def test_pmc_counter_sums_every_matching_kernel_per_step(tmp_path):
     p.write_text("\n".join(rows) + "\n")
     assert bench.pmc_counter(str(p), ["k_gcm"], "WRITE_SIZE") == 1110.0
     assert bench.pmc_counter(str(p), ["k_icm"], "WRITE_SIZE") is None
+
+
+def test_pmc_counter_takes_the_measured_direction(tmp_path):
+    """an unprotect run's sender protects with the same kernels: only the
+    direction measured counts (the PROTECT template argument)"""
+    assert bench.kernel_protect(
+        "void (anonymous namespace)::k_icm_hmac<10, true, false, 0, 0>"
+        "(IcmArgs)") is False
+    assert bench.kernel_protect("k_icm_stg<10, true, true>(IcmArgs)") is True
+    assert bench.kernel_protect("k_gcm<14, false, true, false>(G)") is False
+    assert bench.kernel_protect("k_gcm_bk<14, true>(GcmArgs)") is True
+    assert bench.kernel_protect("k_pp_classify(ClassifyArgs)") is None
+    rows = ["Dispatch_Id,Kernel_Name,Counter_Name,Counter_Value"]
+    for d in range(7):   # the sender's batches
+        rows.append('%d,"k_gcm_bk<14, true>(GcmArgs)",WRITE_SIZE,500' % d)
+    for d in range(7, 10):
+        rows.append('%d,"k_gcm_bk<14, false>(GcmArgs)",WRITE_SIZE,400' % d)
+    p = tmp_path / "counter_collection.csv"
+    p.write_text("\n".join(rows) + "\n")
+    assert bench.pmc_counter(str(p), ["k_gcm"], "WRITE_SIZE", False) == 400.0
+    assert bench.pmc_counter(str(p), ["k_gcm"], "WRITE_SIZE", True) == 500.0
