@@ -429,6 +429,9 @@ uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx);
  * crypto kernel, DESIGN.md "In-order form") committed / declined (restored,
  * then the chain form ran) since the session was created */
 void srtp_mi355x_inorder_stats(srtp_t ctx, uint64_t *runs, uint64_t *declines);
+/* device batches whose crypto ran from key buckets (one key per wave;
+ * srtp_mi355x_set_key_buckets) since the session was created */
+uint64_t srtp_mi355x_bucket_batches(srtp_t ctx);
 /* why the most recent srtp_protect_device fallback left the device
  * pre-pass (0: none so far): 1 unknown SSRC (template clone), 2 stream with MKI / pending ROC
  * / receiver direction, 4 sequence number not advancing by 1..2^15-1,

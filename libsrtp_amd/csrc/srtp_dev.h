@@ -336,6 +336,7 @@ typedef struct srtp_gpu_pp_batch {
     int inorder;            /* out: 1 the in-order form committed the batch,
                                2 it declined it (the chain form ran), 0 not
                                tried */
+    int bucketed;           /* out: the crypto ran from key buckets */
     const uint8_t *mki;     /* protect, HOST array: each packet's master key
                                index for the MKI streams (srtp.c:2536-2545;
                                below every MKI stream's key count: the host

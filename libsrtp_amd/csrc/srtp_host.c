@@ -197,6 +197,7 @@ typedef struct {
     uint64_t sorted_batches; /* fast batches that needed the sorted path  */
     uint64_t io_runs, io_declines; /* one-stream in-order form: batches it
                                       committed / declined (chain form ran) */
+    uint64_t bk_batches;    /* batches whose crypto ran from key buckets */
     int last_abort;         /* reason of the most recent fallback         */
     int async_pending;      /* srtp_protect_device_async left its protect
                                kernel (and the tail of its commit) queued */
@@ -3953,6 +3954,7 @@ static int protect_device_fast(srtp_t ctx, const srtp_device_batch_t *b,
         dt->last_abort = fallback;
         return 0;
     }
+    dt->bk_batches += pb.bucketed != 0;
     if (ctx->timing)
         ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
     dt->sorted_batches += pb.sorted;
@@ -4090,6 +4092,7 @@ static int unprotect_device_fast(srtp_t ctx, const srtp_device_batch_t *b)
         dt->last_abort = fallback;
         return 0;
     }
+    dt->bk_batches += pb.bucketed != 0;
     if (ctx->timing)
         ctx->last_ms = srtp_gpu_last_kernel_ms(ctx->gpu);
     dt->uses_bound += b->n;
@@ -4922,6 +4925,11 @@ srtp_err_status_t srtp_mi355x_debug_key_left(srtp_t ctx, uint32_t ssrc,
 uint64_t srtp_mi355x_prepass_sorted_batches(srtp_t ctx)
 {
     return ctx ? ctx->dt.sorted_batches : 0;
+}
+
+uint64_t srtp_mi355x_bucket_batches(srtp_t ctx)
+{
+    return ctx ? ctx->dt.bk_batches : 0;
 }
 
 void srtp_mi355x_inorder_stats(srtp_t ctx, uint64_t *runs, uint64_t *declines)

@@ -4134,6 +4134,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         if (!sorted)
             return 0;
         unordered = false;   // restored, nothing committed: the chain form
+        b->bucketed = 0;
     }
     for (;;) {
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
@@ -4232,9 +4233,11 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     srtp_gpu_batch_t cb = {};
     // (not with MKI streams: k_mki_keys gave their packets a key each, and
     // the bucketed kernel takes one key per 64-record group)
-    if (unordered && buckets_for(b, N, ns) && !b->mki &&
-        bucket_pass(P, N, b, &cb, stream))
-        return -1;
+    if (unordered && buckets_for(b, N, ns) && !b->mki) {
+        if (bucket_pass(P, N, b, &cb, stream))
+            return -1;
+        b->bucketed = 1;
+    }
     cb.n = n;
     cb.in = b->in;
     cb.in_off = b->in_off;
@@ -4268,6 +4271,7 @@ int srtp_gpu_pp_protect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
     if (unordered && *P->h_abort == AB_ORDER) {
         unordered = false;   // nothing was committed: the sorted path
+        b->bucketed = 0;
         continue;
     }
     b->sorted = !unordered;
@@ -4581,6 +4585,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
             return 0;
         }
         unordered = false;   // restored, nothing committed: the chain form
+        b->bucketed = 0;
     }
     for (;;) {
     *(volatile uint32_t *)P->h_abort = ABORT_UNSET;
@@ -4643,9 +4648,11 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
     srtp_gpu_batch_t cb = {};
     // (not with MKI streams: their packets carry a key each, and the
     // bucketed kernel takes one key per 64-record group)
-    if (unordered && buckets_for(b, N, ns) && !b->mki_rx &&
-        bucket_pass(P, N, b, &cb, stream))
-        return -1;
+    if (unordered && buckets_for(b, N, ns) && !b->mki_rx) {
+        if (bucket_pass(P, N, b, &cb, stream))
+            return -1;
+        b->bucketed = 1;
+    }
     cb.n = n;
     cb.in = b->in;
     cb.in_off = b->in_off;
@@ -4708,6 +4715,7 @@ int srtp_gpu_pp_unprotect(srtp_gpu_t *g, srtp_gpu_pp_batch_t *b,
         PPCHK(hipMemcpy(P->h_abort, P->abort, 4, hipMemcpyDeviceToHost));
     if (unordered && *P->h_abort == AB_ORDER) {
         unordered = false;   // nothing ran or changed: the chain form
+        b->bucketed = 0;
         continue;
     }
     b->sorted = !unordered;

@@ -149,6 +149,7 @@ def lib():
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_prepass_last_abort": ([P], C.c_int),
         "srtp_mi355x_prepass_sorted_batches": ([P], C.c_uint64),
+        "srtp_mi355x_bucket_batches": ([P], C.c_uint64),
         "srtp_mi355x_inorder_stats": ([P, C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)], None),
         "srtp_mi355x_debug_key_left": ([P, C.c_uint32, C.c_size_t,
@@ -564,6 +565,10 @@ class Session:
     def prepass_sorted_batches(self):
         """device pre-pass batches that needed the sorted chain path"""
         return self.L.srtp_mi355x_prepass_sorted_batches(self.h)
+
+    def bucket_batches(self):
+        """device batches whose crypto ran from key buckets"""
+        return self.L.srtp_mi355x_bucket_batches(self.h)
 
     def inorder_stats(self):
         """(batches the one-stream in-order form committed, declined)"""

@@ -486,6 +486,47 @@ def test_configs3_shape_64k_gcm256_streams_fused(op, buckets):
     assert lib.prepass_sorted_batches() == 0
 
 
+@pytest.mark.parametrize("buckets", [1, -1])
+@pytest.mark.parametrize("op", ["protect", "unprotect"])
+@pytest.mark.parametrize("ciphers", ["mixed", "gcm"])
+def test_key_buckets_both_regions_and_mixed_ciphers(ciphers, op, buckets):
+    """key buckets with both regions in one batch -- streams of 90-120
+    packets (wave buckets: k_gcm_bk / KM_WAVE) beside streams of 1-3 (the
+    per-lane record walks) -- over AES-256-GCM and AES-128-ICM streams mixed
+    (each cipher's launch skips the other's groups and records) or GCM
+    only, three batches; every status and byte against the oracle.  With
+    buckets on (1) and in the default mode (-1: the GCM-only batches, with
+    over 32 packets a stream on average, take them; the mixed ones run the
+    fused forms)"""
+    _gpu()
+    L.lib().srtp_mi355x_set_key_buckets(buckets)
+    try:
+        rng = random.Random(911 + buckets)
+        nb, nsm = (40, 900) if ciphers == "mixed" else (100, 150)
+        big = [0x12000000 + k for k in range(nb)]
+        small = [0x12100000 + k for k in range(nsm)]
+        pols = [policy("gcm256_16" if k % 2 or ciphers == "gcm"
+                       else "icm128_hmac80", ssrc=s, seed=k)
+                for k, s in enumerate(big + small)]
+        lib, orc, snd = L.Session(pols), O.Session(pols), O.Session(pols)
+        seq0 = {s: rng.randrange(1, 0xff00) for s in big + small}
+        d0, h0 = lib.prepass_stats()
+        k0 = lib.bucket_batches()
+        for b in range(3):
+            # (one step per packet in the big streams: a batch's span stays
+            # inside the 128-bit window, so the order-free form holds)
+            pk = _interleaved(rng, big, seq0, rng.randrange(90, 120),
+                              steps=(1,), payloads=(0, 20, 160, 1000))
+            pk += _interleaved(rng, small, seq0, rng.randrange(1, 4),
+                               payloads=(0, 20, 160))
+            _pending_run(lib, orc, snd, op, pk)
+        assert lib.prepass_stats() == (d0 + 3, h0), lib.prepass_last_abort()
+        bucketed = buckets == 1 or ciphers == "gcm"
+        assert lib.bucket_batches() == k0 + (3 if bucketed else 0)
+    finally:
+        L.lib().srtp_mi355x_set_key_buckets(-1)
+
+
 def _rr_arena(ns, per, payload, seq0, base_ssrc, gen, slot):
     """configs[3]-shaped arena on the GPU: ns streams round-robin, per
     packets each (packet i: stream i % ns, its packet i // ns)"""
@@ -576,6 +617,8 @@ def test_configs3_bench_shape_128_per_stream(name, tag, buckets):
     assert snd.prepass_stats() == (2, 0), snd.prepass_last_abort()
     assert rcv.prepass_stats() == (2, 0), rcv.prepass_last_abort()
     assert snd.prepass_sorted_batches() == 0
+    assert snd.bucket_batches() == (2 if buckets else 0)
+    assert rcv.bucket_batches() == (2 if buckets else 0)
     snd.L.srtp_mi355x_set_key_buckets(-1)
 
 
