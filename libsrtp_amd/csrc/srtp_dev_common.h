@@ -765,9 +765,41 @@ DEV void ghash_mul(uint32_t x[4], const TAB &T)
 // ghash_mul above.
 struct GhNib4 {
     const u32x4 *t;   // the key's 16 entries v * H
+    DEV u32x4 nib(uint32_t v) const { return t[v]; }
+    DEV void load(const uint32_t *arena, uint32_t gslot)
+    {
+        t = (const u32x4 *)(arena + 1024 * (size_t)gslot);
+    }
 };
 
-DEV void ghash_mul(uint32_t x[4], const GhNib4 &T)
+// ... copied into the lane's own 256 bytes of LDS (the per-lane k_gcm):
+// lane-private, so no barrier; entry v at (v + rot) mod 16, rot = lane mod
+// 16, so that the 16 lanes of a ds_read_b128 group asking for the same v
+// read different banks.  Copied again only when the lane's key changes.
+typedef __attribute__((address_space(3))) u32x4 *LdsQuad;
+struct GhNib4L {
+    LdsQuad t;
+    uint32_t rot;
+    uint32_t slot;   // the GHASH slot the copy holds (~0: none)
+    DEV u32x4 nib(uint32_t v) const { return t[(v + rot) & 15u]; }
+    DEV void load(const uint32_t *arena, uint32_t gslot)
+    {
+        if (gslot == slot)
+            return;
+        const u32x4 *src = (const u32x4 *)(arena + 1024 * (size_t)gslot);
+        u32x4 v[16];
+#pragma unroll
+        for (uint32_t e = 0; e < 16; e++)
+            v[e] = src[e];
+#pragma unroll
+        for (uint32_t e = 0; e < 16; e++)
+            t[(e + rot) & 15u] = v[e];
+        slot = gslot;
+    }
+};
+
+template <class NT>
+DEV void ghash_mul_nib(uint32_t x[4], const NT &T)
 {
     u32x4 z = { 0, 0, 0, 0 };   // (shifting the zero start is harmless)
     uint32_t o = 0;
@@ -780,7 +812,7 @@ DEV void ghash_mul(uint32_t x[4], const GhNib4 &T)
         u32x4 e[4];
 #pragma unroll
         for (int s = 0; s < 4; s++)
-            e[s] = T.t[(w >> (hi + 12 - 4 * s)) & 15u];
+            e[s] = T.nib((w >> (hi + 12 - 4 * s)) & 15u);
 #pragma unroll
         for (int s = 3; s >= 0; s--) {
             o = __builtin_amdgcn_alignbit(z.w, o, 4);
@@ -802,6 +834,9 @@ DEV void ghash_mul(uint32_t x[4], const GhNib4 &T)
     x[2] = z.z;
     x[3] = z.w;
 }
+
+DEV void ghash_mul(uint32_t x[4], const GhNib4 &T) { ghash_mul_nib(x, T); }
+DEV void ghash_mul(uint32_t x[4], const GhNib4L &T) { ghash_mul_nib(x, T); }
 
 DEV void ghash_mul(uint32_t x[4], const GhPos8 &T)
 {

@@ -47,7 +47,7 @@ constexpr uint32_t gcm_vid()
 template <int NR, bool PROTECT, bool UNIFORM, bool TAB4, class GT, class KEY>
 DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
                     uint64_t in_off, uint64_t out_off, uint32_t i,
-                    const AesLds &T, GT G, KEY &rk, uint32_t uslot)
+                    const AesLds &T, GT &G, KEY &rk, uint32_t uslot)
 {
     constexpr uint32_t VID = gcm_vid<NR>();
     if (SRTP_META_STATUS(m.info) || SRTP_META_VARIANT(m.info) != VID)
@@ -56,7 +56,7 @@ DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
     const srtp_dev_key_t *key = A.keys + slot;
     if constexpr (!UNIFORM) {
         rk.reload(A.keys, slot);
-        G.t = (const u32x4 *)(A.ghash + 1024 * key->ghash_slot);
+        G.load(A.ghash, key->ghash_slot);
     }
 
     const uint8_t *in = A.in + in_off;
@@ -197,24 +197,28 @@ DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
 }
 
 // Uniform keys: four AES tables + per-position GHASH tables (160 KiB, one
-// 512-lane workgroup per CU); per-lane keys: (T0, T1) (64 KiB, two per CU).
-// Persistent grid.
+// 512-lane workgroup per CU); per-lane keys: (T0, T1) (64 KiB) + each
+// lane's 4-bit GHASH table (256 B, GhNib4L), 256 lanes: one workgroup of
+// 128 KiB per CU.  Persistent grid.
 #ifndef GCM_THREADS_N
 #define GCM_THREADS_N 512
 #endif
 constexpr int GCM_THREADS = GCM_THREADS_N;
+constexpr int GCM_LANE_THREADS = 256;
 
 // FUSED (in place): the order-free classification in the kernel
 // (srtp_fused.h; srtp_prepass.hip pp_protect_fused / pp_unprotect_fused), as
 // k_icm_hmac does it for AES-ICM -- with per-lane keys, or one key for every
 // stream (a template session's clones) and its LDS tables
 template <int NR, bool PROTECT, bool UNIFORM, bool FUSED = false>
-__global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
+__global__ __launch_bounds__(UNIFORM ? GCM_THREADS : GCM_LANE_THREADS)
+void k_gcm(GcmArgs A)
 {
     constexpr bool TAB4 = UNIFORM;
     constexpr int GH8 = 256 * 16 * 8;   // the per-position GHASH tables
-    __shared__ u32x4 s_tab[(TAB4 ? AES_TAB4_BYTES + GH8 : AES_TAB2_BYTES) /
-                           16];
+    constexpr int GHL = GCM_LANE_THREADS * 256;   // the lanes' 4-bit tables
+    __shared__ u32x4 s_tab[(TAB4 ? AES_TAB4_BYTES + GH8
+                                 : AES_TAB2_BYTES + GHL) / 16];
     if (A.abort && *A.abort)
         return;
     if constexpr (TAB4) {
@@ -312,8 +316,10 @@ __global__ __launch_bounds__(GCM_THREADS) void k_gcm(GcmArgs A)
                                                    A.out_off[i], i, T, G, rk, A.uni);
         return;
     }
-    GhNib4 G;   // set per packet from its key
-    G.t = nullptr;
+    GhNib4L G;   // the lane's copy of its packet's key table
+    G.t = (LdsQuad)((char *)s_tab + AES_TAB2_BYTES + 256 * threadIdx.x);
+    G.rot = threadIdx.x & 15u;
+    G.slot = 0xffffffffu;
     if constexpr (FUSED) {
         for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
              i += stride)
@@ -411,23 +417,27 @@ int launch_gcm_nr(const GcmArgs &A, bool prot, int ncu, hipStream_t st)
         // the streams with few packets with a key per lane (their range)
         GcmArgs L = A;
         L.range = A.range + 2;
-        const dim3 gb((unsigned)ncu), gl((unsigned)ncu * 2), block(GCM_THREADS);
+        const dim3 grid((unsigned)ncu), block(GCM_THREADS),
+            lblock(GCM_LANE_THREADS);
         if (prot) {
-            hipLaunchKernelGGL((k_gcm_bk<NR, true>), gb, block, 0, st, A);
-            hipLaunchKernelGGL((k_gcm<NR, true, false>), gl, block, 0, st, L);
+            hipLaunchKernelGGL((k_gcm_bk<NR, true>), grid, block, 0, st, A);
+            hipLaunchKernelGGL((k_gcm<NR, true, false>), grid, lblock, 0, st,
+                               L);
         } else {
-            hipLaunchKernelGGL((k_gcm_bk<NR, false>), gb, block, 0, st, A);
-            hipLaunchKernelGGL((k_gcm<NR, false, false>), gl, block, 0, st, L);
+            hipLaunchKernelGGL((k_gcm_bk<NR, false>), grid, block, 0, st, A);
+            hipLaunchKernelGGL((k_gcm<NR, false, false>), grid, lblock, 0, st,
+                               L);
         }
         HIPCHK(hipGetLastError());
         return 0;
     }
-    // persistent grid: one workgroup per CU (160 KiB of tables) for uniform
-    // keys, two otherwise (64 KiB)
+    // persistent grid: one workgroup per CU (160 KiB of tables for uniform
+    // keys, 128 KiB with 256 lanes otherwise)
     const bool uni = A.uni != 0xffffffffu;
-    const size_t wgs = (A.n + GCM_THREADS - 1) / GCM_THREADS;
-    const size_t cap = (size_t)ncu * (uni ? 1 : 2);
-    const dim3 grid((unsigned)(wgs < cap ? wgs : cap)), block(GCM_THREADS);
+    const size_t bt = uni ? GCM_THREADS : GCM_LANE_THREADS;
+    const size_t wgs = (A.n + bt - 1) / bt;
+    const size_t cap = (size_t)ncu;
+    const dim3 grid((unsigned)(wgs < cap ? wgs : cap)), block((unsigned)bt);
     if (A.fused && uni && prot)
         hipLaunchKernelGGL((k_gcm<NR, true, true, true>), grid, block, 0, st,
                            A);
