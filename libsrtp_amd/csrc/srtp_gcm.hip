@@ -204,7 +204,10 @@ DEV void gcm_packet(const GcmArgs &A, const srtp_dev_meta_t &m,
 #define GCM_THREADS_N 512
 #endif
 constexpr int GCM_THREADS = GCM_THREADS_N;
-constexpr int GCM_LANE_THREADS = 256;
+#ifndef GCM_LANE_THREADS_N
+#define GCM_LANE_THREADS_N 256
+#endif
+constexpr int GCM_LANE_THREADS = GCM_LANE_THREADS_N;
 
 // FUSED (in place): the order-free classification in the kernel
 // (srtp_fused.h; srtp_prepass.hip pp_protect_fused / pp_unprotect_fused), as
@@ -239,7 +242,9 @@ void k_gcm(GcmArgs A)
             }
         }
     } else {
-        load_aes_tables<false>(s_tab);
+        // the S-box row of the table build sits where the lane tables go
+        load_aes_tables<false>(s_tab,
+                               (uint32_t *)((char *)s_tab + AES_TAB2_BYTES));
     }
     __syncthreads();
     const char *lds = (const char *)s_tab;
