@@ -488,13 +488,15 @@ def test_configs3_shape_64k_gcm256_streams_fused(op, buckets):
 
 @pytest.mark.parametrize("buckets", [1, -1])
 @pytest.mark.parametrize("op", ["protect", "unprotect"])
-@pytest.mark.parametrize("ciphers", ["mixed", "gcm"])
+@pytest.mark.parametrize("ciphers", ["mixed", "gcm", "gcm128_8"])
 def test_key_buckets_both_regions_and_mixed_ciphers(ciphers, op, buckets):
     """key buckets with both regions in one batch -- streams of 90-120
     packets (wave buckets: k_gcm_bk / KM_WAVE) beside streams of 1-3 (the
     per-lane record walks) -- over AES-256-GCM and AES-128-ICM streams mixed
     (each cipher's launch skips the other's groups and records) or GCM
-    only, three batches; every status and byte against the oracle.  With
+    only (AES-256-GCM-16, or AES-128-GCM and AES-256-GCM-8 alternating:
+    the AES-128 kernel and the 8-byte tag), three batches; every status and
+    byte against the oracle.  With
     buckets on (1) and in the default mode (-1: the GCM-only batches, with
     over 32 packets a stream on average, take them; the mixed ones run the
     fused forms)"""
@@ -505,8 +507,12 @@ def test_key_buckets_both_regions_and_mixed_ciphers(ciphers, op, buckets):
         nb, nsm = (40, 900) if ciphers == "mixed" else (100, 150)
         big = [0x12000000 + k for k in range(nb)]
         small = [0x12100000 + k for k in range(nsm)]
-        pols = [policy("gcm256_16" if k % 2 or ciphers == "gcm"
-                       else "icm128_hmac80", ssrc=s, seed=k)
+        def pname(k):
+            if ciphers == "gcm128_8":
+                return "gcm128_16" if k % 2 else "gcm256_8"
+            return "gcm256_16" if k % 2 or ciphers == "gcm" else \
+                "icm128_hmac80"
+        pols = [policy(pname(k), ssrc=s, seed=k)
                 for k, s in enumerate(big + small)]
         lib, orc, snd = L.Session(pols), O.Session(pols), O.Session(pols)
         seq0 = {s: rng.randrange(1, 0xff00) for s in big + small}
@@ -521,7 +527,7 @@ def test_key_buckets_both_regions_and_mixed_ciphers(ciphers, op, buckets):
                                payloads=(0, 20, 160))
             _pending_run(lib, orc, snd, op, pk)
         assert lib.prepass_stats() == (d0 + 3, h0), lib.prepass_last_abort()
-        bucketed = buckets == 1 or ciphers == "gcm"
+        bucketed = buckets == 1 or ciphers != "mixed"
         assert lib.bucket_batches() == k0 + (3 if bucketed else 0)
     finally:
         L.lib().srtp_mi355x_set_key_buckets(-1)
