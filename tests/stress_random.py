@@ -9,7 +9,10 @@ and unknown SSRCs on the sender side and shuffles, forgeries and replays on
 the receiver side.  Every status and byte of both sides is compared with
 the oracle called once per packet, and the streams' ROCs at the end.
 
-  python tools/stress_random.py [seconds] [first_seed]
+  python tests/stress_random.py [seconds] [first_seed]
+
+(test infrastructure, kept under tests/ with the oracle's other callers;
+not collected by pytest: a run takes minutes)
 
 Prints one line per seed and a summary; exits 1 on the first mismatch
 (with the seed, so that tests can pin it).
