@@ -1,12 +1,13 @@
 """Randomised device-path stress against the oracle (GPU box).
 
 Each seed builds a session of 1..600 streams over random policies (AES-ICM
-and AES-GCM, HMAC tags, replay windows), then runs batches through every
+and AES-GCM, HMAC tags, replay windows, MKI with several keys, or one
+ssrc_any template for all of them), then runs batches through every
 device form the library chooses among -- one stream in order (in place, out
 of place, asynchronous back to back), the order-free and sorted forms, key
 buckets forced on / off / by default -- with reordering, duplicates, jumps
-and unknown SSRCs on the sender side and shuffles, forgeries and replays on
-the receiver side.  Every status and byte of both sides is compared with
+and unknown SSRCs and application-set ROCs on the sender side and shuffles,
+forgeries and replays on the receiver side.  Every status and byte of both sides is compared with
 the oracle called once per packet, and the streams' ROCs at the end.
 
   python tests/stress_random.py [seconds] [first_seed]
@@ -79,12 +80,26 @@ def run_seed(seed):
     pols = [policy(c0 if one_cipher else rng.choice(POLS), ssrc=s, seed=k,
                    window=rng.choice([64, 128, 128, 1024]), **mkw)
             for k, s in enumerate(ssrcs)]
-    slib, sorc = L.Session(pols), O.Session(pols)
-    rlib, rorc = L.Session(pols), O.Session(pols)
+    spols = rpols = pols
+    templ = not nkeys and ns > 1 and rng.random() < 0.2
+    if templ:
+        # one ssrc_any_outbound / _inbound template for every stream: the
+        # streams are created on the device (srtp_stream_clone)
+        tp = policy(c0, ssrc_type=3, seed=5)
+        spols, rpols = [tp], [dict(tp, ssrc_type=2)]
+    slib, sorc = L.Session(spols), O.Session(spols)
+    rlib, rorc = L.Session(rpols), O.Session(rpols)
     seq0 = {s: rng.randrange(1, 0xffff) for s in ssrcs}
     what = []
     for b in range(6):
         L.lib().srtp_mi355x_set_key_buckets(rng.choice([-1, -1, 0, 1]))
+        if b and not templ and rng.random() < 0.25:
+            # an application-set ROC (srtp_stream_set_roc, srtp.c:5137-5167)
+            # on a sender stream: ahead, or the current one (pending)
+            s = rng.choice(ssrcs)
+            roc = sorc.get_roc(s)[1] + rng.choice([0, 1])
+            assert slib.set_roc(s, roc) == 0 and sorc.set_roc(s, roc) == 0
+            what.append("roc")
         per = rng.choice([1, 5, 40, 150]) if ns > 1 else \
             rng.choice([20, 700, 3000])
         clean = ns == 1 and rng.random() < 0.6
@@ -181,8 +196,8 @@ def run_seed(seed):
             assert st[i] == rc, ("rx", b, i, st[i], rc)
             assert rc or out[i] == ref, ("rx", b, i)
     for s in ssrcs:
-        assert slib.get_roc(s)[1] == sorc.get_roc(s)[1], hex(s)
-        assert rlib.get_roc(s)[1] == rorc.get_roc(s)[1], hex(s)
+        assert slib.get_roc(s) == sorc.get_roc(s), hex(s)
+        assert rlib.get_roc(s) == rorc.get_roc(s), hex(s)
     L.lib().srtp_mi355x_set_key_buckets(-1)
     return ns, what
 
