@@ -119,8 +119,11 @@ def run_seed(seed):
             s = rng.choice(ssrcs)
             seq0[s] += rng.randrange(100, 20000)
         caps = [len(p) + rng.choice([16, 16, 40]) for p in pk]
-        mode = rng.choice(["inplace", "inplace", "oop", "async"])
-        if nkeys:
+        mode = rng.choice(["inplace", "inplace", "oop", "async", "host",
+                           "single"])
+        if mode == "single" and len(pk) > 400:
+            mode = "host"
+        if nkeys and mode not in ("host", "single"):
             mode = "mki"
         what.append("%s/%d/%s/%s" % (mode, len(pk), event,
                                      "clean" if clean else "mixed"))
@@ -142,6 +145,26 @@ def run_seed(seed):
                         expect[offs[i]:offs[i] + len(ref)] = ref
                         sent.append(ref)
                 assert bytes(expect) == after, ("async arena", b)
+        elif mode in ("host", "single"):
+            # the host-buffer batch API (srtp_protect_batch: staged into HBM,
+            # the device pre-pass) or one srtp_protect per packet (k_one)
+            mk = [rng.randrange(nkeys) for _ in pk] if nkeys else [0] * len(pk)
+            if mode == "host":
+                st, out = slib.protect_batch(pk, caps, mki=mk,
+                                             inplace=rng.random() < 0.5)
+            else:
+                st, out = [], []
+                for i, p in enumerate(pk):
+                    rc, o = slib.protect(p, caps[i], mk[i],
+                                         inplace=rng.random() < 0.5)
+                    st.append(rc)
+                    out.append(o)
+            for i, p in enumerate(pk):
+                rc, ref = sorc.protect(p, caps[i], mk[i])
+                assert st[i] == rc, (mode, b, event, i, st[i], rc)
+                assert rc or out[i] == ref, (mode, b, event, i)
+                if rc == 0:
+                    sent.append(ref)
         elif mode == "mki":
             mk = [rng.randrange(nkeys) for _ in pk]
             st, out = _device_run(slib, pk, caps, "protect", mki=mk)
@@ -179,6 +202,19 @@ def run_seed(seed):
         if rx and rng.random() < 0.3:
             rx.append(rx[rng.randrange(len(rx))])
         if not rx:
+            continue
+        rmode = rng.random()
+        if rmode < 0.15 or (rmode < 0.25 and len(rx) <= 400):
+            # the host-buffer batch API, or one srtp_unprotect per packet
+            if rmode < 0.15:
+                st, out = rlib.unprotect_batch(rx, inplace=rng.random() < 0.5)
+            else:
+                st, out = zip(*[rlib.unprotect(p, inplace=rng.random() < 0.5)
+                                for p in rx])
+            for i, p in enumerate(rx):
+                rc, ref = rorc.unprotect(p, len(p))
+                assert st[i] == rc, ("rx host", b, i, st[i], rc)
+                assert rc or out[i] == ref, ("rx host", b, i)
             continue
         if rng.random() < 0.3:   # out of place: the input arena untouched
             st, bin_, ain, bout, aout, offs = _arena_run_oop(
