@@ -108,6 +108,14 @@ def run_seed(seed):
                           rng.choice([0, 0, 0.1]),
                           steps=(1,) if clean else (1, 1, 1, 2),
                           payloads=(0, 1, 13, 160, 300, 1000))
+        if rng.random() < 0.3:
+            # headers with CSRCs and extensions (the payload's offset and the
+            # keystream phase vary per packet); sequence numbers kept
+            pk = [rtp_packet(rng, int.from_bytes(p[8:12], "big"),
+                             (p[2] << 8) | p[3], len(p) - 12,
+                             cc=rng.choice([0, 0, 1, 3]),
+                             xwords=rng.choice([-1, -1, 0, 2]))
+                  for p in pk]
         event = "none" if clean else rng.choice(["none", "none", "dup",
                                                  "unknown", "jump"])
         if event == "dup" and len(pk) > 10:
